@@ -1,0 +1,313 @@
+#!/usr/bin/env python3
+"""bench.py -- fused dequant + IDCT + upsample + colour kernel on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload 4k420|4k444|fhd420]
+    (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+
+Workload (BASELINE.json configs[2], default): a batch of 1024 synthetic
+3840x2160 4:2:0 frames resident in HBM as int16 quantised zigzag coefficients
+(+ qtables); one step = ONE persistent-kernel launch decoding all 1024 frames to
+BGRX in HBM.  Synthetic content: a pool of distinct frames (FDCT + quantisation
+of smooth+noise blocks, generated on the device) replicated to 1024 frames.
+Multi-GPU: every rank decodes its own 1024-frame batch (image-parallel shards,
+no collective on the data path; weak scaling); value = all ranks' pixels /
+max-over-ranks time.
+
+Printed JSON line fields beyond the driver contract:
+  roofline      achieved GB/s = algorithmic bytes per launch (int16 coefs in +
+                BGRX out, 7 B/px at 4:2:0, 10 B/px at 4:4:4) / mean launch time
+                measured with HIP events on the launch stream; peak 8.0 TB/s.
+                traffic = per-launch HBM bytes from the committed rocprofv3 PMC
+                summary (profiles/*pmc*.json), or null.
+  cpu_baseline  the bit-exact C restatement (oracle/) on a thread pool over the
+                host cores, one frame per task, bounded sample (rank 0, N=1);
+                cpu_reference = the reference's own decode_mcu_data
+                (oracle/_ref/libref.so, 1 thread) when that library is present.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import glob
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+WORKLOADS = {
+    "4k420": dict(width=3840, height=2160, sampling=1, frames=1024,
+                  desc="BASELINE configs[2]: batch of 1024 synthetic 3840x2160 4:2:0 frames, persistent kernel"),
+    "4k444": dict(width=3840, height=2160, sampling=0, frames=1024,
+                  desc="BASELINE configs[3]: batch of 1024 synthetic 3840x2160 4:4:4 frames, persistent kernel"),
+    "fhd420": dict(width=1920, height=1080, sampling=1, frames=1,
+                   desc="BASELINE configs[1]: single 1920x1080 4:2:0 frame, one launch (cache/launch bound)"),
+}
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+POOL = 8
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def std_qtables(scale=1.0):
+    lum = np.array([16, 11, 10, 16, 24, 40, 51, 61, 12, 12, 14, 19, 26, 58, 60, 55,
+                    14, 13, 16, 24, 40, 57, 69, 56, 14, 17, 22, 29, 51, 87, 80, 62,
+                    18, 22, 37, 56, 68, 109, 103, 77, 24, 35, 55, 64, 81, 104, 113, 92,
+                    49, 64, 78, 87, 103, 121, 120, 101, 72, 92, 95, 98, 112, 100, 103, 99])
+    chr_ = np.array([17, 18, 24, 47, 99, 99, 99, 99, 18, 21, 26, 66, 99, 99, 99, 99,
+                     24, 26, 56, 99, 99, 99, 99, 99, 47, 66, 99, 99, 99, 99, 99, 99] + [99] * 32)
+    nat = np.stack([lum, chr_, chr_])
+    return np.clip(np.rint(nat[:, ZIGZAG] * scale), 1, 255).astype(np.int32)
+
+
+ZIGZAG = [0, 1, 8, 16, 9, 2, 3, 10, 17, 24, 32, 25, 18, 11, 4, 5,
+          12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6, 7, 14, 21, 28,
+          35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+          58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63]
+
+
+def synth_frame_gpu(torch, nblk, bpm, qt, seed, device):
+    """Synthetic quantised zigzag coefficients for one frame, on the device:
+    smooth+noise 8x8 sample blocks in [-128,127] -> float FDCT -> quantise
+    (q=90-like tables).  Bounded samples keep the data in the reference's legal
+    domain.  This is input generation, outside every timed region."""
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    k = torch.arange(8, device=device, dtype=torch.float32)
+    cc = torch.where(k == 0, 1 / np.sqrt(2), 1.0)
+    m = torch.cos((2 * k[None, :] + 1) * k[:, None] * np.pi / 16) * cc[:, None] / 2
+    yy, xx = torch.meshgrid(torch.arange(8, device=device), torch.arange(8, device=device), indexing="ij")
+    base = torch.randint(-100, 100, (nblk, 1, 1), generator=g, device=device).float()
+    grad = torch.randn((nblk, 2, 1, 1), generator=g, device=device) * 6
+    pix = base + grad[:, 0] * yy + grad[:, 1] * xx + torch.randn((nblk, 8, 8), generator=g, device=device) * 20
+    pix = pix.clamp(-128, 127)
+    F = torch.einsum("ux,nxy,vy->nuv", m, pix, m).reshape(nblk, 64)
+    qnat = torch.zeros((3, 64), device=device)
+    qnat[:, torch.tensor(ZIGZAG, device=device)] = torch.from_numpy(qt).float().to(device)
+    comp = torch.tensor([0] * (bpm - 2) + [1, 2], device=device).repeat(nblk // bpm)
+    coef_nat = torch.round(F / qnat[comp])
+    return coef_nat[:, torch.tensor(ZIGZAG, device=device)].to(torch.int16).contiguous()
+
+
+def cpu_baseline(coef_pool_host, qt, wl, frames_done_gpu_rate):
+    """CPU leg (rank 0, N=1): oracle C restatement on a pthread pool over the
+    host cores, bounded sample; plus the reference's own decode_mcu_data."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_py as O
+    lib = O.oracle()
+    w, h, s = wl["width"], wl["height"], wl["sampling"]
+    nthreads = int(os.environ.get("HJD_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    # ~1 frame per thread per 0.3 s; keep ~10-20 s of CPU work
+    nframes = max(nthreads, min(16 * nthreads, 160))
+    pool = np.ascontiguousarray(coef_pool_host)
+    stride = pool.shape[1] * 64
+    out = np.empty((nthreads, h * w), dtype=np.uint32)
+    q = np.ascontiguousarray(qt, np.int32)
+    t0 = time.perf_counter()
+    rc = lib.oracle_decode_batch_q16_mt(pool.ctypes.data_as(O.i16p), stride, pool.shape[0],
+                                        q[0].ctypes.data_as(O.i32p), q[1].ctypes.data_as(O.i32p),
+                                        q[2].ctypes.data_as(O.i32p), w, h, s,
+                                        out.ctypes.data_as(O.u32p), h * w, nframes, nthreads)
+    dt = time.perf_counter() - t0
+    assert rc == 0
+    res = {"value": round(nframes * w * h / dt / 1e6, 2), "unit": "Mpixels/s", "cores": nthreads, "kind": "port",
+           "sample": f"{nframes} frames {w}x{h} {'4:2:0' if s == 1 else '4:4:4'} (pool of {pool.shape[0]}), "
+                     f"int16 zigzag -> BGRX in RAM, {nthreads} threads, {dt:.2f} s wall",
+           "cpu_model": _cpu_model(), "nproc": os.cpu_count()}
+    if O.ref_available():
+        try:
+            lib_ref = O.ref()
+            lib_ref.ref_decode_mcu_data.argtypes = [O.i32p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+            nat = O.dequant_natural(pool[0], q, s)
+            reps, t_sum = 3, 0.0
+            cwd = os.getcwd()
+            tmp = tempfile.mkdtemp(prefix="hjd_refbench_")
+            try:
+                os.chdir(tmp)
+                for _ in range(reps):
+                    buf = nat.copy()
+                    t0 = time.perf_counter()
+                    lib_ref.ref_decode_mcu_data(buf.ctypes.data_as(O.i32p), w, h, s)
+                    t_sum += time.perf_counter() - t0
+            finally:
+                os.chdir(cwd)
+            res["reference"] = {"value": round(reps * w * h / t_sum / 1e6, 2), "unit": "Mpixels/s", "cores": 1,
+                                "kind": "reference",
+                                "sample": f"{reps} x decode_mcu_data (src/decoder.cpp:397, USE_CPU_ONLY, incl. its "
+                                          f"BMP fwrite to a temp dir) on one {w}x{h} frame"}
+        except Exception as e:  # pragma: no cover
+            res["reference"] = {"error": str(e)}
+    return res
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def committed_traffic(workload):
+    """Per-launch HBM bytes from the committed PMC summary for this workload."""
+    best = None
+    for p in sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json"))):
+        try:
+            d = json.load(open(p))
+        except Exception:
+            continue
+        if d.get("workload") == workload and d.get("hbm_bytes_per_launch"):
+            best = (d["hbm_bytes_per_launch"], os.path.relpath(p, REPO))
+    return best
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="4k420", choices=sorted(WORKLOADS))
+    ap.add_argument("--frames", type=int, default=0, help="override batch size")
+    ap.add_argument("--grid", type=int, default=0, help="persistent grid (workgroups), 0 = default")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    import ocljpegdecoder_amd as hjd
+
+    wl = dict(WORKLOADS[args.workload])
+    if args.frames:
+        wl["frames"] = args.frames
+    w, h, s, nf = wl["width"], wl["height"], wl["sampling"], wl["frames"]
+    mw, mh, bpm, _ = hjd.mcu_geometry(w, h, s)
+    nblk = mw * mh * bpm
+    qt = std_qtables(1.0)
+
+    # ---- inputs resident in HBM --------------------------------------------------
+    npool = min(POOL, nf)
+    coefs = torch.empty((nf, nblk, 64), dtype=torch.int16, device=dev)
+    for i in range(npool):
+        coefs[i] = synth_frame_gpu(torch, nblk, bpm, qt, seed=1000 * rank + i, device=dev)
+    for i in range(npool, nf):
+        coefs[i].copy_(coefs[i % npool])
+    out = torch.empty((nf, h, w), dtype=torch.int32, device=dev)
+    specs = [hjd.FrameSpec(w, h, s, coef_offset=i * nblk, out_offset=i * h * w * 4, qt_index=(0, 1, 2))
+             for i in range(nf)]
+    ctx = hjd.Context(dev.index)
+    plan = hjd.Plan(ctx, specs, hjd.IN_Q16_ZIGZAG, qtables=qt)
+    torch.cuda.synchronize()
+
+    stream = torch.cuda.current_stream()
+    for _ in range(args.warmup):
+        plan.launch(coefs, out, stream, grid_blocks=args.grid)
+    torch.cuda.synchronize()
+
+    # ---- timed region: exactly K launches ----------------------------------------
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        plan.launch(coefs, out, stream, grid_blocks=args.grid)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps   # HIP events on the launch stream
+
+    elapsed = torch.tensor([wall], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    wall_max = float(elapsed.item())
+
+    px_per_launch = plan.pixels
+    bytes_per_launch = plan.coef_bytes + 4 * plan.pixels
+    total_px = px_per_launch * args.steps * world
+    value = total_px / wall_max / 1e6
+    achieved = bytes_per_launch / (kernel_ms / 1e3) / 1e9
+
+    # device-to-device copy bandwidth for context (same-size read+write)
+    copy_gbps = None
+    try:
+        a = torch.empty(1 << 30, dtype=torch.uint8, device=dev)
+        b = torch.empty_like(a)
+        b.copy_(a); torch.cuda.synchronize()
+        c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        c0.record(stream)
+        for _ in range(5):
+            b.copy_(a)
+        c1.record(stream); torch.cuda.synchronize()
+        copy_gbps = round(2 * 5 * a.numel() / (c0.elapsed_time(c1) / 1e3) / 1e9, 1)
+        del a, b
+    except Exception:
+        pass
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu:
+            pool_host = coefs[:npool].cpu().numpy()
+            log("running CPU baseline leg ...")
+            cpu = cpu_baseline(pool_host, qt, wl, value)
+        traffic = committed_traffic(args.workload)
+        res = {
+            "metric": "Mpixels/s decoded (dequant+IDCT+colour) at 1/2/4/8 GPUs; % HBM roofline",
+            "value": round(value, 1),
+            "unit": "Mpixels/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(wall_max / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic (device-generated FDCT+quantised smooth+noise blocks, pool of "
+                    f"{npool} distinct frames replicated to {nf}); inputs resident in HBM",
+            "config": {"workload": wl["desc"], "frames_per_gpu": nf, "width": w, "height": h,
+                       "sampling": "4:2:0" if s == 1 else "4:4:4", "input": "int16 quantised zigzag + qtables",
+                       "output": "BGRX 4 B/px in HBM", "parallelism": f"image-parallel x{world} (no collective)",
+                       "tasks_per_launch": plan.tasks},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                         "traffic": traffic[0] if traffic else None,
+                         "traffic_source": traffic[1] if traffic else None,
+                         "algorithmic_bytes_per_launch": bytes_per_launch,
+                         "kernel_ms_per_launch": round(kernel_ms, 4)},
+            "cpu_baseline": cpu,
+            "device_copy_GBps": copy_gbps,
+        }
+        if cpu and "reference" in cpu:
+            res["cpu_reference"] = cpu.pop("reference")
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,127 @@
+/*
+ * hjd.h -- C ABI of the MI355X (gfx950) JPEG pixel back-end.
+ *
+ * Hot path (one fused HIP kernel): zigzag + dequant -> 8x8 integer IDCT ->
+ * chroma upsample (nearest, 2x2) -> YCbCr->RGB (JFIF, truncating) -> BGRX store,
+ * bit-exact to the reference CPU path (src/cpuIDCT8x8.cpp + src/decoder.cpp:367-491
+ * of xinfushe/oclJPEGDecoder).  Plain C types only; every device pointer is a
+ * HIP device address, every `stream` a hipStream_t (NULL = default stream).
+ *
+ * The reference's own entry points (src/idct.h:4-18) are provided with their
+ * original C++ signatures by include/idct.h on top of this ABI.
+ *
+ * Errors: functions return HJD_OK (0) or a negative HJD_E_* code and never
+ * throw; hjd_last_error() returns a description of the last failure on the
+ * calling thread.
+ */
+#ifndef HJD_H
+#define HJD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HJD_ABI_VERSION 1
+
+enum hjd_status {
+    HJD_OK = 0,
+    HJD_E_INVALID = -1,   /* bad argument / unsupported geometry */
+    HJD_E_NO_DEVICE = -2, /* no HIP device (or index out of range) */
+    HJD_E_HIP = -3,       /* a HIP runtime call failed */
+    HJD_E_NOMEM = -4,     /* host or device allocation failed */
+    HJD_E_STATE = -5      /* call out of sequence (e.g. run before upload) */
+};
+
+/* Chroma sampling; numerically equal to the reference's ColorSpace enum
+ * (src/macro.h:114-119: YUV444 = 0, YUV411 = 1 (really H2V2 4:2:0), Other = 2). */
+enum hjd_sampling { HJD_YUV444 = 0, HJD_YUV420 = 1, HJD_OTHER = 2 };
+
+/* Coefficient input format. */
+enum hjd_input_format {
+    /* int16 quantised coefficients in zigzag order, exactly as Huffman decoding
+     * produces them (src/decoder.cpp:221-260); dequant + de-zigzag happen in
+     * the kernel load (src/decoder.cpp:338-342). 128 B per block. */
+    HJD_IN_Q16_ZIGZAG = 0,
+    /* int32 dequantised coefficients in natural order: the reference's
+     * jpg.mcu_data layout (src/jpeg.h:76) accepted by
+     * clidct_transfer_data_to_device. 256 B per block. */
+    HJD_IN_I32_NATURAL = 1
+};
+
+/*
+ * One frame of a batch.  Blocks are MCU-major in raster MCU order; per MCU the
+ * Y blocks in HxV raster order, then Cb, then Cr (src/decoder.cpp:286-344).
+ * MCU grid: ceil(W/8)xceil(H/8) (4:4:4) or ceil(W/16)xceil(H/16) (4:2:0).
+ */
+typedef struct hjd_frame {
+    uint64_t coef_offset; /* first block's offset in the coef buffer, in BLOCKS */
+    uint64_t out_offset;  /* byte offset of pixel (0,0) in the output buffer */
+    int32_t width;        /* visible pixels (output is cropped to W x H) */
+    int32_t height;
+    int32_t out_pitch;    /* bytes per output row, >= 4*width, multiple of 4 */
+    int32_t sampling;     /* HJD_YUV444 or HJD_YUV420 */
+    int32_t qt_index[3];  /* per component (Y, Cb, Cr): index into the qtable set */
+    int32_t reserved;     /* must be 0 */
+} hjd_frame;
+
+typedef struct hjd_ctx hjd_ctx;
+typedef struct hjd_plan hjd_plan;
+
+/* ---- library / device ---- */
+int hjd_abi_version(void);
+const char* hjd_last_error(void);
+int hjd_device_count(int* count);
+
+/* Context = one device + one stream of work.  Not thread-safe; use one context
+ * per host thread (or per GPU). */
+int hjd_ctx_create(int device, hjd_ctx** out);
+int hjd_ctx_destroy(hjd_ctx* ctx);
+int hjd_ctx_device(const hjd_ctx* ctx);
+
+/* ---- sizes ---- */
+int hjd_frame_blocks(int width, int height, int sampling, int64_t* nblocks);
+
+/*
+ * Plan: validates a batch of frames, computes the work decomposition and
+ * uploads the frame table and de-zigzagged quantisation tables to the device
+ * (synchronously, outside any timed region).  qtables: nq tables of 64 values
+ * each in FILE (zigzag) order, as DQT stores them (src/parser.cpp:65-89);
+ * ignored (may be NULL) for HJD_IN_I32_NATURAL.
+ */
+int hjd_plan_create(hjd_ctx* ctx, const hjd_frame* frames, int nframes, int input_format,
+                    const int32_t* qtables, int nq, hjd_plan** out);
+int hjd_plan_destroy(hjd_plan* plan);
+int64_t hjd_plan_tasks(const hjd_plan* plan);      /* work items (strips) */
+int64_t hjd_plan_pixels(const hjd_plan* plan);     /* visible pixels */
+int64_t hjd_plan_coef_bytes(const hjd_plan* plan); /* algorithmic input bytes */
+
+/*
+ * Enqueue the fused decode of every frame of the plan on `stream` (async).
+ * d_coefs: coefficient buffer (int16 or int32 per the plan's format);
+ * d_out: output buffer (frames at their out_offset).
+ * grid_blocks: persistent grid size in 256-thread workgroups (0 = default).
+ * The input is never modified (the reference kernel's in-place IDCT,
+ * src/idct8x8.cl:136-155, is not reproduced).
+ */
+int hjd_plan_launch(hjd_plan* plan, const void* d_coefs, void* d_out, void* stream, int grid_blocks);
+
+/* IDCT only (the reference's batch_idct, src/idct8x8.cl:157-166), out of
+ * place: int32 natural-order dequantised blocks -> int32 samples [-256,255]. */
+int hjd_idct_blocks(hjd_ctx* ctx, const int32_t* d_in, int32_t* d_out, int64_t nblocks, void* stream);
+
+/* ---- test / measurement hooks (same device code as the fused kernel) ---- */
+/* Colour stage alone over n (Y,U,V) triples: out[i] = BGRX.  mode 0 = the
+ * kernel's exact-integer formulation, 1 = literal fp64 formulation. */
+int hjd_debug_csc(hjd_ctx* ctx, const int32_t* d_y, const int32_t* d_u, const int32_t* d_v,
+                  uint32_t* d_out, int64_t n, int mode, void* stream);
+/* Exhaustive colour check: evaluates every (Y,U,V) in [-256,255]^3 on the
+ * device and writes the 2^27 BGRX words to d_out (512 MiB). */
+int hjd_debug_csc_exhaustive(hjd_ctx* ctx, uint32_t* d_out, int mode, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,31 @@
+"""ocljpegdecoder_amd -- MI355X-native JPEG pixel back-end.
+
+Drop-in replacement for the OpenCL IDCT/colour back-end of
+xinfushe/oclJPEGDecoder (src/oclDCT8x8.cpp + src/idct8x8.cl behind src/idct.h).
+The hot path is the fused HIP kernel in csrc/hjd_kernels.hpp, reached through
+the C ABI in include/hjd.h (libhjd.so).  Importing this package loads the
+native library and fails loudly if it is missing.
+"""
+from . import _lib
+
+_lib.load()
+
+from .backend import (  # noqa: E402
+    IN_I32_NATURAL,
+    IN_Q16_ZIGZAG,
+    OTHER,
+    YUV420,
+    YUV444,
+    Context,
+    FrameSpec,
+    Plan,
+    decode_frame,
+    device_count,
+    frame_blocks,
+    mcu_geometry,
+)
+
+__all__ = [
+    "Context", "FrameSpec", "Plan", "decode_frame", "device_count", "frame_blocks", "mcu_geometry",
+    "YUV444", "YUV420", "OTHER", "IN_Q16_ZIGZAG", "IN_I32_NATURAL",
+]

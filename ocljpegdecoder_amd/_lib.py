@@ -1,0 +1,131 @@
+"""ctypes binding of the native library (ocljpegdecoder_amd/lib/libhjd.so).
+
+The library is the product: importing the package without it raises
+immediately -- there is no Python or CPU fallback for the pixel path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, "lib", "libhjd.so")
+
+c_i32p = ctypes.POINTER(ctypes.c_int32)
+c_u32p = ctypes.POINTER(ctypes.c_uint32)
+
+
+class HjdFrame(ctypes.Structure):
+    """struct hjd_frame (include/hjd.h)."""
+    _fields_ = [
+        ("coef_offset", ctypes.c_uint64),
+        ("out_offset", ctypes.c_uint64),
+        ("width", ctypes.c_int32),
+        ("height", ctypes.c_int32),
+        ("out_pitch", ctypes.c_int32),
+        ("sampling", ctypes.c_int32),
+        ("qt_index", ctypes.c_int32 * 3),
+        ("reserved", ctypes.c_int32),
+    ]
+
+
+assert ctypes.sizeof(HjdFrame) == 48
+
+
+class HjdJpegInfo(ctypes.Structure):
+    """struct hjd_jpeg_info (include/hjd_host.h)."""
+    _fields_ = [
+        ("width", ctypes.c_int32),
+        ("height", ctypes.c_int32),
+        ("sampling", ctypes.c_int32),
+        ("restart_interval", ctypes.c_int32),
+        ("mcu_w", ctypes.c_int32),
+        ("mcu_h", ctypes.c_int32),
+        ("nblocks", ctypes.c_int64),
+        ("qt", (ctypes.c_int32 * 64) * 3),
+        ("qt_precision", ctypes.c_int32 * 3),
+        ("scan_offset", ctypes.c_int64),
+    ]
+
+
+# (name, restype, argtypes) of every exported C symbol declared in include/*.h
+SIGNATURES = {
+    # include/hjd.h
+    "hjd_abi_version": (ctypes.c_int, []),
+    "hjd_last_error": (ctypes.c_char_p, []),
+    "hjd_device_count": (ctypes.c_int, [c_i32p]),
+    "hjd_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "hjd_ctx_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "hjd_ctx_device": (ctypes.c_int, [ctypes.c_void_p]),
+    "hjd_frame_blocks": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]),
+    "hjd_plan_create": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HjdFrame), ctypes.c_int, ctypes.c_int,
+                                       c_i32p, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "hjd_plan_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "hjd_plan_tasks": (ctypes.c_int64, [ctypes.c_void_p]),
+    "hjd_plan_pixels": (ctypes.c_int64, [ctypes.c_void_p]),
+    "hjd_plan_coef_bytes": (ctypes.c_int64, [ctypes.c_void_p]),
+    "hjd_plan_launch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_int]),
+    "hjd_idct_blocks": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                       ctypes.c_void_p]),
+    "hjd_debug_csc": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]),
+    "hjd_debug_csc_exhaustive": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
+}
+
+_lib = None
+
+
+class HjdError(RuntimeError):
+    def __init__(self, code, what):
+        super().__init__(f"{what} failed with status {code}: {error_string()}")
+        self.code = code
+
+
+def load():
+    """Load libhjd.so (raises if it was not built: no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"native library missing: {LIB_PATH} -- run `python tools/build_native.py` "
+                          "(or __graft_entry__.build()); the HIP path has no fallback")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _bind_host(lib)
+    _lib = lib
+    return lib
+
+
+def _bind_host(lib):
+    """Host JPEG front end symbols (include/hjd_host.h), when compiled in."""
+    u8p = ctypes.POINTER(ctypes.c_uint8)
+    sigs = {
+        "hjd_jpeg_parse": (ctypes.c_int, [u8p, ctypes.c_size_t, ctypes.POINTER(HjdJpegInfo)]),
+        "hjd_jpeg_decode_coefs": (ctypes.c_int, [u8p, ctypes.c_size_t, ctypes.POINTER(HjdJpegInfo),
+                                                 ctypes.POINTER(ctypes.c_int16), ctypes.c_int64]),
+        "hjd_jpeg_decode_batch": (ctypes.c_int, [ctypes.POINTER(u8p), ctypes.POINTER(ctypes.c_size_t), ctypes.c_int,
+                                                 ctypes.POINTER(ctypes.POINTER(ctypes.c_int16)), ctypes.c_int64,
+                                                 ctypes.c_int, c_i32p]),
+    }
+    for name, (res, args) in sigs.items():
+        fn = getattr(lib, name, None)
+        if fn is not None:
+            fn.restype = res
+            fn.argtypes = args
+            SIGNATURES.setdefault(name, (res, args))
+
+
+def error_string() -> str:
+    lib = load()
+    s = lib.hjd_last_error()
+    return s.decode() if s else ""
+
+
+def check(code, what):
+    if code != 0:
+        raise HjdError(code, what)
+    return code

@@ -1,0 +1,164 @@
+"""Python host API over the C ABI (include/hjd.h).
+
+PyTorch is used only as plumbing: device memory (tensors), streams.  All pixel
+work runs in the HIP kernels of libhjd.so.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import HjdFrame, check
+
+YUV444 = 0
+YUV420 = 1  # == the reference's ColorSpace::YUV411 (src/macro.h:114-119), H2V2
+OTHER = 2
+
+IN_Q16_ZIGZAG = 0
+IN_I32_NATURAL = 1
+
+
+def mcu_geometry(width: int, height: int, sampling: int):
+    """(mcu_w, mcu_h, blocks_per_mcu, mcu_px) -- src/decoder.cpp:161-192."""
+    mpx = 16 if sampling == YUV420 else 8
+    bpm = 6 if sampling == YUV420 else 3
+    return (width - 1) // mpx + 1, (height - 1) // mpx + 1, bpm, mpx
+
+
+def frame_blocks(width: int, height: int, sampling: int) -> int:
+    mw, mh, bpm, _ = mcu_geometry(width, height, sampling)
+    return mw * mh * bpm
+
+
+def device_count() -> int:
+    lib = _lib.load()
+    n = ctypes.c_int32(0)
+    check(lib.hjd_device_count(ctypes.byref(n)), "hjd_device_count")
+    return n.value
+
+
+def _stream_ptr(stream) -> Optional[int]:
+    if stream is None:
+        import torch
+        return torch.cuda.current_stream().cuda_stream
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream
+
+
+class Context:
+    """One device (hjd_ctx)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = _lib.load()
+        h = ctypes.c_void_p()
+        check(self.lib.hjd_ctx_create(device, ctypes.byref(h)), "hjd_ctx_create")
+        self.handle = h
+        self.device = device
+
+    def close(self):
+        if self.handle:
+            self.lib.hjd_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- kernels outside a plan -------------------------------------------------
+    def idct_blocks(self, d_in, d_out, nblocks: int, stream=None):
+        """IDCT only (int32 natural in -> int32 samples), tensors on this device."""
+        check(self.lib.hjd_idct_blocks(self.handle, d_in.data_ptr(), d_out.data_ptr(), int(nblocks),
+                                       _stream_ptr(stream)), "hjd_idct_blocks")
+
+    def debug_csc(self, y, u, v, out, mode: int = 0, stream=None):
+        check(self.lib.hjd_debug_csc(self.handle, y.data_ptr(), u.data_ptr(), v.data_ptr(), out.data_ptr(),
+                                     y.numel(), mode, _stream_ptr(stream)), "hjd_debug_csc")
+
+    def debug_csc_exhaustive(self, out, mode: int = 0, stream=None):
+        assert out.numel() * out.element_size() >= 4 << 27
+        check(self.lib.hjd_debug_csc_exhaustive(self.handle, out.data_ptr(), mode, _stream_ptr(stream)),
+              "hjd_debug_csc_exhaustive")
+
+
+@dataclass
+class FrameSpec:
+    width: int
+    height: int
+    sampling: int
+    coef_offset: int = 0          # in blocks
+    out_offset: int = 0           # bytes
+    out_pitch: int = 0            # bytes (0 -> 4*width)
+    qt_index: Sequence[int] = field(default_factory=lambda: (0, 1, 1))
+
+    def to_c(self) -> HjdFrame:
+        f = HjdFrame()
+        f.coef_offset = self.coef_offset
+        f.out_offset = self.out_offset
+        f.width = self.width
+        f.height = self.height
+        f.out_pitch = self.out_pitch or 4 * self.width
+        f.sampling = self.sampling
+        for i in range(3):
+            f.qt_index[i] = int(self.qt_index[i])
+        f.reserved = 0
+        return f
+
+
+class Plan:
+    """A validated batch of frames with its device-side frame table (hjd_plan)."""
+
+    def __init__(self, ctx: Context, frames: Sequence[FrameSpec], input_format: int = IN_Q16_ZIGZAG,
+                 qtables: Optional[np.ndarray] = None):
+        self.ctx = ctx
+        self.lib = ctx.lib
+        self.frames = list(frames)
+        arr = (HjdFrame * max(1, len(self.frames)))(*[f.to_c() for f in self.frames])
+        if qtables is not None:
+            q = np.ascontiguousarray(qtables, dtype=np.int32).reshape(-1, 64)
+            qp, nq = q.ctypes.data_as(_lib.c_i32p), q.shape[0]
+        else:
+            q, qp, nq = None, None, 0
+        h = ctypes.c_void_p()
+        check(self.lib.hjd_plan_create(ctx.handle, arr, len(self.frames), input_format, qp, nq, ctypes.byref(h)),
+              "hjd_plan_create")
+        self.handle = h
+        self.input_format = input_format
+        self.tasks = self.lib.hjd_plan_tasks(h)
+        self.pixels = self.lib.hjd_plan_pixels(h)
+        self.coef_bytes = self.lib.hjd_plan_coef_bytes(h)
+
+    def launch(self, coefs, out, stream=None, grid_blocks: int = 0):
+        """Enqueue the fused kernel; coefs/out are device tensors (or raw pointers)."""
+        cp = coefs if isinstance(coefs, int) else coefs.data_ptr()
+        op = out if isinstance(out, int) else out.data_ptr()
+        check(self.lib.hjd_plan_launch(self.handle, cp, op, _stream_ptr(stream), grid_blocks), "hjd_plan_launch")
+
+    def close(self):
+        if self.handle:
+            self.lib.hjd_plan_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def decode_frame(ctx: Context, coefs, qt: np.ndarray, width: int, height: int, sampling: int,
+                 input_format: int = IN_Q16_ZIGZAG, stream=None):
+    """Decode one frame already resident on the device; returns an int32 (H, W)
+    device tensor holding BGRX words (0x00RRGGBB)."""
+    import torch
+    plan = Plan(ctx, [FrameSpec(width, height, sampling, qt_index=(0, 1, 2))], input_format,
+                qtables=qt if input_format == IN_Q16_ZIGZAG else None)
+    out = torch.empty((height, width), dtype=torch.int32, device=coefs.device)
+    plan.launch(coefs, out, stream)
+    return out, plan

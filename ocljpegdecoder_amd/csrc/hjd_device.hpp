@@ -1,0 +1,147 @@
+// hjd_device.hpp -- device-side arithmetic of the pixel back-end (gfx950).
+//
+// Everything here is bit-exact to the reference CPU path on the reference's
+// legal input domain (the domain on which src/cpuIDCT8x8.cpp is defined: no
+// signed overflow and column outputs inside its iclp[-512..511] table).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace hjd {
+
+// round(2048*sqrt(2)*cos(k*pi/16)): src/cpuIDCT8x8.cpp:6-11
+constexpr int kC1 = 2841, kC2 = 2676, kC3 = 2408, kC5 = 1609, kC6 = 1108, kC7 = 565;
+
+// 24-bit signed multiply (v_mul_i32_i24 / v_mad_i32_i24, full rate).  Exact
+// (low 32 bits of the product) when both operands fit in 24 signed bits.  On
+// the legal domain every operand that goes through it does: by Parseval the
+// block's coefficient energy is bounded by its output energy (|out| <= 512 per
+// sample => ||coef||_2 <= ~4.1e3), so stage-1/2 operands of the row pass are
+// < 2^14 and of the column pass (row outputs, gain 8*sqrt(8)) < 2^18.
+__device__ __forceinline__ int mul24(int a, int b) { return __mul24(a, b); }
+
+// The stage-3 products 181*(a4 +- a5) can exceed 24 bits on the legal domain,
+// so they use a full 32-bit multiply (low 32 bits = the reference's int math).
+__device__ __forceinline__ int mul181(int x) { return x * 181; }
+
+// min/max pairs lower to one v_med3_i32
+__device__ __forceinline__ int clamp_sample(int v) { return min(max(v, -256), 255); }
+__device__ __forceinline__ int clamp_u8(int v) { return min(max(v, 0), 255); }
+
+// One 8-point pass on natural-order values v[0..7] (in place).
+// kCol = false: row pass, src/cpuIDCT8x8.cpp:36-80 (x<<11, +128 on DC, >>8 out).
+// kCol = true:  column pass, src/cpuIDCT8x8.cpp:82-127 (x<<8, +8192 on DC,
+//               (+4)>>3 on stage-1/2 products, >>14 out, clamp [-256,255] --
+//               the CPU clamp, not the OpenCL kernel's [-256,256] at
+//               src/idct8x8.cl:116).
+// The reference's DC-only short-cuts (:40-45, :86-92) give exactly the values
+// of the full butterfly, so the kernel always runs the full butterfly.
+template <bool kCol>
+__device__ __forceinline__ void idct8(int (&v)[8])
+{
+    constexpr int kIn = kCol ? 8 : 11;
+    constexpr int kRnd = kCol ? 4 : 0;
+    constexpr int kSh = kCol ? 3 : 0;
+
+    int e0 = (v[0] << kIn) + (kCol ? 8192 : 128);
+    int e1 = v[4] << kIn;
+
+    // odd part
+    int t = mul24(kC7, v[1] + v[7]) + kRnd;
+    int o4 = (t + mul24(kC1 - kC7, v[1])) >> kSh;
+    int o5 = (t - mul24(kC1 + kC7, v[7])) >> kSh;
+    t = mul24(kC3, v[5] + v[3]) + kRnd;
+    int o6 = (t - mul24(kC3 - kC5, v[5])) >> kSh;
+    int o7 = (t - mul24(kC3 + kC5, v[3])) >> kSh;
+
+    // even part
+    int e8 = e0 + e1;
+    e0 -= e1;
+    t = mul24(kC6, v[2] + v[6]) + kRnd;
+    int e2 = (t - mul24(kC2 + kC6, v[6])) >> kSh;
+    int e3 = (t + mul24(kC2 - kC6, v[2])) >> kSh;
+
+    int a1 = o4 + o6, a4 = o4 - o6;
+    int a6 = o5 + o7, a5 = o5 - o7;
+
+    int f7 = e8 + e3, f8 = e8 - e3;
+    int f3 = e0 + e2, f0 = e0 - e2;
+    int g2 = (mul181(a4 + a5) + 128) >> 8;
+    int g4 = (mul181(a4 - a5) + 128) >> 8;
+
+    int r0 = f7 + a1, r1 = f3 + g2, r2 = f0 + g4, r3 = f8 + a6;
+    int r4 = f8 - a6, r5 = f0 - g4, r6 = f3 - g2, r7 = f7 - a1;
+    if constexpr (kCol) {
+        v[0] = clamp_sample(r0 >> 14); v[1] = clamp_sample(r1 >> 14);
+        v[2] = clamp_sample(r2 >> 14); v[3] = clamp_sample(r3 >> 14);
+        v[4] = clamp_sample(r4 >> 14); v[5] = clamp_sample(r5 >> 14);
+        v[6] = clamp_sample(r6 >> 14); v[7] = clamp_sample(r7 >> 14);
+    } else {
+        v[0] = r0 >> 8; v[1] = r1 >> 8; v[2] = r2 >> 8; v[3] = r3 >> 8;
+        v[4] = r4 >> 8; v[5] = r5 >> 8; v[6] = r6 >> 8; v[7] = r7 >> 8;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Colour conversion.  Reference (src/decoder.cpp:367-370 + src/macro.h:121-145):
+//   R = (int)(Y + 1.402*V + 128), G = (int)(Y - 0.34414*U - 0.71414*V + 128),
+//   B = (int)(Y + 1.772*U + 128) in C double, each clamped to [0,255],
+//   packed 0x00RRGGBB (bytes B,G,R,0).
+//
+// Exact-integer restatement used by the kernel (proved by an exhaustive
+// device test over all 2^27 (Y,U,V) in [-256,255]^3, tests/test_gpu_parity.py):
+//   * clamp(trunc(x)) == clamp(floor(x)) for every real x;
+//   * Y+128 is an integer, so floor(x) = Y + 128 + floor(chroma term);
+//   * 1.402 = 701/500 and 1.772 = 443/250: for V,U != 0 the chroma term sits
+//     >= 1/500 from an integer, far above fp32/fp64 rounding, so
+//     floor(float(V)*1.402f) is exact (and exactly 0 for V == 0);
+//   * G's term is -(17207U + 35707V)/50000; it is computed as an exact integer
+//     floor division.  When the division is exact, the reference's double
+//     rounding can land one below the integer: over the whole domain this
+//     happens only for (U,V) = (-200,200) with Y in [188,201], where the
+//     reference gives one less (enumerated in tests/test_oracle.py).
+// Chroma terms are computed once per chroma sample and shared by the 4 (4:2:0)
+// pixels that replicate it.
+// ---------------------------------------------------------------------------
+struct ChromaTerms {
+    int rq, gq, bq;
+    int special;
+};
+
+__device__ __forceinline__ ChromaTerms chroma_terms(int u, int v)
+{
+    ChromaTerms t;
+    t.rq = __float2int_rd(static_cast<float>(v) * 1.402f);
+    t.bq = __float2int_rd(static_cast<float>(u) * 1.772f);
+    const int n = -(mul24(17207, u) + mul24(35707, v));  // |n| < 2^24: exact in fp32
+    int q = __float2int_rd(static_cast<float>(n) * 2.0e-5f);
+    const int rem = n - mul24(q, 50000);
+    q += (rem >= 50000 ? 1 : 0) - (rem < 0 ? 1 : 0);
+    t.gq = q;
+    t.special = (u == -200) & (v == 200);
+    return t;
+}
+
+__device__ __forceinline__ uint32_t pixel_bgrx(int y, const ChromaTerms& t)
+{
+    const int yb = y + 128;
+    const int r = clamp_u8(yb + t.rq);
+    const int g = clamp_u8(yb + t.gq - (t.special & (static_cast<unsigned>(y - 188) < 14u)));
+    const int b = clamp_u8(yb + t.bq);
+    return (static_cast<uint32_t>(r) << 16) | (static_cast<uint32_t>(g) << 8) | static_cast<uint32_t>(b);
+}
+
+// Literal fp64 form of src/decoder.cpp:369 (C evaluation order, no FMA
+// contraction) -- kept as the cross-check arm of the exhaustive test.
+__device__ __forceinline__ uint32_t pixel_bgrx_f64(int y, int u, int v)
+{
+#pragma clang fp contract(off)
+    const double Y = y, U = u, V = v;
+    const int r = static_cast<int>(Y + 1.402 * V + 128);
+    const int g = static_cast<int>(Y - 0.34414 * U - 0.71414 * V + 128);
+    const int b = static_cast<int>(Y + 1.772 * U + 128);
+    return (static_cast<uint32_t>(clamp_u8(r)) << 16) | (static_cast<uint32_t>(clamp_u8(g)) << 8) |
+           static_cast<uint32_t>(clamp_u8(b));
+}
+
+}  // namespace hjd

@@ -1,0 +1,314 @@
+// hjd_runtime.hip -- C-ABI runtime of the MI355X pixel back-end (include/hjd.h).
+//
+// Replaces the reference's OpenCL host runtime (src/oclDCT8x8.cpp:25-341):
+// device selection, buffers, kernel selection per colour space and launch.
+// Unlike the reference there is no file-static state here: contexts and plans
+// are handles, so several images / frames / devices can be in flight.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "hjd.h"
+#include "hjd_kernels.hpp"
+
+using hjd::FrameDev;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char* fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
+
+#define HJD_HIP(call)                                                                        \
+    do {                                                                                     \
+        hipError_t e_ = (call);                                                              \
+        if (e_ != hipSuccess)                                                                \
+            return fail(HJD_E_HIP, "%s failed: %s (%s:%d)", #call, hipGetErrorString(e_),    \
+                        __FILE__, __LINE__);                                                 \
+    } while (0)
+
+// JPEG zigzag: natural index of zigzag position k (src/zigzag.h:15-40).
+constexpr int kZigzag[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
+                             12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
+                             35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+                             58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+
+}  // namespace
+
+struct hjd_ctx {
+    int device = 0;
+    int num_cu = 256;
+};
+
+struct hjd_plan {
+    hjd_ctx* ctx = nullptr;
+    int input_format = 0;
+    int sampling = -1;          // common sampling of all frames (kernel template)
+    int nframes = 0;
+    int64_t tasks = 0;
+    int64_t pixels = 0;
+    int64_t coef_bytes = 0;
+    FrameDev* d_frames = nullptr;
+    int* d_qt = nullptr;        // natural-order tables [nq][64]
+};
+
+extern "C" {
+
+int hjd_abi_version(void) { return HJD_ABI_VERSION; }
+
+const char* hjd_last_error(void) { return g_last_error.c_str(); }
+
+int hjd_device_count(int* count)
+{
+    if (!count) return fail(HJD_E_INVALID, "count is NULL");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) {
+        *count = 0;
+        if (e == hipErrorNoDevice) return HJD_OK;
+        return fail(HJD_E_HIP, "hipGetDeviceCount: %s", hipGetErrorString(e));
+    }
+    *count = n;
+    return HJD_OK;
+}
+
+int hjd_ctx_create(int device, hjd_ctx** out)
+{
+    if (!out) return fail(HJD_E_INVALID, "out is NULL");
+    *out = nullptr;
+    int n = 0;
+    int rc = hjd_device_count(&n);
+    if (rc) return rc;
+    if (device < 0 || device >= n) return fail(HJD_E_NO_DEVICE, "device %d not present (%d devices)", device, n);
+    HJD_HIP(hipSetDevice(device));
+    hjd_ctx* c = new (std::nothrow) hjd_ctx;
+    if (!c) return fail(HJD_E_NOMEM, "context allocation");
+    c->device = device;
+    int cu = 0;
+    if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cu > 0)
+        c->num_cu = cu;
+    *out = c;
+    return HJD_OK;
+}
+
+int hjd_ctx_destroy(hjd_ctx* ctx)
+{
+    delete ctx;
+    return HJD_OK;
+}
+
+int hjd_ctx_device(const hjd_ctx* ctx) { return ctx ? ctx->device : -1; }
+
+static int geometry(int width, int height, int sampling, int& mcu_w, int& mcu_h, int& bpm, int& mpx)
+{
+    if (width <= 0 || height <= 0 || width > 65535 || height > 65535)
+        return fail(HJD_E_INVALID, "invalid dimensions %dx%d", width, height);
+    if (sampling != HJD_YUV444 && sampling != HJD_YUV420)
+        return fail(HJD_E_INVALID, "unsupported sampling %d (only 4:4:4 and 4:2:0)", sampling);
+    mpx = sampling == HJD_YUV420 ? 16 : 8;
+    bpm = sampling == HJD_YUV420 ? 6 : 3;
+    mcu_w = (width - 1) / mpx + 1;   // src/decoder.cpp:189-190
+    mcu_h = (height - 1) / mpx + 1;
+    return HJD_OK;
+}
+
+int hjd_frame_blocks(int width, int height, int sampling, int64_t* nblocks)
+{
+    int mw, mh, bpm, mpx;
+    int rc = geometry(width, height, sampling, mw, mh, bpm, mpx);
+    if (rc) return rc;
+    if (!nblocks) return fail(HJD_E_INVALID, "nblocks is NULL");
+    *nblocks = static_cast<int64_t>(mw) * mh * bpm;
+    return HJD_OK;
+}
+
+int hjd_plan_create(hjd_ctx* ctx, const hjd_frame* frames, int nframes, int input_format,
+                    const int32_t* qtables, int nq, hjd_plan** out)
+{
+    if (!ctx || !out || (!frames && nframes > 0) || nframes < 0)
+        return fail(HJD_E_INVALID, "invalid plan arguments");
+    *out = nullptr;
+    if (input_format != HJD_IN_Q16_ZIGZAG && input_format != HJD_IN_I32_NATURAL)
+        return fail(HJD_E_INVALID, "unknown input format %d", input_format);
+    if (input_format == HJD_IN_Q16_ZIGZAG && (!qtables || nq <= 0))
+        return fail(HJD_E_INVALID, "quantisation tables required for HJD_IN_Q16_ZIGZAG");
+
+    std::vector<FrameDev> fd(static_cast<size_t>(std::max(nframes, 1)));
+    int64_t tasks = 0, pixels = 0, blocks = 0;
+    int sampling = nframes > 0 ? frames[0].sampling : HJD_YUV420;
+    for (int i = 0; i < nframes; ++i) {
+        const hjd_frame& f = frames[i];
+        int mw, mh, bpm, mpx;
+        int rc = geometry(f.width, f.height, f.sampling, mw, mh, bpm, mpx);
+        if (rc) return fail(rc, "frame %d: %s", i, g_last_error.c_str());
+        if (f.sampling != sampling)
+            return fail(HJD_E_INVALID, "frame %d: mixed sampling in one plan (use one plan per sampling)", i);
+        if (f.out_pitch < 4 * f.width || (f.out_pitch & 3) || (f.out_offset & 3))
+            return fail(HJD_E_INVALID, "frame %d: bad output pitch/offset", i);
+        if (f.reserved != 0) return fail(HJD_E_INVALID, "frame %d: reserved field must be 0", i);
+        FrameDev& d = fd[i];
+        if (input_format == HJD_IN_Q16_ZIGZAG) {
+            for (int c = 0; c < 3; ++c)
+                if (f.qt_index[c] < 0 || f.qt_index[c] >= nq)
+                    return fail(HJD_E_INVALID, "frame %d: qt_index[%d]=%d out of range", i, c, f.qt_index[c]);
+        }
+        const int tasks_mcus = f.sampling == HJD_YUV420 ? 8 : 16;
+        d.coef_base = static_cast<int64_t>(f.coef_offset);
+        d.out_base = static_cast<int64_t>(f.out_offset);
+        d.task_begin = tasks;
+        d.width = f.width;
+        d.height = f.height;
+        d.pitch = f.out_pitch;
+        d.sampling = f.sampling;
+        d.mcu_w = mw;
+        d.strips = (mw + tasks_mcus - 1) / tasks_mcus;
+        for (int c = 0; c < 3; ++c) d.qt[c] = input_format == HJD_IN_Q16_ZIGZAG ? f.qt_index[c] : 0;
+        d.vec_ok = ((f.out_pitch & 15) == 0 && (f.out_offset & 15) == 0) ? 1 : 0;
+        tasks += static_cast<int64_t>(d.strips) * mh;
+        pixels += static_cast<int64_t>(f.width) * f.height;
+        blocks += static_cast<int64_t>(mw) * mh * bpm;
+    }
+
+    HJD_HIP(hipSetDevice(ctx->device));
+    hjd_plan* p = new (std::nothrow) hjd_plan;
+    if (!p) return fail(HJD_E_NOMEM, "plan allocation");
+    p->ctx = ctx;
+    p->input_format = input_format;
+    p->sampling = sampling;
+    p->nframes = nframes;
+    p->tasks = tasks;
+    p->pixels = pixels;
+    p->coef_bytes = blocks * (input_format == HJD_IN_Q16_ZIGZAG ? 128 : 256);
+
+    // qtables: file (zigzag) order -> natural order, so a lane reads its row's
+    // 8 factors contiguously.
+    const int nqt = input_format == HJD_IN_Q16_ZIGZAG ? nq : 1;
+    std::vector<int32_t> qnat(static_cast<size_t>(nqt) * 64, 0);
+    if (input_format == HJD_IN_Q16_ZIGZAG)
+        for (int t = 0; t < nq; ++t)
+            for (int k = 0; k < 64; ++k) qnat[t * 64 + kZigzag[k]] = qtables[t * 64 + k];
+
+    hipError_t e = hipMalloc(&p->d_frames, fd.size() * sizeof(FrameDev));
+    if (e == hipSuccess) e = hipMalloc(&p->d_qt, qnat.size() * sizeof(int32_t));
+    if (e == hipSuccess) e = hipMemcpy(p->d_frames, fd.data(), fd.size() * sizeof(FrameDev), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(p->d_qt, qnat.data(), qnat.size() * sizeof(int32_t), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        (void)hipFree(p->d_frames);
+        (void)hipFree(p->d_qt);
+        delete p;
+        return fail(HJD_E_HIP, "plan upload: %s", hipGetErrorString(e));
+    }
+    *out = p;
+    return HJD_OK;
+}
+
+int hjd_plan_destroy(hjd_plan* plan)
+{
+    if (!plan) return HJD_OK;
+    (void)hipSetDevice(plan->ctx->device);
+    (void)hipFree(plan->d_frames);
+    (void)hipFree(plan->d_qt);
+    delete plan;
+    return HJD_OK;
+}
+
+int64_t hjd_plan_tasks(const hjd_plan* plan) { return plan ? plan->tasks : -1; }
+int64_t hjd_plan_pixels(const hjd_plan* plan) { return plan ? plan->pixels : -1; }
+int64_t hjd_plan_coef_bytes(const hjd_plan* plan) { return plan ? plan->coef_bytes : -1; }
+
+static int default_grid(const hjd_ctx* ctx, int64_t work_waves)
+{
+    // 4 resident 256-thread groups per CU (16 waves/CU; LDS 36 KiB per group).
+    const int64_t cap = static_cast<int64_t>(ctx->num_cu) * 4;
+    const int64_t need = (work_waves + hjd::kWavesPerGroup - 1) / hjd::kWavesPerGroup;
+    return static_cast<int>(std::max<int64_t>(1, std::min(cap, need)));
+}
+
+int hjd_plan_launch(hjd_plan* plan, const void* d_coefs, void* d_out, void* stream, int grid_blocks)
+{
+    if (!plan) return fail(HJD_E_INVALID, "plan is NULL");
+    if (plan->tasks == 0) return HJD_OK;
+    if (!d_coefs || !d_out) return fail(HJD_E_INVALID, "NULL device buffer");
+    if (grid_blocks < 0) return fail(HJD_E_INVALID, "grid_blocks < 0");
+    HJD_HIP(hipSetDevice(plan->ctx->device));
+    const int grid = grid_blocks > 0 ? grid_blocks : default_grid(plan->ctx, plan->tasks);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    uint8_t* out = static_cast<uint8_t*>(d_out);
+    const dim3 gdim(grid), bdim(hjd::kGroupThreads);
+    if (plan->input_format == HJD_IN_Q16_ZIGZAG) {
+        if (plan->sampling == HJD_YUV420)
+            hipLaunchKernelGGL((hjd::decode_kernel<1, 0>), gdim, bdim, 0, s, d_coefs, plan->d_qt, plan->d_frames,
+                               plan->nframes, plan->tasks, out);
+        else
+            hipLaunchKernelGGL((hjd::decode_kernel<0, 0>), gdim, bdim, 0, s, d_coefs, plan->d_qt, plan->d_frames,
+                               plan->nframes, plan->tasks, out);
+    } else {
+        if (plan->sampling == HJD_YUV420)
+            hipLaunchKernelGGL((hjd::decode_kernel<1, 1>), gdim, bdim, 0, s, d_coefs, plan->d_qt, plan->d_frames,
+                               plan->nframes, plan->tasks, out);
+        else
+            hipLaunchKernelGGL((hjd::decode_kernel<0, 1>), gdim, bdim, 0, s, d_coefs, plan->d_qt, plan->d_frames,
+                               plan->nframes, plan->tasks, out);
+    }
+    HJD_HIP(hipGetLastError());
+    return HJD_OK;
+}
+
+int hjd_idct_blocks(hjd_ctx* ctx, const int32_t* d_in, int32_t* d_out, int64_t nblocks, void* stream)
+{
+    if (!ctx || nblocks < 0 || ((!d_in || !d_out) && nblocks > 0)) return fail(HJD_E_INVALID, "invalid arguments");
+    if (nblocks == 0) return HJD_OK;
+    HJD_HIP(hipSetDevice(ctx->device));
+    const int grid = default_grid(ctx, (nblocks + 7) / 8);
+    hipLaunchKernelGGL(hjd::idct_blocks_kernel, dim3(grid), dim3(hjd::kGroupThreads), 0,
+                       static_cast<hipStream_t>(stream), d_in, d_out, nblocks);
+    HJD_HIP(hipGetLastError());
+    return HJD_OK;
+}
+
+int hjd_debug_csc(hjd_ctx* ctx, const int32_t* d_y, const int32_t* d_u, const int32_t* d_v, uint32_t* d_out,
+                  int64_t n, int mode, void* stream)
+{
+    if (!ctx || n < 0 || (mode != 0 && mode != 1)) return fail(HJD_E_INVALID, "invalid arguments");
+    if (n == 0) return HJD_OK;
+    HJD_HIP(hipSetDevice(ctx->device));
+    const int grid = static_cast<int>(std::min<int64_t>((n + 255) / 256, 65536));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (mode == 0)
+        hipLaunchKernelGGL(hjd::csc_kernel<0>, dim3(grid), dim3(256), 0, s, d_y, d_u, d_v, d_out, n);
+    else
+        hipLaunchKernelGGL(hjd::csc_kernel<1>, dim3(grid), dim3(256), 0, s, d_y, d_u, d_v, d_out, n);
+    HJD_HIP(hipGetLastError());
+    return HJD_OK;
+}
+
+int hjd_debug_csc_exhaustive(hjd_ctx* ctx, uint32_t* d_out, int mode, void* stream)
+{
+    if (!ctx || !d_out || (mode != 0 && mode != 1)) return fail(HJD_E_INVALID, "invalid arguments");
+    HJD_HIP(hipSetDevice(ctx->device));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (mode == 0)
+        hipLaunchKernelGGL(hjd::csc_exhaustive_kernel<0>, dim3(8192), dim3(256), 0, s, d_out);
+    else
+        hipLaunchKernelGGL(hjd::csc_exhaustive_kernel<1>, dim3(8192), dim3(256), 0, s, d_out);
+    HJD_HIP(hipGetLastError());
+    return HJD_OK;
+}
+
+}  // extern "C"

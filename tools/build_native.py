@@ -1,0 +1,86 @@
+"""Build the native library in-tree: ocljpegdecoder_amd/lib/libhjd.so (gfx950).
+
+    python tools/build_native.py [--force]
+
+One shared library holds the HIP kernels + C-ABI runtime (include/hjd.h), the
+idct.h compatibility shim (include/idct.h) and the host JPEG front end
+(include/hjd_host.h).  hipcc cross-compiles for gfx950 without a GPU.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "ocljpegdecoder_amd")
+CSRC = os.path.join(PKG, "csrc")
+INCLUDE = os.path.join(REPO, "include")
+LIBDIR = os.path.join(PKG, "lib")
+LIB = os.path.join(LIBDIR, "libhjd.so")
+OBJDIR = os.path.join(REPO, "build", "obj")
+
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("HJD_ARCH", "gfx950")
+
+HIP_SOURCES = ["hjd_runtime.hip"]
+CXX_SOURCES = ["idct_compat.cpp", "jpeg_host.cpp", "stream_pipeline.cpp"]
+
+COMMON = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", f"-I{INCLUDE}", f"-I{CSRC}"]
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"command failed ({r.returncode}): {' '.join(cmd)}\n{r.stdout}")
+    return r.stdout
+
+
+def _needs(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _headers():
+    hs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hpp", ".h"))]
+    hs += [os.path.join(INCLUDE, f) for f in os.listdir(INCLUDE) if f.endswith(".h")]
+    return hs
+
+
+def build(verbose: bool = False, force: bool = False) -> str:
+    os.makedirs(LIBDIR, exist_ok=True)
+    os.makedirs(OBJDIR, exist_ok=True)
+    headers = _headers()
+    jobs = []
+    objs = []
+    for src in HIP_SOURCES:
+        s = os.path.join(CSRC, src)
+        o = os.path.join(OBJDIR, src + ".o")
+        objs.append(o)
+        if force or _needs(o, [s] + headers):
+            jobs.append([HIPCC, f"--offload-arch={ARCH}", *COMMON, "-c", s, "-o", o])
+    for src in CXX_SOURCES:
+        s = os.path.join(CSRC, src)
+        if not os.path.exists(s):
+            continue
+        o = os.path.join(OBJDIR, src + ".o")
+        objs.append(o)
+        if force or _needs(o, [s] + headers):
+            # host-only C++ (no device code): compiled by hipcc's clang as plain C++
+            jobs.append([HIPCC, *COMMON, "-x", "c++", "-pthread", "-c", s, "-o", o])
+    with ThreadPoolExecutor(max_workers=min(8, max(1, len(jobs)))) as ex:
+        for out in ex.map(_run, jobs):
+            if verbose and out.strip():
+                print(out)
+    if force or jobs or _needs(LIB, objs):
+        out = _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", "-o", LIB, *objs])
+        if verbose and out.strip():
+            print(out)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(verbose=True, force="--force" in sys.argv))
