@@ -90,6 +90,15 @@ def load():
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"native library missing: {LIB_PATH} -- run `python tools/build_native.py` "
                           "(or __graft_entry__.build()); the HIP path has no fallback")
+    # One HIP runtime per process: PyTorch-ROCm bundles its own libamdhip64.so
+    # (SONAME libamdhip64.so.7) and NEEDs it unversioned, so if libhjd.so pulled
+    # /opt/rocm's copy in first, torch would load a second runtime beside it.
+    # Loading torch first makes libhjd.so's NEEDED libamdhip64.so.7 resolve to
+    # the runtime torch already mapped.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)

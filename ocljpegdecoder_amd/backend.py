@@ -74,10 +74,16 @@ class Context:
     # -- kernels outside a plan -------------------------------------------------
     def idct_blocks(self, d_in, d_out, nblocks: int, stream=None):
         """IDCT only (int32 natural in -> int32 samples), tensors on this device."""
+        for t in (d_in, d_out):
+            if not (t.is_cuda and t.is_contiguous() and t.element_size() == 4 and t.numel() >= 64 * nblocks):
+                raise ValueError("idct_blocks needs contiguous int32 device tensors of >= 64*nblocks elements")
         check(self.lib.hjd_idct_blocks(self.handle, d_in.data_ptr(), d_out.data_ptr(), int(nblocks),
                                        _stream_ptr(stream)), "hjd_idct_blocks")
 
     def debug_csc(self, y, u, v, out, mode: int = 0, stream=None):
+        for t in (y, u, v, out):
+            if not (t.is_cuda and t.is_contiguous() and t.element_size() == 4 and t.numel() >= y.numel()):
+                raise ValueError("debug_csc needs contiguous 4-byte device tensors of equal length")
         check(self.lib.hjd_debug_csc(self.handle, y.data_ptr(), u.data_ptr(), v.data_ptr(), out.data_ptr(),
                                      y.numel(), mode, _stream_ptr(stream)), "hjd_debug_csc")
 
@@ -133,11 +139,32 @@ class Plan:
         self.tasks = self.lib.hjd_plan_tasks(h)
         self.pixels = self.lib.hjd_plan_pixels(h)
         self.coef_bytes = self.lib.hjd_plan_coef_bytes(h)
+        # extents the kernel will touch: validated against the tensors at launch
+        self.coef_elem_bytes = 2 if input_format == IN_Q16_ZIGZAG else 4
+        self.coef_elems_needed = max([64 * (f.coef_offset + frame_blocks(f.width, f.height, f.sampling))
+                                      for f in self.frames] or [0])
+        self.out_bytes_needed = max([f.out_offset + (f.height - 1) * (f.out_pitch or 4 * f.width) + 4 * f.width
+                                     for f in self.frames] or [0])
+
+    def _check_tensor(self, t, what, elem_bytes, nbytes_needed):
+        if isinstance(t, int):
+            return t                       # raw device pointer: caller's responsibility
+        if not t.is_cuda:
+            raise ValueError(f"{what} must be a device tensor")
+        if not t.is_contiguous():
+            raise ValueError(f"{what} must be contiguous")
+        if elem_bytes and t.element_size() != elem_bytes:
+            raise ValueError(f"{what} must have {elem_bytes}-byte elements for this plan, got {t.dtype}")
+        if t.numel() * t.element_size() < nbytes_needed:
+            raise ValueError(f"{what} too small: {t.numel() * t.element_size()} B < {nbytes_needed} B")
+        if t.device.index != self.ctx.device:
+            raise ValueError(f"{what} is on {t.device}, plan is for device {self.ctx.device}")
+        return t.data_ptr()
 
     def launch(self, coefs, out, stream=None, grid_blocks: int = 0):
         """Enqueue the fused kernel; coefs/out are device tensors (or raw pointers)."""
-        cp = coefs if isinstance(coefs, int) else coefs.data_ptr()
-        op = out if isinstance(out, int) else out.data_ptr()
+        cp = self._check_tensor(coefs, "coefs", self.coef_elem_bytes, self.coef_elems_needed * self.coef_elem_bytes)
+        op = self._check_tensor(out, "out", 0, self.out_bytes_needed)
         check(self.lib.hjd_plan_launch(self.handle, cp, op, _stream_ptr(stream), grid_blocks), "hjd_plan_launch")
 
     def close(self):

@@ -157,7 +157,7 @@ def synthetic_coefs(width, height, sampling, seed=0, quality_scale=1.0):
     qnat = np.zeros((3, 64), np.int32)
     qnat[:, ZIGZAG] = qt
     coef_nat = np.rint(F / qnat[comp]).astype(np.int32)
-    coefs = coef_nat[:, ZIGZAG].astype(np.int16)
+    coefs = np.ascontiguousarray(coef_nat[:, ZIGZAG].astype(np.int16))
     return coefs, qt
 
 
