@@ -94,6 +94,9 @@ int hjd_frame_blocks(int width, int height, int sampling, int64_t* nblocks);
 int hjd_plan_create(hjd_ctx* ctx, const hjd_frame* frames, int nframes, int input_format,
                     const int32_t* qtables, int nq, hjd_plan** out);
 int hjd_plan_destroy(hjd_plan* plan);
+/* Tuning hook: kernel variant bits (0 = default).  bit 0: plain instead of
+ * non-temporal output stores.  Results are identical for every variant. */
+int hjd_plan_set_variant(hjd_plan* plan, int variant);
 int64_t hjd_plan_tasks(const hjd_plan* plan);      /* work items (strips) */
 int64_t hjd_plan_pixels(const hjd_plan* plan);     /* visible pixels */
 int64_t hjd_plan_coef_bytes(const hjd_plan* plan); /* algorithmic input bytes */

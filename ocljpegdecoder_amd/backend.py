@@ -161,6 +161,10 @@ class Plan:
             raise ValueError(f"{what} is on {t.device}, plan is for device {self.ctx.device}")
         return t.data_ptr()
 
+    def set_variant(self, variant: int):
+        """Kernel variant bits (tuning/A-B only; outputs are identical)."""
+        check(self.lib.hjd_plan_set_variant(self.handle, int(variant)), "hjd_plan_set_variant")
+
     def launch(self, coefs, out, stream=None, grid_blocks: int = 0):
         """Enqueue the fused kernel; coefs/out are device tensors (or raw pointers)."""
         cp = self._check_tensor(coefs, "coefs", self.coef_elem_bytes, self.coef_elems_needed * self.coef_elem_bytes)

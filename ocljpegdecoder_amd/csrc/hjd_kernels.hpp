@@ -22,10 +22,12 @@ namespace hjd {
 
 constexpr int kTaskBlocks = 48;      // blocks per task (6 rounds x 8 lane groups)
 constexpr int kSlotBytes = 144;      // LDS bytes per block slot (128 + 16 pad: bank spread)
-constexpr int kRowBufBlock = 288;    // LDS bytes per block in the transpose buffer (256 + 32)
-constexpr int kWaveLds = kTaskBlocks * kSlotBytes + 8 * kRowBufBlock;  // 9216
+constexpr int kRowStride = 48;       // transpose buffer: bytes per row (b128 row writes conflict-free)
+constexpr int kRowBufBlock = 416;    // transpose buffer: bytes per block (104 dwords = 8 mod 32 banks)
+constexpr int kWaveLds = kTaskBlocks * kSlotBytes + 8 * kRowBufBlock;  // 10240
 constexpr int kWavesPerGroup = 4;
 constexpr int kGroupThreads = 64 * kWavesPerGroup;
+static_assert(kWavesPerGroup * kWaveLds * 4 <= 160 * 1024, "4 groups per CU must fit the 160 KiB LDS");
 
 // Device-side frame record built by hjd_plan_create.
 struct FrameDev {
@@ -44,7 +46,6 @@ static_assert(sizeof(FrameDev) == 64, "FrameDev layout");
 // Natural index n -> zigzag position (inverse of the JPEG zigzag, src/zigzag.h).
 __device__ __forceinline__ int zz_of_natural(int n)
 {
-    // packed 6-bit table, 64 entries
     constexpr unsigned char kInv[64] = {
         0,  1,  5,  6,  14, 15, 27, 28, 2,  4,  7,  13, 16, 26, 29, 42,
         3,  8,  12, 17, 25, 30, 41, 43, 9,  11, 18, 24, 31, 40, 44, 53,
@@ -63,24 +64,91 @@ __device__ __forceinline__ void wave_lds_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Binary search of the frame owning global task `task` (wave-uniform).
-__device__ __forceinline__ int find_frame(const FrameDev* __restrict__ fr, int nframes, int64_t task)
+// Wave-uniform view of the frame that owns a task range (lives in SGPRs).
+struct FrameCursor {
+    int idx;
+    int64_t begin, end;      // [begin, end) global task ids of this frame
+    int64_t coef_base, out_base;
+    int width, height, pitch, mcu_w, strips, vec_ok;
+    int qt0, qt1, qt2;
+};
+
+__device__ __forceinline__ void cursor_load(FrameCursor& c, const FrameDev* __restrict__ fr, int nframes,
+                                            int64_t total, int i)
+{
+    const FrameDev& f = fr[i];
+    c.idx = i;
+    c.begin = f.task_begin;
+    c.end = (i + 1 < nframes) ? fr[i + 1].task_begin : total;
+    c.coef_base = f.coef_base;
+    c.out_base = f.out_base;
+    c.width = f.width;
+    c.height = f.height;
+    c.pitch = f.pitch;
+    c.mcu_w = f.mcu_w;
+    c.strips = f.strips;
+    c.vec_ok = f.vec_ok;
+    c.qt0 = f.qt[0];
+    c.qt1 = f.qt[1];
+    c.qt2 = f.qt[2];
+}
+
+// Scalar binary search for the frame owning `task` (once per wave).
+__device__ __forceinline__ void cursor_seek(FrameCursor& c, const FrameDev* __restrict__ fr, int nframes,
+                                            int64_t total, int64_t task)
 {
     int lo = 0, hi = nframes - 1;
     while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
         if (fr[mid].task_begin <= task) lo = mid; else hi = mid - 1;
     }
-    return lo;
+    cursor_load(c, fr, nframes, total, lo);
 }
 
-// Store 4 horizontally adjacent BGRX pixels (cropping at the frame edge).
-__device__ __forceinline__ void store4(uint8_t* __restrict__ row, int x, int width, bool vec_ok,
-                                       uint32_t p0, uint32_t p1, uint32_t p2, uint32_t p3)
+// Where a task's strip sits in its frame.
+struct TaskGeom {
+    int64_t blk0;   // first coefficient block (global)
+    int nblk;       // blocks in the strip (48, fewer on the right edge)
+    int y_base;     // first pixel row
+    int x_base;     // first pixel column
+};
+
+template <int kSampling>
+__device__ __forceinline__ TaskGeom task_geom(const FrameCursor& c, int64_t task)
+{
+    constexpr int kMcuPerTask = kSampling == 1 ? 8 : 16;
+    constexpr int kBpm = kSampling == 1 ? 6 : 3;
+    constexpr int kMcuPx = kSampling == 1 ? 16 : 8;
+    const int local = static_cast<int>(task - c.begin);
+    const int my = local / c.strips;
+    const int mx0 = (local - my * c.strips) * kMcuPerTask;
+    TaskGeom g;
+    g.nblk = min(kMcuPerTask, c.mcu_w - mx0) * kBpm;
+    g.blk0 = c.coef_base + (static_cast<int64_t>(my) * c.mcu_w + mx0) * kBpm;
+    g.y_base = my * kMcuPx;
+    g.x_base = mx0 * kMcuPx;
+    return g;
+}
+
+// Kernel variants (hjd_plan_set_variant): bit 0 = plain instead of
+// non-temporal 16-byte output stores.
+constexpr int kVarPlainStores = 1;
+
+// 4 horizontally adjacent BGRX pixels.  kFull: the whole strip row lies inside
+// the frame and rows are 16-byte aligned -> one global_store_dwordx4 (nt by
+// default: the output is streamed and never re-read by the kernel).
+template <bool kFull, int kVariant = 0>
+__device__ __forceinline__ void store4(uint8_t* __restrict__ row, int x, int width, uint32_t p0, uint32_t p1,
+                                       uint32_t p2, uint32_t p3)
 {
     uint32_t* dst = reinterpret_cast<uint32_t*>(row) + x;
-    if (vec_ok && x + 4 <= width) {
-        *reinterpret_cast<uint4*>(dst) = make_uint4(p0, p1, p2, p3);
+    if constexpr (kFull) {
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 v = {p0, p1, p2, p3};
+        if constexpr (kVariant & kVarPlainStores)
+            *reinterpret_cast<u32x4*>(dst) = v;
+        else
+            __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst));
     } else {
         if (x + 0 < width) dst[0] = p0;
         if (x + 1 < width) dst[1] = p1;
@@ -90,9 +158,12 @@ __device__ __forceinline__ void store4(uint8_t* __restrict__ row, int x, int wid
 }
 
 // Colour stage of one task (samples are int16, row-major, in the block slots).
-template <int kSampling>
+// 4:2:0: lane = 4 px x 2 rows (one chroma row shared by both); 4 iterations
+// cover the 128x16 strip, each wave store instruction writes two 512-byte row
+// segments.  4:4:4: same lane shape over a 128x8 strip.
+template <int kSampling, bool kFull, int kVariant>
 __device__ __forceinline__ void colour_stage(const char* __restrict__ slots, int lane, uint8_t* __restrict__ out,
-                                             const FrameDev& f, int y_base, int x_base)
+                                             int pitch, int width, int height, int y_base, int x_base)
 {
     const int cg = lane & 31;     // 4-pixel column group within the 128-px strip
     const int x0 = cg * 4;
@@ -113,16 +184,14 @@ __device__ __forceinline__ void colour_stage(const char* __restrict__ slots, int
             const ChromaTerms c0 = chroma_terms(static_cast<short>(cu), static_cast<short>(cv));
             const ChromaTerms c1 = chroma_terms(cu >> 16, cv >> 16);
             const int ya0 = y_base + y0;
-            if (ya0 < f.height) {
-                store4(out + static_cast<int64_t>(ya0) * f.pitch, xa, f.width, f.vec_ok,
-                       pixel_bgrx(static_cast<short>(ya.x), c0), pixel_bgrx(ya.x >> 16, c0),
-                       pixel_bgrx(static_cast<short>(ya.y), c1), pixel_bgrx(ya.y >> 16, c1));
-            }
-            if (ya0 + 1 < f.height) {
-                store4(out + static_cast<int64_t>(ya0 + 1) * f.pitch, xa, f.width, f.vec_ok,
-                       pixel_bgrx(static_cast<short>(yb.x), c0), pixel_bgrx(yb.x >> 16, c0),
-                       pixel_bgrx(static_cast<short>(yb.y), c1), pixel_bgrx(yb.y >> 16, c1));
-            }
+            uint8_t* row0 = out + static_cast<int64_t>(ya0) * pitch;
+            if (kFull || ya0 < height)
+                store4<kFull, kVariant>(row0, xa, width, pixel_bgrx(static_cast<short>(ya.x), c0), pixel_bgrx(ya.x >> 16, c0),
+                              pixel_bgrx(static_cast<short>(ya.y), c1), pixel_bgrx(ya.y >> 16, c1));
+            if (kFull || ya0 + 1 < height)
+                store4<kFull, kVariant>(row0 + pitch, xa, width, pixel_bgrx(static_cast<short>(yb.x), c0),
+                              pixel_bgrx(yb.x >> 16, c0), pixel_bgrx(static_cast<short>(yb.y), c1),
+                              pixel_bgrx(yb.y >> 16, c1));
         }
     } else {
         const int m = cg >> 1;        // MCU within strip (16 x 8 px)
@@ -138,14 +207,14 @@ __device__ __forceinline__ void colour_stage(const char* __restrict__ slots, int
                 const int2 su = *reinterpret_cast<const int2*>(base + kSlotBytes);
                 const int2 sv = *reinterpret_cast<const int2*>(base + 2 * kSlotBytes);
                 const int ya = y_base + y;
-                if (ya < f.height) {
+                if (kFull || ya < height) {
                     const uint32_t q0 = pixel_bgrx(static_cast<short>(sy.x),
                                                    chroma_terms(static_cast<short>(su.x), static_cast<short>(sv.x)));
                     const uint32_t q1 = pixel_bgrx(sy.x >> 16, chroma_terms(su.x >> 16, sv.x >> 16));
                     const uint32_t q2 = pixel_bgrx(static_cast<short>(sy.y),
                                                    chroma_terms(static_cast<short>(su.y), static_cast<short>(sv.y)));
                     const uint32_t q3 = pixel_bgrx(sy.y >> 16, chroma_terms(su.y >> 16, sv.y >> 16));
-                    store4(out + static_cast<int64_t>(ya) * f.pitch, xa, f.width, f.vec_ok, q0, q1, q2, q3);
+                    store4<kFull, kVariant>(out + static_cast<int64_t>(ya) * pitch, xa, width, q0, q1, q2, q3);
                 }
             }
         }
@@ -163,7 +232,7 @@ __device__ __forceinline__ constexpr int round_component(int i)
 // LDS slots; kFmt 1: int32 natural rows read straight from global memory.
 // Samples end up as int16 row-major in the block slots.
 template <int kSampling, int kFmt>
-__device__ __forceinline__ void idct_stage(char* __restrict__ slots, int* __restrict__ rowbuf, int lane,
+__device__ __forceinline__ void idct_stage(char* __restrict__ slots, char* __restrict__ rowbuf, int lane,
                                            const int (&zoff)[8], const int (&q)[3][8],
                                            const int* __restrict__ src32, int nblk)
 {
@@ -192,15 +261,15 @@ __device__ __forceinline__ void idct_stage(char* __restrict__ slots, int* __rest
         }
         idct8<false>(v);
         {
-            int4* dst = reinterpret_cast<int4*>(reinterpret_cast<char*>(rowbuf) + g * kRowBufBlock + r * 32);
+            int4* dst = reinterpret_cast<int4*>(rowbuf + g * kRowBufBlock + r * kRowStride);
             dst[0] = make_int4(v[0], v[1], v[2], v[3]);
             dst[1] = make_int4(v[4], v[5], v[6], v[7]);
         }
         wave_lds_sync();
         {
-            const char* col = reinterpret_cast<const char*>(rowbuf) + g * kRowBufBlock + r * 4;
+            const char* col = rowbuf + g * kRowBufBlock + r * 4;
 #pragma unroll
-            for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const int*>(col + k * 32);
+            for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const int*>(col + k * kRowStride);
         }
         idct8<true>(v);
         {
@@ -212,99 +281,98 @@ __device__ __forceinline__ void idct_stage(char* __restrict__ slots, int* __rest
     }
 }
 
-template <int kSampling, int kFmt>
+// The fused kernel.  Persistent grid; wave w owns the contiguous task range
+// [w*T/W, (w+1)*T/W) so its frame changes rarely and the frame record stays in
+// SGPRs; the next task's coefficients are prefetched into VGPRs while the
+// current one is transformed.
+template <int kSampling, int kFmt, int kVariant>
 __global__ __launch_bounds__(kGroupThreads) void decode_kernel(const void* __restrict__ coefs,
                                                               const int* __restrict__ qt_pool,
                                                               const FrameDev* __restrict__ frames, int nframes,
                                                               int64_t total_tasks, uint8_t* __restrict__ out)
 {
     __shared__ __attribute__((aligned(16))) char lds[kWavesPerGroup * kWaveLds];
-    const int wave = threadIdx.x >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     char* slots = lds + wave * kWaveLds;
-    int* rowbuf = reinterpret_cast<int*>(slots + kTaskBlocks * kSlotBytes);
+    char* rowbuf = slots + kTaskBlocks * kSlotBytes;
     const int r = lane & 7;
+
+    // this wave's contiguous task range
+    const int64_t nwaves = static_cast<int64_t>(gridDim.x) * kWavesPerGroup;
+    const int64_t gw = static_cast<int64_t>(blockIdx.x) * kWavesPerGroup + wave;
+    const int64_t chunk = total_tasks / nwaves, rem = total_tasks % nwaves;
+    const int64_t t_begin = gw * chunk + min(gw, rem);
+    const int64_t t_end = t_begin + chunk + (gw < rem ? 1 : 0);
+    if (t_begin >= t_end) return;
 
     int zoff[8];
 #pragma unroll
     for (int c = 0; c < 8; ++c) zoff[c] = 2 * zz_of_natural(r * 8 + c);
 
-    const int64_t nwaves = static_cast<int64_t>(gridDim.x) * kWavesPerGroup;
-    int64_t task = static_cast<int64_t>(blockIdx.x) * kWavesPerGroup + wave;
-
-    constexpr int kMcuPerTask = kSampling == 1 ? 8 : 16;
-    constexpr int kBpm = kSampling == 1 ? 6 : 3;
-    constexpr int kMcuPx = kSampling == 1 ? 16 : 8;
-
-    int cur_frame = -1;
     int q[3][8];
+    int q_tables[3] = {-1, -1, -1};
 #pragma unroll
     for (int c = 0; c < 3; ++c)
 #pragma unroll
         for (int k = 0; k < 8; ++k) q[c][k] = 0;
 
-    // prefetch registers (kFmt 0 only): 6 x 16 B per lane = 6 KiB per wave
-    int4 pre[6];
-    auto locate = [&](int64_t t, int& fi, int64_t& blk0, int& nblk, int& my, int& mx0) {
-        fi = find_frame(frames, nframes, t);
-        const FrameDev& f = frames[fi];
-        const int64_t local = t - f.task_begin;
-        my = static_cast<int>(local / f.strips);
-        const int s = static_cast<int>(local - static_cast<int64_t>(my) * f.strips);
-        mx0 = s * kMcuPerTask;
-        const int nmcu = min(kMcuPerTask, f.mcu_w - mx0);
-        nblk = nmcu * kBpm;
-        blk0 = f.coef_base + (static_cast<int64_t>(my) * f.mcu_w + mx0) * kBpm;
-    };
-    auto prefetch = [&](int64_t t) {
-        int fi, nblk, my, mx0;
-        int64_t blk0;
-        locate(t, fi, blk0, nblk, my, mx0);
-        const int4* src = reinterpret_cast<const int4*>(static_cast<const short*>(coefs) + blk0 * 64);
-#pragma unroll
-        for (int k = 0; k < 6; ++k) {
-            const int j = lane + 64 * k;   // 16-byte chunk index within the task
-            pre[k] = (j < nblk * 8) ? src[j] : make_int4(0, 0, 0, 0);
-        }
-    };
+    FrameCursor pc;   // frame of the task being prefetched
+    cursor_seek(pc, frames, nframes, total_tasks, t_begin);
 
-    if constexpr (kFmt == 0) {
-        if (task < total_tasks) prefetch(task);
-    }
-
-    for (; task < total_tasks; task += nwaves) {
-        int fi, nblk, my, mx0;
-        int64_t blk0;
-        locate(task, fi, blk0, nblk, my, mx0);
-        const FrameDev& f = frames[fi];
-        if (kFmt == 0 && fi != cur_frame) {   // wave-uniform: (re)load this lane's qtable rows
-            cur_frame = fi;
+    int4 pre[6];      // prefetch registers (kFmt 0): 6 x 16 B per lane = 6 KiB per wave
+    auto prefetch = [&](const TaskGeom& g) {
+        const int4* src = reinterpret_cast<const int4*>(static_cast<const short*>(coefs) + g.blk0 * 64);
+        if (g.nblk == kTaskBlocks) {
 #pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                const int4* qp = reinterpret_cast<const int4*>(qt_pool + f.qt[c] * 64 + r * 8);
-                const int4 a = qp[0], b = qp[1];
-                q[c][0] = a.x; q[c][1] = a.y; q[c][2] = a.z; q[c][3] = a.w;
-                q[c][4] = b.x; q[c][5] = b.y; q[c][6] = b.z; q[c][7] = b.w;
+            for (int k = 0; k < 6; ++k) pre[k] = src[lane + 64 * k];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+                const int j = lane + 64 * k;   // 16-byte chunk index within the task
+                pre[k] = (j < g.nblk * 8) ? src[j] : make_int4(0, 0, 0, 0);
             }
         }
+    };
+    if constexpr (kFmt == 0) prefetch(task_geom<kSampling>(pc, t_begin));
 
-        const int* src32 = nullptr;
+    for (int64_t task = t_begin; task < t_end; ++task) {
+        const FrameCursor cc = pc;
+        const TaskGeom tg = task_geom<kSampling>(cc, task);
         if constexpr (kFmt == 0) {
+            if (cc.qt0 != q_tables[0] || cc.qt1 != q_tables[1] || cc.qt2 != q_tables[2]) {
+                q_tables[0] = cc.qt0; q_tables[1] = cc.qt1; q_tables[2] = cc.qt2;
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    const int4* qp = reinterpret_cast<const int4*>(qt_pool + q_tables[c] * 64 + r * 8);
+                    const int4 a = qp[0], b = qp[1];
+                    q[c][0] = a.x; q[c][1] = a.y; q[c][2] = a.z; q[c][3] = a.w;
+                    q[c][4] = b.x; q[c][5] = b.y; q[c][6] = b.z; q[c][7] = b.w;
+                }
+            }
 #pragma unroll
             for (int k = 0; k < 6; ++k) {
                 const int j = lane + 64 * k;
                 *reinterpret_cast<int4*>(slots + (j >> 3) * kSlotBytes + (j & 7) * 16) = pre[k];
             }
             wave_lds_sync();
-            const int64_t next = task + nwaves;
-            if (next < total_tasks) prefetch(next);
+            if (task + 1 < t_end) {
+                if (task + 1 >= pc.end) cursor_load(pc, frames, nframes, total_tasks, pc.idx + 1);
+                prefetch(task_geom<kSampling>(pc, task + 1));
+            }
         } else {
-            src32 = static_cast<const int*>(coefs) + blk0 * 64;
+            if (task + 1 < t_end && task + 1 >= pc.end) cursor_load(pc, frames, nframes, total_tasks, pc.idx + 1);
         }
 
-        idct_stage<kSampling, kFmt>(slots, rowbuf, lane, zoff, q, src32, nblk);
+        idct_stage<kSampling, kFmt>(slots, rowbuf, lane, zoff, q,
+                                    static_cast<const int*>(coefs) + tg.blk0 * 64, tg.nblk);
 
-        colour_stage<kSampling>(slots, lane, out + f.out_base, f, my * kMcuPx, mx0 * kMcuPx);
+        constexpr int kRows = kSampling == 1 ? 16 : 8;
+        uint8_t* fout = out + cc.out_base;
+        if (cc.vec_ok && tg.x_base + 128 <= cc.width && tg.y_base + kRows <= cc.height)
+            colour_stage<kSampling, true, kVariant>(slots, lane, fout, cc.pitch, cc.width, cc.height, tg.y_base, tg.x_base);
+        else
+            colour_stage<kSampling, false, kVariant>(slots, lane, fout, cc.pitch, cc.width, cc.height, tg.y_base, tg.x_base);
         wave_lds_sync();
     }
 }
@@ -316,7 +384,7 @@ __global__ __launch_bounds__(kGroupThreads) void idct_blocks_kernel(const int* _
     __shared__ __attribute__((aligned(16))) char lds[kWavesPerGroup * 8 * kRowBufBlock];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int g = lane >> 3, r = lane & 7;
-    int* rowbuf = reinterpret_cast<int*>(lds + wave * 8 * kRowBufBlock);
+    char* rowbuf = lds + wave * 8 * kRowBufBlock;
     const int64_t ngroups = (nblocks + 7) / 8;
     for (int64_t grp = static_cast<int64_t>(blockIdx.x) * kWavesPerGroup + wave; grp < ngroups;
          grp += static_cast<int64_t>(gridDim.x) * kWavesPerGroup) {
@@ -330,13 +398,13 @@ __global__ __launch_bounds__(kGroupThreads) void idct_blocks_kernel(const int* _
             v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
         }
         idct8<false>(v);
-        int4* dst = reinterpret_cast<int4*>(reinterpret_cast<char*>(rowbuf) + g * kRowBufBlock + r * 32);
+        int4* dst = reinterpret_cast<int4*>(rowbuf + g * kRowBufBlock + r * kRowStride);
         dst[0] = make_int4(v[0], v[1], v[2], v[3]);
         dst[1] = make_int4(v[4], v[5], v[6], v[7]);
         wave_lds_sync();
-        const char* col = reinterpret_cast<const char*>(rowbuf) + g * kRowBufBlock + r * 4;
+        const char* col = rowbuf + g * kRowBufBlock + r * 4;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const int*>(col + k * 32);
+        for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const int*>(col + k * kRowStride);
         wave_lds_sync();
         idct8<true>(v);
         if (valid) {

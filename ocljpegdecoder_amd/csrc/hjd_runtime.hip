@@ -66,6 +66,7 @@ struct hjd_plan {
     int64_t coef_bytes = 0;
     FrameDev* d_frames = nullptr;
     int* d_qt = nullptr;        // natural-order tables [nq][64]
+    int variant = 0;            // kernel variant bits (hjd_plan_set_variant)
 };
 
 extern "C" {
@@ -228,6 +229,14 @@ int hjd_plan_destroy(hjd_plan* plan)
     return HJD_OK;
 }
 
+int hjd_plan_set_variant(hjd_plan* plan, int variant)
+{
+    if (!plan) return fail(HJD_E_INVALID, "plan is NULL");
+    if (variant < 0 || variant > 1) return fail(HJD_E_INVALID, "unknown kernel variant %d", variant);
+    plan->variant = variant;
+    return HJD_OK;
+}
+
 int64_t hjd_plan_tasks(const hjd_plan* plan) { return plan ? plan->tasks : -1; }
 int64_t hjd_plan_pixels(const hjd_plan* plan) { return plan ? plan->pixels : -1; }
 int64_t hjd_plan_coef_bytes(const hjd_plan* plan) { return plan ? plan->coef_bytes : -1; }
@@ -251,21 +260,15 @@ int hjd_plan_launch(hjd_plan* plan, const void* d_coefs, void* d_out, void* stre
     hipStream_t s = static_cast<hipStream_t>(stream);
     uint8_t* out = static_cast<uint8_t*>(d_out);
     const dim3 gdim(grid), bdim(hjd::kGroupThreads);
-    if (plan->input_format == HJD_IN_Q16_ZIGZAG) {
-        if (plan->sampling == HJD_YUV420)
-            hipLaunchKernelGGL((hjd::decode_kernel<1, 0>), gdim, bdim, 0, s, d_coefs, plan->d_qt, plan->d_frames,
-                               plan->nframes, plan->tasks, out);
-        else
-            hipLaunchKernelGGL((hjd::decode_kernel<0, 0>), gdim, bdim, 0, s, d_coefs, plan->d_qt, plan->d_frames,
-                               plan->nframes, plan->tasks, out);
-    } else {
-        if (plan->sampling == HJD_YUV420)
-            hipLaunchKernelGGL((hjd::decode_kernel<1, 1>), gdim, bdim, 0, s, d_coefs, plan->d_qt, plan->d_frames,
-                               plan->nframes, plan->tasks, out);
-        else
-            hipLaunchKernelGGL((hjd::decode_kernel<0, 1>), gdim, bdim, 0, s, d_coefs, plan->d_qt, plan->d_frames,
-                               plan->nframes, plan->tasks, out);
-    }
+    const int fmt = plan->input_format == HJD_IN_Q16_ZIGZAG ? 0 : 1;
+    const int key = (plan->sampling == HJD_YUV420 ? 4 : 0) | (fmt << 1) | (plan->variant & 1);
+    using K = void (*)(const void*, const int*, const FrameDev*, int, int64_t, uint8_t*);
+    static const K kTable[8] = {
+        hjd::decode_kernel<0, 0, 0>, hjd::decode_kernel<0, 0, 1>, hjd::decode_kernel<0, 1, 0>,
+        hjd::decode_kernel<0, 1, 1>, hjd::decode_kernel<1, 0, 0>, hjd::decode_kernel<1, 0, 1>,
+        hjd::decode_kernel<1, 1, 0>, hjd::decode_kernel<1, 1, 1>};
+    hipLaunchKernelGGL(kTable[key], gdim, bdim, 0, s, d_coefs, plan->d_qt, plan->d_frames, plan->nframes,
+                       plan->tasks, out);
     HJD_HIP(hipGetLastError());
     return HJD_OK;
 }
