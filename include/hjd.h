@@ -104,7 +104,7 @@ int64_t hjd_plan_coef_bytes(const hjd_plan* plan); /* algorithmic input bytes */
 /*
  * Enqueue the fused decode of every frame of the plan on `stream` (async).
  * d_coefs: coefficient buffer (int16 or int32 per the plan's format);
- * d_out: output buffer (frames at their out_offset).
+ * d_out: output buffer (frames at their out_offset).  Both 16-byte aligned.
  * grid_blocks: persistent grid size in 256-thread workgroups (0 = default).
  * The input is never modified (the reference kernel's in-place IDCT,
  * src/idct8x8.cl:136-155, is not reproduced).

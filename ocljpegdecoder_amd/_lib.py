@@ -121,6 +121,13 @@ def _bind_host(lib):
                                                  ctypes.POINTER(ctypes.POINTER(ctypes.c_int16)), ctypes.c_int64,
                                                  ctypes.c_int, c_i32p]),
     }
+    vp = ctypes.c_void_p
+    sigs.update({
+        "hjd_stream_create": (ctypes.c_int, [vp, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]),
+        "hjd_stream_destroy": (ctypes.c_int, [vp]),
+        "hjd_stream_submit": (ctypes.c_int, [vp, u8p, ctypes.c_size_t, vp, ctypes.c_int32]),
+        "hjd_stream_sync": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int64)]),
+    })
     for name, (res, args) in sigs.items():
         fn = getattr(lib, name, None)
         if fn is not None:

@@ -18,14 +18,23 @@ constexpr int kC1 = 2841, kC2 = 2676, kC3 = 2408, kC5 = 1609, kC6 = 1108, kC7 = 
 // block's coefficient energy is bounded by its output energy (|out| <= 512 per
 // sample => ||coef||_2 <= ~4.1e3), so stage-1/2 operands of the row pass are
 // < 2^14 and of the column pass (row outputs, gain 8*sqrt(8)) < 2^18.
-__device__ __forceinline__ int mul24(int a, int b) { return __mul24(a, b); }
+// The host build (the idct.h CPU entry points share this code) multiplies in
+// plain 32-bit int, which is the same value on that domain.
+__host__ __device__ __forceinline__ int mul24(int a, int b)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __mul24(a, b);
+#else
+    return a * b;
+#endif
+}
 
 // The stage-3 products 181*(a4 +- a5) can exceed 24 bits on the legal domain,
 // so they use a full 32-bit multiply (low 32 bits = the reference's int math).
-__device__ __forceinline__ int mul181(int x) { return x * 181; }
+__host__ __device__ __forceinline__ int mul181(int x) { return x * 181; }
 
 // min/max pairs lower to one v_med3_i32
-__device__ __forceinline__ int clamp_sample(int v) { return min(max(v, -256), 255); }
+__host__ __device__ __forceinline__ int clamp_sample(int v) { return v < -256 ? -256 : (v > 255 ? 255 : v); }
 __device__ __forceinline__ int clamp_u8(int v) { return min(max(v, 0), 255); }
 
 // One 8-point pass on natural-order values v[0..7] (in place).
@@ -37,7 +46,7 @@ __device__ __forceinline__ int clamp_u8(int v) { return min(max(v, 0), 255); }
 // The reference's DC-only short-cuts (:40-45, :86-92) give exactly the values
 // of the full butterfly, so the kernel always runs the full butterfly.
 template <bool kCol>
-__device__ __forceinline__ void idct8(int (&v)[8])
+__host__ __device__ __forceinline__ void idct8(int (&v)[8])
 {
     constexpr int kIn = kCol ? 8 : 11;
     constexpr int kRnd = kCol ? 4 : 0;

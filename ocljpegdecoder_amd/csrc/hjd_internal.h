@@ -1,0 +1,35 @@
+// hjd_internal.h -- helpers shared by the translation units of libhjd.so.
+#pragma once
+#include <stdint.h>
+
+struct hjd_ctx;
+
+namespace hjd_internal {
+
+// Record the calling thread's last error (returned by hjd_last_error()) and
+// return `code`.  Defined in hjd_runtime.hip.
+int set_error(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+
+// Device frame record of the fused kernel (layout of hjd::FrameDev).
+struct FrameRecord {
+    int64_t coef_base, out_base, task_begin;
+    int32_t width, height, pitch, sampling, mcu_w, strips;
+    int32_t qt[3];
+    int32_t vec_ok;
+};
+
+// Fill a one-frame record (task_begin 0); returns the frame's task count, or
+// a negative status for an unsupported geometry.
+int64_t make_frame_record(int width, int height, int sampling, int64_t coef_base, int64_t out_base, int pitch,
+                          const int qt_index[3], FrameRecord* rec);
+
+// Launch the fused kernel on device-resident frame records / natural-order
+// qtables (no host synchronisation, safe to call from any host thread).
+int launch_decode(int device, int num_cu, int sampling, int input_format, int variant, const void* d_coefs,
+                  const int32_t* d_qt_nat, const FrameRecord* d_frames, int nframes, int64_t tasks, void* d_out,
+                  void* stream, int grid_blocks);
+
+// hjd_ctx accessors for the other translation units
+int ctx_num_cu(const struct ::hjd_ctx* ctx);
+
+}  // namespace hjd_internal

@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "hjd.h"
+#include "hjd_internal.h"
 #include "hjd_kernels.hpp"
 
 using hjd::FrameDev;
@@ -51,6 +52,17 @@ constexpr int kZigzag[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18,
 
 }  // namespace
 
+int hjd_internal::set_error(int code, const char* fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
+
 struct hjd_ctx {
     int device = 0;
     int num_cu = 256;
@@ -68,6 +80,56 @@ struct hjd_plan {
     int* d_qt = nullptr;        // natural-order tables [nq][64]
     int variant = 0;            // kernel variant bits (hjd_plan_set_variant)
 };
+
+static int geometry(int width, int height, int sampling, int& mcu_w, int& mcu_h, int& bpm, int& mpx);
+static int default_grid_cu(int num_cu, int64_t work_waves);
+
+int hjd_internal::ctx_num_cu(const hjd_ctx* ctx) { return ctx->num_cu; }
+
+int64_t hjd_internal::make_frame_record(int width, int height, int sampling, int64_t coef_base, int64_t out_base,
+                                        int pitch, const int qt_index[3], FrameRecord* rec)
+{
+    int mw, mh, bpm, mpx;
+    int rc = geometry(width, height, sampling, mw, mh, bpm, mpx);
+    if (rc) return rc;
+    static_assert(sizeof(FrameRecord) == sizeof(FrameDev), "record layout");
+    FrameDev d;
+    memset(&d, 0, sizeof(d));
+    const int tasks_mcus = sampling == HJD_YUV420 ? 8 : 16;
+    d.coef_base = coef_base;
+    d.out_base = out_base;
+    d.task_begin = 0;
+    d.width = width;
+    d.height = height;
+    d.pitch = pitch;
+    d.sampling = sampling;
+    d.mcu_w = mw;
+    d.strips = (mw + tasks_mcus - 1) / tasks_mcus;
+    for (int c = 0; c < 3; ++c) d.qt[c] = qt_index ? qt_index[c] : 0;
+    d.vec_ok = ((pitch & 15) == 0 && (out_base & 15) == 0) ? 1 : 0;
+    memcpy(rec, &d, sizeof(d));
+    return static_cast<int64_t>(d.strips) * mh;
+}
+
+int hjd_internal::launch_decode(int device, int num_cu, int sampling, int input_format, int variant,
+                                const void* d_coefs, const int32_t* d_qt_nat, const FrameRecord* d_frames,
+                                int nframes, int64_t tasks, void* d_out, void* stream, int grid_blocks)
+{
+    HJD_HIP(hipSetDevice(device));
+    const int grid = grid_blocks > 0 ? grid_blocks : default_grid_cu(num_cu, tasks);
+    const int fmt = input_format == HJD_IN_Q16_ZIGZAG ? 0 : 1;
+    const int key = (sampling == HJD_YUV420 ? 4 : 0) | (fmt << 1) | (variant & 1);
+    using K = void (*)(const void*, const int*, const FrameDev*, int, int64_t, uint8_t*);
+    static const K kTable[8] = {
+        hjd::decode_kernel<0, 0, 0>, hjd::decode_kernel<0, 0, 1>, hjd::decode_kernel<0, 1, 0>,
+        hjd::decode_kernel<0, 1, 1>, hjd::decode_kernel<1, 0, 0>, hjd::decode_kernel<1, 0, 1>,
+        hjd::decode_kernel<1, 1, 0>, hjd::decode_kernel<1, 1, 1>};
+    hipLaunchKernelGGL(kTable[key], dim3(grid), dim3(hjd::kGroupThreads), 0, static_cast<hipStream_t>(stream),
+                       d_coefs, d_qt_nat, reinterpret_cast<const FrameDev*>(d_frames), nframes, tasks,
+                       static_cast<uint8_t*>(d_out));
+    HJD_HIP(hipGetLastError());
+    return HJD_OK;
+}
 
 extern "C" {
 
@@ -241,9 +303,16 @@ int64_t hjd_plan_tasks(const hjd_plan* plan) { return plan ? plan->tasks : -1; }
 int64_t hjd_plan_pixels(const hjd_plan* plan) { return plan ? plan->pixels : -1; }
 int64_t hjd_plan_coef_bytes(const hjd_plan* plan) { return plan ? plan->coef_bytes : -1; }
 
+static int default_grid_cu(int num_cu, int64_t work_waves)
+{
+    // 4 resident 256-thread groups per CU (16 waves/CU; LDS 40 KiB per group).
+    const int64_t cap = static_cast<int64_t>(num_cu) * 4;
+    const int64_t need = (work_waves + hjd::kWavesPerGroup - 1) / hjd::kWavesPerGroup;
+    return static_cast<int>(std::max<int64_t>(1, std::min(cap, need)));
+}
+
 static int default_grid(const hjd_ctx* ctx, int64_t work_waves)
 {
-    // 4 resident 256-thread groups per CU (16 waves/CU; LDS 36 KiB per group).
     const int64_t cap = static_cast<int64_t>(ctx->num_cu) * 4;
     const int64_t need = (work_waves + hjd::kWavesPerGroup - 1) / hjd::kWavesPerGroup;
     return static_cast<int>(std::max<int64_t>(1, std::min(cap, need)));
@@ -254,23 +323,13 @@ int hjd_plan_launch(hjd_plan* plan, const void* d_coefs, void* d_out, void* stre
     if (!plan) return fail(HJD_E_INVALID, "plan is NULL");
     if (plan->tasks == 0) return HJD_OK;
     if (!d_coefs || !d_out) return fail(HJD_E_INVALID, "NULL device buffer");
+    if ((reinterpret_cast<uintptr_t>(d_coefs) | reinterpret_cast<uintptr_t>(d_out)) & 15)
+        return fail(HJD_E_INVALID, "device buffers must be 16-byte aligned");
     if (grid_blocks < 0) return fail(HJD_E_INVALID, "grid_blocks < 0");
-    HJD_HIP(hipSetDevice(plan->ctx->device));
-    const int grid = grid_blocks > 0 ? grid_blocks : default_grid(plan->ctx, plan->tasks);
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    uint8_t* out = static_cast<uint8_t*>(d_out);
-    const dim3 gdim(grid), bdim(hjd::kGroupThreads);
-    const int fmt = plan->input_format == HJD_IN_Q16_ZIGZAG ? 0 : 1;
-    const int key = (plan->sampling == HJD_YUV420 ? 4 : 0) | (fmt << 1) | (plan->variant & 1);
-    using K = void (*)(const void*, const int*, const FrameDev*, int, int64_t, uint8_t*);
-    static const K kTable[8] = {
-        hjd::decode_kernel<0, 0, 0>, hjd::decode_kernel<0, 0, 1>, hjd::decode_kernel<0, 1, 0>,
-        hjd::decode_kernel<0, 1, 1>, hjd::decode_kernel<1, 0, 0>, hjd::decode_kernel<1, 0, 1>,
-        hjd::decode_kernel<1, 1, 0>, hjd::decode_kernel<1, 1, 1>};
-    hipLaunchKernelGGL(kTable[key], gdim, bdim, 0, s, d_coefs, plan->d_qt, plan->d_frames, plan->nframes,
-                       plan->tasks, out);
-    HJD_HIP(hipGetLastError());
-    return HJD_OK;
+    return hjd_internal::launch_decode(plan->ctx->device, plan->ctx->num_cu, plan->sampling, plan->input_format,
+                                       plan->variant, d_coefs, plan->d_qt,
+                                       reinterpret_cast<const hjd_internal::FrameRecord*>(plan->d_frames),
+                                       plan->nframes, plan->tasks, d_out, stream, grid_blocks);
 }
 
 int hjd_idct_blocks(hjd_ctx* ctx, const int32_t* d_in, int32_t* d_out, int64_t nblocks, void* stream)

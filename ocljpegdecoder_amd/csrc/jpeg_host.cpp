@@ -1,0 +1,399 @@
+// jpeg_host.cpp -- host JPEG front end: markers + Huffman decode (include/hjd_host.h).
+//
+// Produces the fused kernel's input (int16 quantised zigzag coefficients,
+// MCU-major) from a baseline JPEG.  Covers the reference's L2/L3
+// (src/parser.cpp:7-419, src/decoder.cpp:72-365) with a fresh table-driven
+// design: a 64-bit bit accumulator with byte de-stuffing, a 9-bit first-level
+// lookup per Huffman table (canonical MAXCODE/VALPTR search for longer codes,
+// JPEG Annex F.2.2.3), restart-marker resynchronisation, and a thread pool
+// that decodes independent files in parallel.
+#include <atomic>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "hjd.h"
+#include "hjd_host.h"
+#include "hjd_internal.h"
+
+using hjd_internal::set_error;
+
+namespace {
+
+struct HuffTable {
+    bool defined = false;
+    uint16_t fast[512];      // (length << 8) | symbol for codes of <= 9 bits; 0 = slow path
+    int32_t maxcode[18];     // largest code of each length (-1: none)
+    int32_t valptr[17];
+    int32_t mincode[17];
+    uint8_t vals[256];
+};
+
+struct Component {
+    int id = 0, h = 1, v = 1, tq = 0;
+    int td = 0, ta = 0;      // DC / AC Huffman table ids (from SOS)
+};
+
+struct Frame {
+    int width = 0, height = 0, ncomp = 0;
+    Component comp[3];
+    int32_t qt[4][64];
+    int qt_prec[4] = {-1, -1, -1, -1};
+    HuffTable dc[4], ac[4];
+    int restart_interval = 0;
+    int scan_order[3] = {0, 1, 2};   // frame component index of each scan component
+    size_t scan_offset = 0;
+    int sampling = -1;
+};
+
+inline int be16(const uint8_t* p) { return (p[0] << 8) | p[1]; }
+
+int build_table(HuffTable& t, const uint8_t counts[16], const uint8_t* symbols, int nsym)
+{
+    memset(t.fast, 0, sizeof(t.fast));
+    int code = 0, k = 0;
+    for (int len = 1; len <= 16; ++len) {
+        const int n = counts[len - 1];
+        t.valptr[len] = k;
+        t.mincode[len] = code;
+        for (int i = 0; i < n; ++i, ++k, ++code) {
+            if (k >= nsym) return -1;
+            if (code >= (1 << len)) return -1;   // over-subscribed table
+            t.vals[k] = symbols[k];
+            if (len <= 9) {
+                const int shift = 9 - len;
+                for (int j = 0; j < (1 << shift); ++j)
+                    t.fast[(code << shift) | j] = static_cast<uint16_t>((len << 8) | symbols[k]);
+            }
+        }
+        t.maxcode[len] = n ? code - 1 : -1;
+        code <<= 1;
+    }
+    t.maxcode[17] = 0x7fffffff;
+    t.defined = true;
+    return 0;
+}
+
+int parse(const uint8_t* d, size_t n, Frame& f)
+{
+    if (n < 4 || d[0] != 0xFF || d[1] != 0xD8) return set_error(HJD_E_INVALID, "SOI missing");
+    size_t p = 2;
+    bool have_sof = false;
+    for (;;) {
+        while (p < n && d[p] != 0xFF) ++p;           // tolerate garbage between segments
+        while (p < n && d[p] == 0xFF) ++p;           // fill bytes
+        if (p >= n) return set_error(HJD_E_INVALID, "no SOS marker");
+        const uint8_t m = d[p++];
+        if (m == 0xD8 || (m >= 0xD0 && m <= 0xD7) || m == 0x01) continue;   // no length
+        if (m == 0xD9) return set_error(HJD_E_INVALID, "EOI before SOS");
+        if (p + 2 > n) return set_error(HJD_E_INVALID, "truncated marker segment");
+        const int len = be16(d + p);
+        if (len < 2 || p + len > n) return set_error(HJD_E_INVALID, "bad segment length");
+        const uint8_t* s = d + p + 2;
+        const int sl = len - 2;
+        switch (m) {
+        case 0xDB: {   // DQT (src/parser.cpp:47-100; 16-bit entries big-endian per T.81 B.2.4.1)
+            int q = 0;
+            while (q < sl) {
+                const int pq = s[q] >> 4, tq = s[q] & 15;
+                if (pq > 1 || tq > 3) return set_error(HJD_E_INVALID, "bad DQT table %d precision %d", tq, pq);
+                if (q + 1 + 64 * (pq + 1) > sl) return set_error(HJD_E_INVALID, "truncated DQT");
+                for (int i = 0; i < 64; ++i)
+                    f.qt[tq][i] = pq ? be16(s + q + 1 + 2 * i) : s[q + 1 + i];
+                f.qt_prec[tq] = pq;
+                q += 1 + 64 * (pq + 1);
+            }
+            break;
+        }
+        case 0xC0: {   // SOF0 (src/parser.cpp:102-130)
+            if (sl < 6) return set_error(HJD_E_INVALID, "truncated SOF0");
+            if (s[0] != 8) return set_error(HJD_E_INVALID, "unsupported bit depth %d", s[0]);
+            f.height = be16(s + 1);
+            f.width = be16(s + 3);
+            f.ncomp = s[5];
+            if (f.ncomp != 3) return set_error(HJD_E_INVALID, "unsupported number of components %d", f.ncomp);
+            if (sl < 6 + 3 * f.ncomp) return set_error(HJD_E_INVALID, "truncated SOF0");
+            if (f.width <= 0 || f.height <= 0) return set_error(HJD_E_INVALID, "invalid dimensions");
+            for (int c = 0; c < 3; ++c) {
+                f.comp[c].id = s[6 + 3 * c];
+                f.comp[c].h = s[7 + 3 * c] >> 4;
+                f.comp[c].v = s[7 + 3 * c] & 15;
+                f.comp[c].tq = s[8 + 3 * c];
+                if (f.comp[c].tq > 3) return set_error(HJD_E_INVALID, "bad quantisation table id");
+            }
+            // src/decoder.cpp:58-69: only H2V2/H1V1/H1V1 and all-H1V1
+            const Component* c = f.comp;
+            if (c[0].h == 2 && c[0].v == 2 && c[1].h == 1 && c[1].v == 1 && c[2].h == 1 && c[2].v == 1)
+                f.sampling = HJD_YUV420;
+            else if (c[0].h == 1 && c[0].v == 1 && c[1].h == 1 && c[1].v == 1 && c[2].h == 1 && c[2].v == 1)
+                f.sampling = HJD_YUV444;
+            else
+                return set_error(HJD_E_INVALID, "unsupported sampling (only 4:2:0 and 4:4:4)");
+            have_sof = true;
+            break;
+        }
+        case 0xC1: case 0xC2: case 0xC3: case 0xC5: case 0xC6: case 0xC7:
+        case 0xC9: case 0xCA: case 0xCB: case 0xCD: case 0xCE: case 0xCF:
+            return set_error(HJD_E_INVALID, "only baseline (SOF0) JPEG is supported");
+        case 0xC4: {   // DHT (src/parser.cpp:170-270)
+            int q = 0;
+            while (q < sl) {
+                if (q + 17 > sl) return set_error(HJD_E_INVALID, "truncated DHT");
+                const int tc = s[q] >> 4, th = s[q] & 15;
+                if (tc > 1 || th > 3) return set_error(HJD_E_INVALID, "bad DHT class/id");
+                int nsym = 0;
+                for (int i = 0; i < 16; ++i) nsym += s[q + 1 + i];
+                if (nsym > 256 || q + 17 + nsym > sl) return set_error(HJD_E_INVALID, "bad DHT size");
+                HuffTable& t = tc ? f.ac[th] : f.dc[th];
+                if (build_table(t, s + q + 1, s + q + 17, nsym)) return set_error(HJD_E_INVALID, "invalid Huffman table");
+                q += 17 + nsym;
+            }
+            break;
+        }
+        case 0xDD:     // DRI (src/parser.cpp:156-168)
+            if (sl < 2) return set_error(HJD_E_INVALID, "truncated DRI");
+            f.restart_interval = be16(s);
+            break;
+        case 0xDA: {   // SOS (src/parser.cpp:132-154)
+            if (!have_sof) return set_error(HJD_E_INVALID, "SOS before SOF0");
+            if (sl < 1 || s[0] != 3 || sl < 1 + 2 * 3 + 3)
+                return set_error(HJD_E_INVALID, "unsupported scan (needs all 3 components interleaved)");
+            for (int i = 0; i < 3; ++i) {
+                const int cid = s[1 + 2 * i], tdta = s[2 + 2 * i];
+                int fc = -1;
+                for (int c = 0; c < 3; ++c)
+                    if (f.comp[c].id == cid) fc = c;
+                if (fc < 0) return set_error(HJD_E_INVALID, "scan component %d not in frame", cid);
+                f.scan_order[i] = fc;
+                f.comp[fc].td = tdta >> 4;
+                f.comp[fc].ta = tdta & 15;
+                if (f.comp[fc].td > 3 || f.comp[fc].ta > 3) return set_error(HJD_E_INVALID, "bad Huffman table id");
+            }
+            const uint8_t* tail = s + 1 + 2 * 3;
+            if (tail[0] != 0 || tail[1] != 63 || tail[2] != 0)
+                return set_error(HJD_E_INVALID, "not a baseline scan (Ss/Se/Ah/Al)");
+            for (int c = 0; c < 3; ++c) {
+                if (f.qt_prec[f.comp[c].tq] < 0) return set_error(HJD_E_INVALID, "missing quantisation table");
+                if (!f.dc[f.comp[c].td].defined) return set_error(HJD_E_INVALID, "missing DC Huffman table");
+                if (!f.ac[f.comp[c].ta].defined) return set_error(HJD_E_INVALID, "missing AC Huffman table");
+            }
+            f.scan_offset = p + len;
+            return HJD_OK;
+        }
+        default:       // APPn, COM, DNL, ...: skip (src/parser.cpp:295-322 skips APPn)
+            break;
+        }
+        p += len;
+    }
+}
+
+void fill_info(const Frame& f, hjd_jpeg_info* info)
+{
+    memset(info, 0, sizeof(*info));
+    info->width = f.width;
+    info->height = f.height;
+    info->sampling = f.sampling;
+    info->restart_interval = f.restart_interval;
+    const int mpx = f.sampling == HJD_YUV420 ? 16 : 8;
+    const int bpm = f.sampling == HJD_YUV420 ? 6 : 3;
+    info->mcu_w = (f.width - 1) / mpx + 1;
+    info->mcu_h = (f.height - 1) / mpx + 1;
+    info->nblocks = static_cast<int64_t>(info->mcu_w) * info->mcu_h * bpm;
+    for (int c = 0; c < 3; ++c) {
+        memcpy(info->qt[c], f.qt[f.comp[c].tq], sizeof(info->qt[c]));
+        info->qt_precision[c] = f.qt_prec[f.comp[c].tq];
+    }
+    info->scan_offset = static_cast<int64_t>(f.scan_offset);
+}
+
+// Entropy-coded segment reader: 64-bit MSB-first accumulator, FF00 de-stuffing,
+// stops feeding (zeros) at the first marker.
+struct BitReader {
+    const uint8_t* p;
+    const uint8_t* end;
+    uint64_t acc = 0;
+    int nbits = 0;
+    bool at_marker = false;
+
+    void refill()
+    {
+        while (nbits <= 56) {
+            uint64_t b = 0;
+            if (!at_marker && p < end) {
+                if (p[0] != 0xFF) {
+                    b = *p++;
+                } else if (p + 1 < end && p[1] == 0x00) {
+                    b = 0xFF;
+                    p += 2;
+                } else {
+                    at_marker = true;   // leave p on the marker
+                }
+            }
+            acc |= b << (56 - nbits);
+            nbits += 8;
+        }
+    }
+    uint32_t peek(int n) const { return static_cast<uint32_t>(acc >> (64 - n)); }
+    void skip(int n) { acc <<= n; nbits -= n; }
+
+    // Restart: drop buffered bits, expect RSTn at the next marker.
+    bool restart(int expect)
+    {
+        acc = 0;
+        nbits = 0;
+        if (!at_marker) {
+            while (p + 1 < end && !(p[0] == 0xFF && p[1] != 0x00)) ++p;
+        }
+        while (p < end && p[0] == 0xFF) ++p;   // marker prefix + fill bytes
+        if (p >= end || *p != 0xD0 + (expect & 7)) return false;
+        ++p;
+        at_marker = false;
+        return true;
+    }
+};
+
+inline int decode_symbol(BitReader& br, const HuffTable& t)
+{
+    if (br.nbits < 16) br.refill();
+    const uint16_t e = t.fast[br.peek(9)];
+    if (e) {
+        br.skip(e >> 8);
+        return e & 0xFF;
+    }
+    const uint32_t code16 = br.peek(16);
+    for (int len = 10; len <= 16; ++len) {
+        const int32_t c = static_cast<int32_t>(code16 >> (16 - len));
+        if (c <= t.maxcode[len]) {
+            br.skip(len);
+            return t.vals[t.valptr[len] + c - t.mincode[len]];
+        }
+    }
+    return -1;
+}
+
+// receive + extend (T.81 F.2.2.1; src/decoder.cpp:72-92)
+inline int receive_extend(BitReader& br, int s)
+{
+    if (s == 0) return 0;
+    if (br.nbits < s) br.refill();
+    const int v = static_cast<int>(br.peek(s));
+    br.skip(s);
+    return v < (1 << (s - 1)) ? v - (1 << s) + 1 : v;
+}
+
+// One block (src/decoder.cpp:221-260).
+inline bool decode_block(BitReader& br, const HuffTable& dc, const HuffTable& ac, int& pred, int16_t* out)
+{
+    int s = decode_symbol(br, dc);
+    if (s < 0 || s > 11) return false;
+    pred += receive_extend(br, s);
+    if (pred < -32768 || pred > 32767) return false;
+    memset(out, 0, 64 * sizeof(int16_t));
+    out[0] = static_cast<int16_t>(pred);
+    for (int k = 1; k < 64;) {
+        const int rs = decode_symbol(br, ac);
+        if (rs < 0) return false;
+        const int r = rs >> 4, sz = rs & 15;
+        if (sz == 0) {
+            if (r != 15) break;   // EOB
+            k += 16;              // ZRL
+            continue;
+        }
+        k += r;
+        if (k > 63) return false;
+        out[k++] = static_cast<int16_t>(receive_extend(br, sz));
+    }
+    return true;
+}
+
+int decode_scan(const uint8_t* d, size_t n, const Frame& f, const hjd_jpeg_info& info, int16_t* coefs)
+{
+    BitReader br{d + f.scan_offset, d + n};
+    int pred[3] = {0, 0, 0};
+    const int nblk_c[3] = {f.comp[0].h * f.comp[0].v, 1, 1};
+    int blk_base[3];   // block offset of each frame component inside an MCU
+    blk_base[0] = 0;
+    blk_base[1] = nblk_c[0];
+    blk_base[2] = nblk_c[0] + 1;
+    const int bpm = nblk_c[0] + 2;
+    const int64_t nmcu = static_cast<int64_t>(info.mcu_w) * info.mcu_h;
+    int restarts = 0, since = 0;
+    for (int64_t m = 0; m < nmcu; ++m) {
+        if (f.restart_interval > 0 && since == f.restart_interval) {   // src/decoder.cpp:288-307
+            if (!br.restart(restarts)) return set_error(HJD_E_INVALID, "expected RST%d before MCU %lld", restarts & 7,
+                                                      static_cast<long long>(m));
+            ++restarts;
+            since = 0;
+            pred[0] = pred[1] = pred[2] = 0;
+        }
+        ++since;
+        int16_t* mcu = coefs + m * bpm * 64;
+        for (int si = 0; si < 3; ++si) {
+            const int c = f.scan_order[si];
+            const HuffTable& dc = f.dc[f.comp[c].td];
+            const HuffTable& ac = f.ac[f.comp[c].ta];
+            for (int b = 0; b < nblk_c[c]; ++b)
+                if (!decode_block(br, dc, ac, pred[c], mcu + (blk_base[c] + b) * 64))
+                    return set_error(HJD_E_INVALID, "corrupt entropy data in MCU %lld", static_cast<long long>(m));
+        }
+    }
+    return HJD_OK;
+}
+
+int decode_one(const uint8_t* data, size_t size, hjd_jpeg_info* info, int16_t* coefs, int64_t capacity)
+{
+    if (!data || !info) return set_error(HJD_E_INVALID, "NULL argument");
+    Frame f;
+    int rc = parse(data, size, f);
+    if (rc) return rc;
+    fill_info(f, info);
+    if (!coefs) return set_error(HJD_E_INVALID, "coefs is NULL");
+    if (capacity < info->nblocks)
+        return set_error(HJD_E_INVALID, "capacity %lld < %lld blocks", static_cast<long long>(capacity),
+                         static_cast<long long>(info->nblocks));
+    return decode_scan(data, size, f, *info, coefs);
+}
+
+}  // namespace
+
+extern "C" {
+
+int hjd_jpeg_parse(const uint8_t* data, size_t size, hjd_jpeg_info* info)
+{
+    if (!data || !info) return set_error(HJD_E_INVALID, "NULL argument");
+    Frame f;
+    int rc = parse(data, size, f);
+    if (rc) return rc;
+    fill_info(f, info);
+    return HJD_OK;
+}
+
+int hjd_jpeg_decode_coefs(const uint8_t* data, size_t size, hjd_jpeg_info* info, int16_t* coefs,
+                          int64_t capacity_blocks)
+{
+    return decode_one(data, size, info, coefs, capacity_blocks);
+}
+
+int hjd_jpeg_decode_batch(const uint8_t* const* datas, const size_t* sizes, int n, int16_t* const* coefs,
+                          int64_t capacity_blocks, int nthreads, int32_t* status)
+{
+    if (n < 0 || (n > 0 && (!datas || !sizes || !coefs))) return set_error(HJD_E_INVALID, "invalid arguments");
+    if (nthreads <= 0) nthreads = static_cast<int>(std::max(1u, std::thread::hardware_concurrency()));
+    nthreads = std::min(nthreads, std::max(n, 1));
+    std::atomic<int> next{0}, failed{0};
+    auto work = [&]() {
+        hjd_jpeg_info info;
+        for (int i = next++; i < n; i = next++) {
+            const int rc = decode_one(datas[i], sizes[i], &info, coefs[i], capacity_blocks);
+            if (status) status[i] = rc;
+            if (rc) failed++;
+        }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < nthreads; ++t) pool.emplace_back(work);
+    work();
+    for (auto& t : pool) t.join();
+    return failed ? set_error(HJD_E_INVALID, "%d of %d files failed to decode", failed.load(), n) : HJD_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,281 @@
+// stream_pipeline.hip -- host Huffman || H2D || fused kernel (include/hjd_host.h).
+//
+// The reference runs parse -> Huffman -> one blocking upload -> kernel ->
+// blocking read-back strictly in sequence for one image (src/parser.cpp:375-397,
+// src/decoder.cpp:352-416).  Here every submitted JPEG becomes a job:
+//   worker thread:  Huffman-decode into pinned slot s (job j uses s = j % nslots)
+//                   together with its frame record + natural-order qtables;
+//   copy stream:    one hipMemcpyAsync of the slot to device slot s;
+//   compute stream: the fused kernel reads device slot s, writes the caller's
+//                   BGRX buffer.
+// Slot reuse is ordered by events: the host waits for job j-nslots' upload
+// before refilling pinned slot s, and the upload of job j waits (on the GPU)
+// for job j-nslots' kernel before overwriting device slot s.
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <new>
+#include <thread>
+#include <vector>
+
+#include "hjd.h"
+#include "hjd_host.h"
+#include "hjd_internal.h"
+
+using hjd_internal::FrameRecord;
+using hjd_internal::set_error;
+
+namespace {
+
+constexpr size_t kHeader = 1024;   // [FrameRecord | pad][qt natural 3x64 int32][pad] then coefficients
+constexpr size_t kQtOffset = 256;
+
+constexpr int kZigzag[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
+                             12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
+                             35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+                             58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+
+struct Job {
+    int64_t index;
+    const uint8_t* data;
+    size_t size;
+    void* d_out;
+    int32_t pitch;
+};
+
+}  // namespace
+
+struct hjd_stream {
+    hjd_ctx* ctx = nullptr;
+    int device = 0, num_cu = 256;
+    int64_t max_blocks = 0;
+    size_t slot_bytes = 0;
+    int nslots = 0;
+    std::vector<uint8_t*> host;      // pinned staging
+    std::vector<uint8_t*> dev;       // device slots
+    std::vector<hipEvent_t> h2d_done, kernel_done;
+    std::vector<int64_t> slot_issued;   // last job index whose GPU work was issued on the slot
+    hipStream_t copy = nullptr, compute = nullptr;
+
+    std::mutex mu;
+    std::condition_variable cv_jobs, cv_slots, cv_idle;
+    std::deque<Job> queue;
+    int64_t submitted = 0, finished = 0;
+    bool stop = false;
+    std::vector<std::thread> workers;
+
+    std::atomic<int64_t> images{0}, pixels{0}, decode_ns{0}, h2d_bytes{0}, launches{0};
+    int first_error = HJD_OK;
+    std::string first_error_msg;
+
+    void record_error(int rc, const char* msg)
+    {
+        std::lock_guard<std::mutex> g(mu);
+        if (first_error == HJD_OK) {
+            first_error = rc;
+            first_error_msg = msg;
+        }
+    }
+
+    int run_job(const Job& job);
+    void worker();
+};
+
+int hjd_stream::run_job(const Job& job)
+{
+    const int s = static_cast<int>(job.index % nslots);
+    {   // wait until the previous job on this slot has issued its GPU work
+        std::unique_lock<std::mutex> lk(mu);
+        cv_slots.wait(lk, [&] { return slot_issued[s] == job.index - nslots || stop; });
+    }
+    if (hipSetDevice(device) != hipSuccess) return set_error(HJD_E_HIP, "hipSetDevice");
+    if (job.index >= nslots && hipEventSynchronize(h2d_done[s]) != hipSuccess)   // pinned slot free
+        return set_error(HJD_E_HIP, "hipEventSynchronize(h2d)");
+
+    uint8_t* h = host[s];
+    hjd_jpeg_info info;
+    const auto t0 = std::chrono::steady_clock::now();
+    int rc = hjd_jpeg_decode_coefs(job.data, job.size, &info, reinterpret_cast<int16_t*>(h + kHeader), max_blocks);
+    decode_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+    if (rc == HJD_OK && job.pitch < 4 * info.width) rc = set_error(HJD_E_INVALID, "output pitch too small");
+
+    const size_t coef_bytes = rc == HJD_OK ? static_cast<size_t>(info.nblocks) * 128 : 0;
+    int64_t tasks = 0;
+    if (rc == HJD_OK) {
+        FrameRecord rec;
+        const int qti[3] = {0, 1, 2};
+        tasks = hjd_internal::make_frame_record(info.width, info.height, info.sampling, 0,
+                                                0, job.pitch, qti, &rec);
+        if (tasks < 0) rc = static_cast<int>(tasks);
+        memcpy(h, &rec, sizeof(rec));
+        int32_t* qn = reinterpret_cast<int32_t*>(h + kQtOffset);
+        for (int c = 0; c < 3; ++c)
+            for (int k = 0; k < 64; ++k) qn[c * 64 + kZigzag[k]] = info.qt[c][k];
+    }
+
+    // Issue the GPU work (also on failure, with nothing to do, so the slot's
+    // event chain stays intact for the next job).
+    hipError_t e = hipStreamWaitEvent(copy, kernel_done[s], 0);
+    if (e == hipSuccess && rc == HJD_OK)
+        e = hipMemcpyAsync(dev[s], h, kHeader + coef_bytes, hipMemcpyHostToDevice, copy);
+    if (e == hipSuccess) e = hipEventRecord(h2d_done[s], copy);
+    if (e == hipSuccess) e = hipStreamWaitEvent(compute, h2d_done[s], 0);
+    int lrc = HJD_OK;
+    if (e == hipSuccess && rc == HJD_OK && tasks > 0) {
+        lrc = hjd_internal::launch_decode(device, num_cu, info.sampling, HJD_IN_Q16_ZIGZAG, 0, dev[s] + kHeader,
+                                          reinterpret_cast<const int32_t*>(dev[s] + kQtOffset),
+                                          reinterpret_cast<const FrameRecord*>(dev[s]), 1, tasks, job.d_out,
+                                          compute, 0);
+        launches++;
+    }
+    if (e == hipSuccess) e = hipEventRecord(kernel_done[s], compute);
+    {
+        std::lock_guard<std::mutex> g(mu);
+        slot_issued[s] = job.index;
+    }
+    cv_slots.notify_all();
+    if (e != hipSuccess) return set_error(HJD_E_HIP, "stream issue: %s", hipGetErrorString(e));
+    if (rc != HJD_OK) return rc;
+    if (lrc != HJD_OK) return lrc;
+    images++;
+    pixels += static_cast<int64_t>(info.width) * info.height;
+    h2d_bytes += static_cast<int64_t>(kHeader + coef_bytes);
+    return HJD_OK;
+}
+
+void hjd_stream::worker()
+{
+    for (;;) {
+        Job job;
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv_jobs.wait(lk, [&] { return stop || !queue.empty(); });
+            if (queue.empty()) return;
+            job = queue.front();
+            queue.pop_front();
+        }
+        const int rc = run_job(job);
+        if (rc != HJD_OK) record_error(rc, hjd_last_error());
+        {
+            std::lock_guard<std::mutex> g(mu);
+            ++finished;
+        }
+        cv_idle.notify_all();
+    }
+}
+
+extern "C" {
+
+int hjd_stream_create(hjd_ctx* ctx, int64_t max_blocks, int nslots, int nthreads, hjd_stream** out)
+{
+    if (!ctx || !out || max_blocks <= 0 || nslots < 2) return set_error(HJD_E_INVALID, "invalid stream arguments");
+    *out = nullptr;
+    if (nthreads <= 0) nthreads = static_cast<int>(std::max(1u, std::thread::hardware_concurrency()));
+    hjd_stream* st = new (std::nothrow) hjd_stream;
+    if (!st) return set_error(HJD_E_NOMEM, "stream allocation");
+    st->ctx = ctx;
+    st->device = hjd_ctx_device(ctx);
+    st->num_cu = hjd_internal::ctx_num_cu(ctx);
+    st->max_blocks = max_blocks;
+    st->slot_bytes = kHeader + static_cast<size_t>(max_blocks) * 128;
+    st->nslots = nslots;
+    auto bail = [&](const char* what, hipError_t e) {
+        hjd_stream_destroy(st);
+        return set_error(HJD_E_HIP, "%s: %s", what, hipGetErrorString(e));
+    };
+    hipError_t e = hipSetDevice(st->device);
+    if (e != hipSuccess) return bail("hipSetDevice", e);
+    if ((e = hipStreamCreateWithFlags(&st->copy, hipStreamNonBlocking)) != hipSuccess) return bail("stream", e);
+    if ((e = hipStreamCreateWithFlags(&st->compute, hipStreamNonBlocking)) != hipSuccess) return bail("stream", e);
+    st->host.assign(nslots, nullptr);
+    st->dev.assign(nslots, nullptr);
+    st->h2d_done.assign(nslots, nullptr);
+    st->kernel_done.assign(nslots, nullptr);
+    st->slot_issued.assign(nslots, 0);
+    for (int s = 0; s < nslots; ++s) {
+        st->slot_issued[s] = s - nslots;
+        if ((e = hipHostMalloc(reinterpret_cast<void**>(&st->host[s]), st->slot_bytes, hipHostMallocDefault)) !=
+            hipSuccess)
+            return bail("hipHostMalloc", e);
+        if ((e = hipMalloc(reinterpret_cast<void**>(&st->dev[s]), st->slot_bytes)) != hipSuccess)
+            return bail("hipMalloc", e);
+        if ((e = hipEventCreateWithFlags(&st->h2d_done[s], hipEventDisableTiming)) != hipSuccess)
+            return bail("event", e);
+        if ((e = hipEventCreateWithFlags(&st->kernel_done[s], hipEventDisableTiming)) != hipSuccess)
+            return bail("event", e);
+    }
+    for (int t = 0; t < nthreads; ++t) st->workers.emplace_back([st] { st->worker(); });
+    *out = st;
+    return HJD_OK;
+}
+
+int hjd_stream_destroy(hjd_stream* st)
+{
+    if (!st) return HJD_OK;
+    {
+        std::lock_guard<std::mutex> g(st->mu);
+        st->stop = true;
+    }
+    st->cv_jobs.notify_all();
+    st->cv_slots.notify_all();
+    for (auto& t : st->workers) t.join();
+    (void)hipSetDevice(st->device);
+    if (st->compute) (void)hipStreamSynchronize(st->compute);
+    if (st->copy) (void)hipStreamSynchronize(st->copy);
+    for (size_t s = 0; s < st->host.size(); ++s) {
+        if (st->host[s]) (void)hipHostFree(st->host[s]);
+        if (st->dev[s]) (void)hipFree(st->dev[s]);
+        if (st->h2d_done[s]) (void)hipEventDestroy(st->h2d_done[s]);
+        if (st->kernel_done[s]) (void)hipEventDestroy(st->kernel_done[s]);
+    }
+    if (st->copy) (void)hipStreamDestroy(st->copy);
+    if (st->compute) (void)hipStreamDestroy(st->compute);
+    delete st;
+    return HJD_OK;
+}
+
+int hjd_stream_submit(hjd_stream* st, const uint8_t* data, size_t size, void* d_out, int32_t out_pitch)
+{
+    if (!st || !data || !d_out || out_pitch <= 0 || (out_pitch & 3) || (reinterpret_cast<uintptr_t>(d_out) & 15))
+        return set_error(HJD_E_INVALID, "invalid submit arguments (d_out must be 16-byte aligned)");
+    {
+        std::lock_guard<std::mutex> g(st->mu);
+        st->queue.push_back(Job{st->submitted++, data, size, d_out, out_pitch});
+    }
+    st->cv_jobs.notify_one();
+    return HJD_OK;
+}
+
+int hjd_stream_sync(hjd_stream* st, int64_t stats[5])
+{
+    if (!st) return set_error(HJD_E_INVALID, "stream is NULL");
+    {
+        std::unique_lock<std::mutex> lk(st->mu);
+        st->cv_idle.wait(lk, [&] { return st->finished == st->submitted; });
+    }
+    hipError_t e = hipSetDevice(st->device);
+    if (e == hipSuccess) e = hipStreamSynchronize(st->compute);
+    if (e == hipSuccess) e = hipStreamSynchronize(st->copy);
+    if (stats) {
+        stats[0] = st->images;
+        stats[1] = st->pixels;
+        stats[2] = st->decode_ns;
+        stats[3] = st->h2d_bytes;
+        stats[4] = st->launches;
+    }
+    if (e != hipSuccess) return set_error(HJD_E_HIP, "stream sync: %s", hipGetErrorString(e));
+    std::lock_guard<std::mutex> g(st->mu);
+    if (st->first_error != HJD_OK) {
+        const int rc = st->first_error;
+        st->first_error = HJD_OK;
+        return set_error(rc, "%s", st->first_error_msg.c_str());
+    }
+    return HJD_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,149 @@
+"""Host JPEG front end + streaming decode (include/hjd_host.h).
+
+    info = parse(data)                        # headers only
+    coefs, info = decode_coefs(data)          # host Huffman -> int16 zigzag coefficients
+    pixels = decode_jpeg(ctx, data)           # host Huffman + fused HIP kernel, BGRX on the device
+    with JpegStream(ctx, max_blocks) as st:   # Huffman workers || H2D || kernel
+        st.submit(data, out_tensor); st.sync()
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import HjdJpegInfo, check
+
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_i16p = ctypes.POINTER(ctypes.c_int16)
+
+
+@dataclass
+class JpegInfo:
+    width: int
+    height: int
+    sampling: int
+    restart_interval: int
+    mcu_w: int
+    mcu_h: int
+    nblocks: int
+    qt: np.ndarray            # [3][64] file (zigzag) order, per component
+    qt_precision: tuple
+    scan_offset: int
+
+    @classmethod
+    def from_c(cls, c: HjdJpegInfo) -> "JpegInfo":
+        return cls(c.width, c.height, c.sampling, c.restart_interval, c.mcu_w, c.mcu_h, c.nblocks,
+                   np.array(c.qt, dtype=np.int32), tuple(c.qt_precision), c.scan_offset)
+
+
+def _buf(data: bytes):
+    return (ctypes.c_uint8 * len(data)).from_buffer_copy(data)
+
+
+def parse(data: bytes) -> JpegInfo:
+    lib = _lib.load()
+    info = HjdJpegInfo()
+    check(lib.hjd_jpeg_parse(_buf(data), len(data), ctypes.byref(info)), "hjd_jpeg_parse")
+    return JpegInfo.from_c(info)
+
+
+def decode_coefs(data: bytes):
+    """Host Huffman decode -> (int16 [nblocks][64] zigzag coefficients, JpegInfo)."""
+    lib = _lib.load()
+    buf = _buf(data)
+    info = HjdJpegInfo()
+    check(lib.hjd_jpeg_parse(buf, len(data), ctypes.byref(info)), "hjd_jpeg_parse")
+    coefs = np.empty((info.nblocks, 64), np.int16)
+    check(lib.hjd_jpeg_decode_coefs(buf, len(data), ctypes.byref(info), coefs.ctypes.data_as(_i16p), info.nblocks),
+          "hjd_jpeg_decode_coefs")
+    return coefs, JpegInfo.from_c(info)
+
+
+def decode_coefs_batch(datas: Sequence[bytes], nthreads: int = 0) -> List[np.ndarray]:
+    """Decode many files on a host thread pool."""
+    lib = _lib.load()
+    infos = [parse(d) for d in datas]
+    outs = [np.empty((i.nblocks, 64), np.int16) for i in infos]
+    cap = max([i.nblocks for i in infos] or [0])
+    bufs = [_buf(d) for d in datas]
+    arr_d = (_u8p * len(bufs))(*[ctypes.cast(b, _u8p) for b in bufs])
+    arr_s = (ctypes.c_size_t * len(datas))(*[len(d) for d in datas])
+    arr_o = (_i16p * len(outs))(*[o.ctypes.data_as(_i16p) for o in outs])
+    status = (ctypes.c_int32 * len(datas))()
+    # every output holds exactly its own file's blocks: capacity checked per file
+    for o, i in zip(outs, infos):
+        assert o.shape[0] >= i.nblocks
+    check(lib.hjd_jpeg_decode_batch(arr_d, arr_s, len(datas), arr_o, cap, nthreads, status),
+          "hjd_jpeg_decode_batch")
+    return outs
+
+
+def decode_jpeg(ctx, data: bytes, stream=None):
+    """JPEG bytes -> (H, W) int32 device tensor of BGRX words (host Huffman,
+    then the fused kernel on the device)."""
+    import torch
+    from .backend import IN_Q16_ZIGZAG, FrameSpec, Plan
+    coefs, info = decode_coefs(data)
+    dev = torch.device("cuda", ctx.device)
+    d_coefs = torch.from_numpy(coefs).to(dev)
+    out = torch.empty((info.height, info.width), dtype=torch.int32, device=dev)
+    plan = Plan(ctx, [FrameSpec(info.width, info.height, info.sampling, qt_index=(0, 1, 2))], IN_Q16_ZIGZAG,
+                qtables=info.qt)
+    plan.launch(d_coefs, out, stream)
+    return out
+
+
+class JpegStream:
+    """hjd_stream: host Huffman workers -> pinned slots -> H2D -> fused kernel."""
+
+    def __init__(self, ctx, max_blocks: int, nslots: int = 4, nthreads: int = 0):
+        self.lib = _lib.load()
+        self.ctx = ctx
+        h = ctypes.c_void_p()
+        check(self.lib.hjd_stream_create(ctx.handle, int(max_blocks), int(nslots), int(nthreads), ctypes.byref(h)),
+              "hjd_stream_create")
+        self.handle = h
+        self._keep = []   # bytes must stay alive until sync
+
+    def submit(self, data: bytes, out, out_pitch: Optional[int] = None):
+        buf = _buf(data) if not isinstance(data, ctypes.Array) else data
+        self._keep.append(buf)
+        if isinstance(out, int):
+            ptr = out
+            assert out_pitch, "out_pitch required with a raw pointer"
+        else:
+            if not (out.is_cuda and out.is_contiguous()):
+                raise ValueError("out must be a contiguous device tensor")
+            ptr = out.data_ptr()
+            out_pitch = out_pitch or out.shape[-1] * out.element_size()
+        check(self.lib.hjd_stream_submit(self.handle, ctypes.cast(buf, _u8p), len(buf), ptr, int(out_pitch)),
+              "hjd_stream_submit")
+
+    def sync(self) -> dict:
+        stats = (ctypes.c_int64 * 5)()
+        rc = self.lib.hjd_stream_sync(self.handle, stats)
+        self._keep.clear()
+        check(rc, "hjd_stream_sync")
+        return {"images": stats[0], "pixels": stats[1], "host_decode_ns": stats[2], "h2d_bytes": stats[3],
+                "kernel_launches": stats[4]}
+
+    def close(self):
+        if self.handle:
+            self.lib.hjd_stream_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

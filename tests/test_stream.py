@@ -1,0 +1,87 @@
+"""GPU: JPEG bytes -> pixels through the host front end and the stream
+pipeline (host Huffman || pinned H2D || fused kernel).  Golden files are
+checked against the reference's BGRX; other files against the oracle applied
+to the host-decoded coefficients (the Huffman stage itself is pinned to the
+reference in tests/test_jpeg_host.py)."""
+import io
+import os
+
+import numpy as np
+import pytest
+
+import oracle_py as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _pil(w, h, q, sub, seed, **kw):
+    from PIL import Image
+    rng = np.random.default_rng(seed)
+    x = np.linspace(0, 255, w)[None, :, None]
+    y = np.linspace(0, 255, h)[:, None, None]
+    img = np.clip(x * [1, 0, 0.5] + y * [0, 1, 0.5] + rng.normal(0, 20, (h, w, 3)), 0, 255).astype(np.uint8)
+    b = io.BytesIO()
+    Image.fromarray(img).save(b, format="JPEG", quality=q, subsampling=sub, **kw)
+    return b.getvalue()
+
+
+def test_decode_jpeg_golden(hjd, ctx):
+    import torch
+    for name in O.golden_cases():
+        data = open(os.path.join(O.GOLDEN, name + ".jpg"), "rb").read()
+        out = hjd.decode_jpeg(ctx, data)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), O.load_case(name)["bgrx"])
+
+
+@pytest.mark.parametrize("nslots,nthreads", [(2, 1), (3, 4), (8, 16)])
+def test_stream_many_images(hjd, ctx, nslots, nthreads):
+    import torch
+    files = []
+    for name in O.golden_cases():
+        files.append((open(os.path.join(O.GOLDEN, name + ".jpg"), "rb").read(), O.load_case(name)["bgrx"]))
+    rng = np.random.default_rng(nslots * 7 + nthreads)
+    for i in range(12):
+        w, h = int(rng.integers(1, 700)), int(rng.integers(1, 300))
+        sub = int(rng.choice([0, 2]))
+        kw = {"restart_marker_blocks": int(rng.integers(1, 9))} if i % 3 == 0 else {}
+        data = _pil(w, h, int(rng.integers(30, 100)), sub, seed=i, **kw)
+        coefs, info = hjd.decode_coefs(data)
+        files.append((data, O.decode_q16(coefs, info.qt, info.width, info.height, info.sampling)))
+    files = files * 2
+    max_blocks = max(hjd.parse(d).nblocks for d, _ in files)
+    outs = [torch.full(e.shape, -1, dtype=torch.int32, device="cuda") for _, e in files]
+    with hjd.JpegStream(ctx, max_blocks, nslots=nslots, nthreads=nthreads) as st:
+        for (d, _), o in zip(files, outs):
+            st.submit(d, o)
+        stats = st.sync()
+    assert stats["images"] == len(files) and stats["kernel_launches"] == len(files)
+    for (d, e), o in zip(files, outs):
+        np.testing.assert_array_equal(o.cpu().numpy().view(np.uint32), e)
+
+
+def test_stream_reports_bad_file_and_continues(hjd, ctx):
+    import torch
+    good = open(os.path.join(O.GOLDEN, "syn420_96x64_q90.jpg"), "rb").read()
+    exp = O.load_case("syn420_96x64_q90")["bgrx"]
+    bad = good[:200]   # truncated
+    outs = [torch.zeros((64, 96), dtype=torch.int32, device="cuda") for _ in range(3)]
+    st = hjd.JpegStream(ctx, 1024, nslots=2, nthreads=2)
+    st.submit(good, outs[0]); st.submit(bad, outs[1]); st.submit(good, outs[2])
+    with pytest.raises(Exception):
+        st.sync()
+    np.testing.assert_array_equal(outs[0].cpu().numpy().view(np.uint32), exp)
+    np.testing.assert_array_equal(outs[2].cpu().numpy().view(np.uint32), exp)
+    st.submit(good, outs[1])      # the stream stays usable after an error
+    st.sync()
+    np.testing.assert_array_equal(outs[1].cpu().numpy().view(np.uint32), exp)
+    st.close()
+
+
+def test_4k_jpeg_end_to_end(hjd, ctx):
+    import torch
+    data = _pil(3840, 2160, 90, 2, seed=4)
+    coefs, info = hjd.decode_coefs(data)
+    out = hjd.decode_jpeg(ctx, data)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), O.decode_q16(coefs, info.qt, 3840, 2160, 1))

@@ -24,8 +24,8 @@ OBJDIR = os.path.join(REPO, "build", "obj")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("HJD_ARCH", "gfx950")
 
-HIP_SOURCES = ["hjd_runtime.hip"]
-CXX_SOURCES = ["idct_compat.cpp", "jpeg_host.cpp", "stream_pipeline.cpp"]
+HIP_SOURCES = ["hjd_runtime.hip", "idct_compat.hip", "stream_pipeline.hip"]
+CXX_SOURCES = ["jpeg_host.cpp"]
 
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", f"-I{INCLUDE}", f"-I{CSRC}"]
 
@@ -58,6 +58,8 @@ def build(verbose: bool = False, force: bool = False) -> str:
     objs = []
     for src in HIP_SOURCES:
         s = os.path.join(CSRC, src)
+        if not os.path.exists(s):
+            continue
         o = os.path.join(OBJDIR, src + ".o")
         objs.append(o)
         if force or _needs(o, [s] + headers):
