@@ -227,10 +227,8 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
-    el = torch.tensor([wall], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    wall_max = float(el.item())
+    from ocljpegdecoder_amd import shard
+    wall_max = shard.aggregate({"seconds": wall})["seconds"]   # max over ranks
     px = nf * w * h * args.steps * world
     if rank == 0:
         res = {
@@ -264,18 +262,25 @@ def main():
     ap.add_argument("--frames", type=int, default=0, help="override batch size")
     ap.add_argument("--grid", type=int, default=0, help="persistent grid (workgroups), 0 = default")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend for the barrier/timing reduction (no data-path collective)")
     args = ap.parse_args()
 
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    from ocljpegdecoder_amd import shard
+    rank, world, local_rank = shard.env_rank()
+    # HJD_BENCH_SAME_DEVICE=1 + --dist-backend gloo: rehearse the N-rank path on
+    # one GPU (every rank on device 0); the real multi-GPU run uses RCCL ("nccl").
+    gpu = 0 if os.environ.get("HJD_BENCH_SAME_DEVICE") == "1" else local_rank
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        torch.cuda.set_device(gpu)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(args.dist_backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -328,10 +333,7 @@ def main():
     wall = time.perf_counter() - t0
     kernel_ms = ev0.elapsed_time(ev1) / args.steps   # HIP events on the launch stream
 
-    elapsed = torch.tensor([wall], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    wall_max = float(elapsed.item())
+    wall_max = shard.aggregate({"seconds": wall})["seconds"]   # max over ranks
 
     px_per_launch = plan.pixels
     bytes_per_launch = plan.coef_bytes + 4 * plan.pixels
