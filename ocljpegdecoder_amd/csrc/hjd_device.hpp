@@ -117,27 +117,108 @@ struct ChromaTerms {
     int special;
 };
 
+// Exact fixed-point floors (S = 20; K and the bias searched and proved over
+// v,u in [-256,255] by tests/test_oracle.py::test_fixed_point_colour_terms):
+//   floor(1.402 v) + 128 = (v*1470091 + (128<<20) + 1048) >> 20
+//   floor(1.772 u) + 128 = (u*1858077 + (128<<20) + 2097) >> 20
+// The +2^20/(2*den) bias keeps every case >= 1/1000 (R) or 1/500 (B) away
+// from an integer, which also covers the exact multiples (u = +-250).
+constexpr int kRK = 1470091, kRBias = (128 << 20) + 1048;
+constexpr int kBK = 1858077, kBBias = (128 << 20) + 2097;
+
+__host__ __device__ __forceinline__ int r_term(int v) { return (mul24(v, kRK) + kRBias) >> 20; }
+__host__ __device__ __forceinline__ int b_term(int u) { return (mul24(u, kBK) + kBBias) >> 20; }
+
+// floor(-(17207u + 35707v) / 50000) + 128, exactly.  The fp32 estimate is
+// biased down by 5e-5 (> its worst-case error of 2.2e-5 for |m| < 2^24) so it
+// is floor or floor-1; one remainder test fixes it.
+__device__ __forceinline__ int g_term(int u, int v)
+{
+    const int m = mul24(u, -17207) + mul24(v, -35707);
+    const int q0 = __float2int_rd(__builtin_fmaf(static_cast<float>(m), 2.0e-5f, -5.0e-5f));
+    const int r = m + mul24(q0, -50000);
+    return q0 + (r >= 50000 ? 129 : 128);
+}
+
 __device__ __forceinline__ ChromaTerms chroma_terms(int u, int v)
 {
     ChromaTerms t;
-    t.rq = __float2int_rd(static_cast<float>(v) * 1.402f);
-    t.bq = __float2int_rd(static_cast<float>(u) * 1.772f);
-    const int n = -(mul24(17207, u) + mul24(35707, v));  // |n| < 2^24: exact in fp32
-    int q = __float2int_rd(static_cast<float>(n) * 2.0e-5f);
-    const int rem = n - mul24(q, 50000);
-    q += (rem >= 50000 ? 1 : 0) - (rem < 0 ? 1 : 0);
-    t.gq = q;
+    t.rq = r_term(v);
+    t.bq = b_term(u);
+    t.gq = g_term(u, v);
     t.special = (u == -200) & (v == 200);
     return t;
 }
 
+// ---- packed (2 x int16 per VGPR) pixel math ---------------------------------
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t pk_add16(uint32_t a, uint32_t b)
+{
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(s16x2, a) + __builtin_bit_cast(s16x2, b));
+}
+
+__device__ __forceinline__ uint32_t pk_clamp_u8(uint32_t a)
+{
+    s16x2 x = __builtin_bit_cast(s16x2, a);
+    x = __builtin_elementwise_max(x, (s16x2){0, 0});
+    x = __builtin_elementwise_min(x, (s16x2){255, 255});
+    return __builtin_bit_cast(uint32_t, x);
+}
+
+// v_perm_b32: result byte i = sel byte i of {S1 bytes 0-3 -> 0..3, S0 bytes -> 4..7, 0x0c -> 0}
+__device__ __forceinline__ uint32_t perm(uint32_t s0, uint32_t s1, uint32_t sel)
+{
+    return __builtin_amdgcn_perm(s0, s1, sel);
+}
+constexpr uint32_t kSelLoLo = 0x05040100u;   // (s1.lo16) | (s0.lo16 << 16)
+
+// The chroma terms of two pixels as int16 pairs (low half = first pixel).
+struct ChromaPair {
+    uint32_t r, g, b;
+    int special;      // either pixel's chroma is the (U,V) = (-200,200) corner
+};
+
+__device__ __forceinline__ ChromaPair pair_of(const ChromaTerms& c0, const ChromaTerms& c1)
+{
+    ChromaPair p;
+    p.r = perm(c1.rq, c0.rq, kSelLoLo);
+    p.g = perm(c1.gq, c0.gq, kSelLoLo);
+    p.b = perm(c1.bq, c0.bq, kSelLoLo);
+    p.special = c0.special | c1.special;
+    return p;
+}
+
+// Two BGRX pixels from an int16 pair of Y samples (low half first) and their
+// chroma pair.  kCheckSpecial adds the reference's double-rounding corner
+// (G one lower for (U,V) = (-200,200), Y in [188,201]); callers take that path
+// only when some lane of the wave needs it.
+template <bool kCheckSpecial>
+__device__ __forceinline__ void pixels2(uint32_t ypair, const ChromaPair& c, const ChromaTerms* c0,
+                                        const ChromaTerms* c1, uint32_t& px0, uint32_t& px1)
+{
+    const uint32_t R = pk_clamp_u8(pk_add16(ypair, c.r));
+    uint32_t graw = pk_add16(ypair, c.g);
+    if constexpr (kCheckSpecial) {
+        const int y0 = static_cast<short>(ypair), y1 = static_cast<int>(ypair) >> 16;
+        const short d0 = (c0->special && static_cast<unsigned>(y0 - 188) < 14u) ? 1 : 0;
+        const short d1 = (c1->special && static_cast<unsigned>(y1 - 188) < 14u) ? 1 : 0;
+        graw = __builtin_bit_cast(uint32_t, __builtin_bit_cast(s16x2, graw) - (s16x2){d0, d1});
+    }
+    const uint32_t G = pk_clamp_u8(graw);
+    const uint32_t B = pk_clamp_u8(pk_add16(ypair, c.b));
+    const uint32_t T = perm(G, B, 0x06020400u);   // B.b0 G.b0 B.b2 G.b2
+    px0 = perm(R, T, 0x0c040100u);                // b0 g0 r0 0
+    px1 = perm(R, T, 0x0c060302u);                // b1 g1 r1 0
+}
+
+// Scalar form (one pixel) on top of the same code, for the colour test hooks.
 __device__ __forceinline__ uint32_t pixel_bgrx(int y, const ChromaTerms& t)
 {
-    const int yb = y + 128;
-    const int r = clamp_u8(yb + t.rq);
-    const int g = clamp_u8(yb + t.gq - (t.special & (static_cast<unsigned>(y - 188) < 14u)));
-    const int b = clamp_u8(yb + t.bq);
-    return (static_cast<uint32_t>(r) << 16) | (static_cast<uint32_t>(g) << 8) | static_cast<uint32_t>(b);
+    const uint32_t yp = perm(static_cast<uint32_t>(y), static_cast<uint32_t>(y), kSelLoLo);
+    uint32_t p0, p1;
+    pixels2<true>(yp, pair_of(t, t), &t, &t, p0, p1);
+    return p0;
 }
 
 // Literal fp64 form of src/decoder.cpp:369 (C evaluation order, no FMA

@@ -158,9 +158,23 @@ __device__ __forceinline__ void store4(uint8_t* __restrict__ row, int x, int wid
 }
 
 // Colour stage of one task (samples are int16, row-major, in the block slots).
-// 4:2:0: lane = 4 px x 2 rows (one chroma row shared by both); 4 iterations
-// cover the 128x16 strip, each wave store instruction writes two 512-byte row
-// segments.  4:4:4: same lane shape over a 128x8 strip.
+// Each lane owns 4 px x 2 rows.  4:2:0: one chroma row serves both pixel rows
+// (nearest 2x2 replication, src/decoder.cpp:474-483), chroma terms are computed
+// once per chroma sample; 4 iterations cover the 128x16 strip and every wave
+// store instruction writes two 512-byte row segments.  4:4:4: the same lane
+// shape over the 128x8 strip, chroma per pixel (src/decoder.cpp:457-471).
+// Pixel math is packed: two pixels per int16x2 VGPR (pixels2).
+template <bool kCheck, int kVariant, bool kFull>
+__device__ __forceinline__ void emit_row4(uint8_t* __restrict__ row, int xa, int width, uint32_t y01, uint32_t y23,
+                                          const ChromaPair& p01, const ChromaPair& p23, const ChromaTerms* c0,
+                                          const ChromaTerms* c1, const ChromaTerms* c2, const ChromaTerms* c3)
+{
+    uint32_t q0, q1, q2, q3;
+    pixels2<kCheck>(y01, p01, c0, c1, q0, q1);
+    pixels2<kCheck>(y23, p23, c2, c3, q2, q3);
+    store4<kFull, kVariant>(row, xa, width, q0, q1, q2, q3);
+}
+
 template <int kSampling, bool kFull, int kVariant>
 __device__ __forceinline__ void colour_stage(const char* __restrict__ slots, int lane, uint8_t* __restrict__ out,
                                              int pitch, int width, int height, int y_base, int x_base)
@@ -183,15 +197,21 @@ __device__ __forceinline__ void colour_stage(const char* __restrict__ slots, int
             const int cv = *reinterpret_cast<const int*>(slots + (m * 6 + 5) * kSlotBytes + coff);
             const ChromaTerms c0 = chroma_terms(static_cast<short>(cu), static_cast<short>(cv));
             const ChromaTerms c1 = chroma_terms(cu >> 16, cv >> 16);
+            const ChromaPair p0 = pair_of(c0, c0), p1 = pair_of(c1, c1);
             const int ya0 = y_base + y0;
             uint8_t* row0 = out + static_cast<int64_t>(ya0) * pitch;
-            if (kFull || ya0 < height)
-                store4<kFull, kVariant>(row0, xa, width, pixel_bgrx(static_cast<short>(ya.x), c0), pixel_bgrx(ya.x >> 16, c0),
-                              pixel_bgrx(static_cast<short>(ya.y), c1), pixel_bgrx(ya.y >> 16, c1));
-            if (kFull || ya0 + 1 < height)
-                store4<kFull, kVariant>(row0 + pitch, xa, width, pixel_bgrx(static_cast<short>(yb.x), c0),
-                              pixel_bgrx(yb.x >> 16, c0), pixel_bgrx(static_cast<short>(yb.y), c1),
-                              pixel_bgrx(yb.y >> 16, c1));
+            if (__builtin_amdgcn_ballot_w64((p0.special | p1.special) != 0)) {   // wave-uniform, rare
+                if (kFull || ya0 < height)
+                    emit_row4<true, kVariant, kFull>(row0, xa, width, ya.x, ya.y, p0, p1, &c0, &c0, &c1, &c1);
+                if (kFull || ya0 + 1 < height)
+                    emit_row4<true, kVariant, kFull>(row0 + pitch, xa, width, yb.x, yb.y, p0, p1, &c0, &c0, &c1, &c1);
+            } else {
+                if (kFull || ya0 < height)
+                    emit_row4<false, kVariant, kFull>(row0, xa, width, ya.x, ya.y, p0, p1, &c0, &c0, &c1, &c1);
+                if (kFull || ya0 + 1 < height)
+                    emit_row4<false, kVariant, kFull>(row0 + pitch, xa, width, yb.x, yb.y, p0, p1, &c0, &c0, &c1,
+                                                      &c1);
+            }
         }
     } else {
         const int m = cg >> 1;        // MCU within strip (16 x 8 px)
@@ -206,15 +226,18 @@ __device__ __forceinline__ void colour_stage(const char* __restrict__ slots, int
                 const int2 sy = *reinterpret_cast<const int2*>(base);
                 const int2 su = *reinterpret_cast<const int2*>(base + kSlotBytes);
                 const int2 sv = *reinterpret_cast<const int2*>(base + 2 * kSlotBytes);
+                const ChromaTerms c0 = chroma_terms(static_cast<short>(su.x), static_cast<short>(sv.x));
+                const ChromaTerms c1 = chroma_terms(su.x >> 16, sv.x >> 16);
+                const ChromaTerms c2 = chroma_terms(static_cast<short>(su.y), static_cast<short>(sv.y));
+                const ChromaTerms c3 = chroma_terms(su.y >> 16, sv.y >> 16);
+                const ChromaPair p01 = pair_of(c0, c1), p23 = pair_of(c2, c3);
                 const int ya = y_base + y;
+                uint8_t* row = out + static_cast<int64_t>(ya) * pitch;
                 if (kFull || ya < height) {
-                    const uint32_t q0 = pixel_bgrx(static_cast<short>(sy.x),
-                                                   chroma_terms(static_cast<short>(su.x), static_cast<short>(sv.x)));
-                    const uint32_t q1 = pixel_bgrx(sy.x >> 16, chroma_terms(su.x >> 16, sv.x >> 16));
-                    const uint32_t q2 = pixel_bgrx(static_cast<short>(sy.y),
-                                                   chroma_terms(static_cast<short>(su.y), static_cast<short>(sv.y)));
-                    const uint32_t q3 = pixel_bgrx(sy.y >> 16, chroma_terms(su.y >> 16, sv.y >> 16));
-                    store4<kFull, kVariant>(out + static_cast<int64_t>(ya) * pitch, xa, width, q0, q1, q2, q3);
+                    if (__builtin_amdgcn_ballot_w64((p01.special | p23.special) != 0))
+                        emit_row4<true, kVariant, kFull>(row, xa, width, sy.x, sy.y, p01, p23, &c0, &c1, &c2, &c3);
+                    else
+                        emit_row4<false, kVariant, kFull>(row, xa, width, sy.x, sy.y, p01, p23, &c0, &c1, &c2, &c3);
                 }
             }
         }
@@ -233,7 +256,7 @@ __device__ __forceinline__ constexpr int round_component(int i)
 // Samples end up as int16 row-major in the block slots.
 template <int kSampling, int kFmt>
 __device__ __forceinline__ void idct_stage(char* __restrict__ slots, char* __restrict__ rowbuf, int lane,
-                                           const int (&zoff)[8], const int (&q)[3][8],
+                                           const int (&zoff)[8], const uint32_t (&q)[3][4],
                                            const int* __restrict__ src32, int nblk)
 {
     const int g = lane >> 3, r = lane & 7;
@@ -247,7 +270,9 @@ __device__ __forceinline__ void idct_stage(char* __restrict__ slots, char* __res
 #pragma unroll
             for (int c = 0; c < 8; ++c) {
                 const int coef = *reinterpret_cast<const short*>(blk + zoff[c]);
-                v[c] = mul24(coef, q[comp][c]);   // dequant (src/decoder.cpp:340)
+                const uint32_t qq = q[comp][c >> 1];   // two 16-bit factors per VGPR
+                const int qc = (c & 1) ? static_cast<int>(qq >> 16) : static_cast<int>(qq & 0xffffu);
+                v[c] = mul24(coef, qc);   // dequant (src/decoder.cpp:340)
             }
         } else {
             int4 lo = make_int4(0, 0, 0, 0), hi = lo;
@@ -286,7 +311,7 @@ __device__ __forceinline__ void idct_stage(char* __restrict__ slots, char* __res
 // SGPRs; the next task's coefficients are prefetched into VGPRs while the
 // current one is transformed.
 template <int kSampling, int kFmt, int kVariant>
-__global__ __launch_bounds__(kGroupThreads) void decode_kernel(const void* __restrict__ coefs,
+__global__ __launch_bounds__(kGroupThreads, 4) void decode_kernel(const void* __restrict__ coefs,
                                                               const int* __restrict__ qt_pool,
                                                               const FrameDev* __restrict__ frames, int nframes,
                                                               int64_t total_tasks, uint8_t* __restrict__ out)
@@ -310,12 +335,12 @@ __global__ __launch_bounds__(kGroupThreads) void decode_kernel(const void* __res
 #pragma unroll
     for (int c = 0; c < 8; ++c) zoff[c] = 2 * zz_of_natural(r * 8 + c);
 
-    int q[3][8];
+    uint32_t q[3][4];   // this lane's row of each component's qtable, 16-bit pairs
     int q_tables[3] = {-1, -1, -1};
 #pragma unroll
     for (int c = 0; c < 3; ++c)
 #pragma unroll
-        for (int k = 0; k < 8; ++k) q[c][k] = 0;
+        for (int k = 0; k < 4; ++k) q[c][k] = 0;
 
     FrameCursor pc;   // frame of the task being prefetched
     cursor_seek(pc, frames, nframes, total_tasks, t_begin);
@@ -345,9 +370,11 @@ __global__ __launch_bounds__(kGroupThreads) void decode_kernel(const void* __res
 #pragma unroll
                 for (int c = 0; c < 3; ++c) {
                     const int4* qp = reinterpret_cast<const int4*>(qt_pool + q_tables[c] * 64 + r * 8);
-                    const int4 a = qp[0], b = qp[1];
-                    q[c][0] = a.x; q[c][1] = a.y; q[c][2] = a.z; q[c][3] = a.w;
-                    q[c][4] = b.x; q[c][5] = b.y; q[c][6] = b.z; q[c][7] = b.w;
+                    const int4 a = qp[0], b = qp[1];   // DQT entries are <= 65535
+                    q[c][0] = (a.x & 0xffff) | (a.y << 16);
+                    q[c][1] = (a.z & 0xffff) | (a.w << 16);
+                    q[c][2] = (b.x & 0xffff) | (b.y << 16);
+                    q[c][3] = (b.z & 0xffff) | (b.w << 16);
                 }
             }
 #pragma unroll
