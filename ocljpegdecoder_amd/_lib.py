@@ -9,7 +9,7 @@ import ctypes
 import os
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG, "lib", "libhjd.so")
+LIB_PATH = os.environ.get("HJD_LIB") or os.path.join(_PKG, "lib", "libhjd.so")   # HJD_LIB: tuning builds only
 
 c_i32p = ctypes.POINTER(ctypes.c_int32)
 c_u32p = ctypes.POINTER(ctypes.c_uint32)

@@ -133,6 +133,9 @@ __device__ __forceinline__ TaskGeom task_geom(const FrameCursor& c, int64_t task
 // Kernel variants (hjd_plan_set_variant): bit 0 = plain instead of
 // non-temporal 16-byte output stores.
 constexpr int kVarPlainStores = 1;
+// Ablation bits: compiled into the tuning-only library (HJD_ABLATION, see
+// tools/build_native.py --ablation); their outputs are deliberately wrong.
+constexpr int kAblNoStore = 4, kAblNoColour = 8, kAblNoIdct = 16;
 
 // 4 horizontally adjacent BGRX pixels.  kFull: the whole strip row lies inside
 // the frame and rows are 16-byte aligned -> one global_store_dwordx4 (nt by
@@ -142,6 +145,10 @@ __device__ __forceinline__ void store4(uint8_t* __restrict__ row, int x, int wid
                                        uint32_t p2, uint32_t p3)
 {
     uint32_t* dst = reinterpret_cast<uint32_t*>(row) + x;
+    if constexpr ((kVariant & kAblNoStore) != 0) {
+        asm volatile("" ::"v"(p0), "v"(p1), "v"(p2), "v"(p3));
+        return;
+    }
     if constexpr (kFull) {
         typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
         const u32x4 v = {p0, p1, p2, p3};
@@ -359,7 +366,10 @@ __global__ __launch_bounds__(kGroupThreads, 4) void decode_kernel(const void* __
             }
         }
     };
-    if constexpr (kFmt == 0) prefetch(task_geom<kSampling>(pc, t_begin));
+    if constexpr (kFmt == 0) {
+        prefetch(task_geom<kSampling>(pc, t_begin));
+        __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0): see the edge-strip drain below
+    }
 
     for (int64_t task = t_begin; task < t_end; ++task) {
         const FrameCursor cc = pc;
@@ -391,15 +401,23 @@ __global__ __launch_bounds__(kGroupThreads, 4) void decode_kernel(const void* __
             if (task + 1 < t_end && task + 1 >= pc.end) cursor_load(pc, frames, nframes, total_tasks, pc.idx + 1);
         }
 
-        idct_stage<kSampling, kFmt>(slots, rowbuf, lane, zoff, q,
-                                    static_cast<const int*>(coefs) + tg.blk0 * 64, tg.nblk);
+        if constexpr ((kVariant & kAblNoIdct) == 0)
+            idct_stage<kSampling, kFmt>(slots, rowbuf, lane, zoff, q,
+                                        static_cast<const int*>(coefs) + tg.blk0 * 64, tg.nblk);
 
         constexpr int kRows = kSampling == 1 ? 16 : 8;
         uint8_t* fout = out + cc.out_base;
-        if (cc.vec_ok && tg.x_base + 128 <= cc.width && tg.y_base + kRows <= cc.height)
+        if constexpr ((kVariant & kAblNoColour) != 0) {
+            (void)fout;
+        } else if (cc.vec_ok && tg.x_base + 128 <= cc.width && tg.y_base + kRows <= cc.height)
             colour_stage<kSampling, true, kVariant>(slots, lane, fout, cc.pitch, cc.width, cc.height, tg.y_base, tg.x_base);
-        else
+        else {
             colour_stage<kSampling, false, kVariant>(slots, lane, fout, cc.pitch, cc.width, cc.height, tg.y_base, tg.x_base);
+            // Edge strips issue a data-dependent number of stores; drain them
+            // here so the loop head's wait for the prefetched coefficients can
+            // be a fixed vmcnt (the full path's stores may stay in flight).
+            __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0)
+        }
         wave_lds_sync();
     }
 }

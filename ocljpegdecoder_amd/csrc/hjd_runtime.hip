@@ -118,6 +118,26 @@ int hjd_internal::launch_decode(int device, int num_cu, int sampling, int input_
     HJD_HIP(hipSetDevice(device));
     const int grid = grid_blocks > 0 ? grid_blocks : default_grid_cu(num_cu, tasks);
     const int fmt = input_format == HJD_IN_Q16_ZIGZAG ? 0 : 1;
+#ifdef HJD_ABLATION
+    if (fmt == 0 && variant > 1) {
+        using KA = void (*)(const void*, const int*, const FrameDev*, int, int64_t, uint8_t*);
+        KA k = nullptr;
+        const bool s420 = sampling == HJD_YUV420;
+        switch (variant) {
+        case 4: k = s420 ? hjd::decode_kernel<1, 0, 4> : hjd::decode_kernel<0, 0, 4>; break;
+        case 8: k = s420 ? hjd::decode_kernel<1, 0, 8> : hjd::decode_kernel<0, 0, 8>; break;
+        case 16: k = s420 ? hjd::decode_kernel<1, 0, 16> : hjd::decode_kernel<0, 0, 16>; break;
+        case 20: k = s420 ? hjd::decode_kernel<1, 0, 20> : hjd::decode_kernel<0, 0, 20>; break;
+        case 24: k = s420 ? hjd::decode_kernel<1, 0, 24> : hjd::decode_kernel<0, 0, 24>; break;
+        default: return hjd_internal::set_error(HJD_E_INVALID, "unknown ablation variant %d", variant);
+        }
+        hipLaunchKernelGGL(k, dim3(grid), dim3(hjd::kGroupThreads), 0, static_cast<hipStream_t>(stream), d_coefs,
+                           d_qt_nat, reinterpret_cast<const FrameDev*>(d_frames), nframes, tasks,
+                           static_cast<uint8_t*>(d_out));
+        HJD_HIP(hipGetLastError());
+        return HJD_OK;
+    }
+#endif
     const int key = (sampling == HJD_YUV420 ? 4 : 0) | (fmt << 1) | (variant & 1);
     using K = void (*)(const void*, const int*, const FrameDev*, int, int64_t, uint8_t*);
     static const K kTable[8] = {
@@ -294,7 +314,11 @@ int hjd_plan_destroy(hjd_plan* plan)
 int hjd_plan_set_variant(hjd_plan* plan, int variant)
 {
     if (!plan) return fail(HJD_E_INVALID, "plan is NULL");
+#ifdef HJD_ABLATION
+    if (variant < 0 || variant > 31) return fail(HJD_E_INVALID, "unknown kernel variant %d", variant);
+#else
     if (variant < 0 || variant > 1) return fail(HJD_E_INVALID, "unknown kernel variant %d", variant);
+#endif
     plan->variant = variant;
     return HJD_OK;
 }

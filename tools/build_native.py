@@ -50,7 +50,16 @@ def _headers():
     return hs
 
 
-def build(verbose: bool = False, force: bool = False) -> str:
+def build(verbose: bool = False, force: bool = False, ablation: bool = False) -> str:
+    """ablation=True builds the TUNING-ONLY library build/ablation/libhjd.so with
+    -DHJD_ABLATION (stage-skipping kernel variants for tools/tune.py; wrong
+    outputs by design).  Load it with HJD_LIB=build/ablation/libhjd.so."""
+    global LIBDIR, LIB, OBJDIR
+    if ablation:
+        LIBDIR = os.path.join(REPO, "build", "ablation")
+        LIB = os.path.join(LIBDIR, "libhjd.so")
+        OBJDIR = os.path.join(REPO, "build", "obj_ablation")
+        COMMON.append("-DHJD_ABLATION")
     os.makedirs(LIBDIR, exist_ok=True)
     os.makedirs(OBJDIR, exist_ok=True)
     headers = _headers()
@@ -85,4 +94,4 @@ def build(verbose: bool = False, force: bool = False) -> str:
 
 
 if __name__ == "__main__":
-    print(build(verbose=True, force="--force" in sys.argv))
+    print(build(verbose=True, force="--force" in sys.argv, ablation="--ablation" in sys.argv))

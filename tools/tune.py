@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--variants", default="0,1")
     ap.add_argument("--grids", default="0")
+    ap.add_argument("--no-check", action="store_true", help="ablation variants: outputs differ by design")
     args = ap.parse_args()
 
     import torch
@@ -66,7 +67,7 @@ def main():
                 e1.record(stream)
                 torch.cuda.synchronize()
                 times[(v, g)].append(e0.elapsed_time(e1) / args.reps)
-                if rnd == 0:
+                if rnd == 0 and not args.no_check:
                     sig = int(out[:, ::97, ::89].sum().item())
                     ref = sig if ref is None else ref
                     assert sig == ref, f"variant {v} grid {g} output differs"
