@@ -129,15 +129,28 @@ constexpr int kBK = 1858077, kBBias = (128 << 20) + 2097;
 __host__ __device__ __forceinline__ int r_term(int v) { return (mul24(v, kRK) + kRBias) >> 20; }
 __host__ __device__ __forceinline__ int b_term(int u) { return (mul24(u, kBK) + kBBias) >> 20; }
 
-// floor(-(17207u + 35707v) / 50000) + 128, exactly.  The fp32 estimate is
-// biased down by 5e-5 (> its worst-case error of 2.2e-5 for |m| < 2^24) so it
-// is floor or floor-1; one remainder test fixes it.
-__device__ __forceinline__ int g_term(int u, int v)
+// floor(-(17207u + 35707v) / 50000) + 128, exactly, with one multiply-high:
+// m' = -(17207u + 35707v) + 300*50000 lies in [1.5e6, 2.9e7] < 2^25, and
+// floor(m'/50000) == mulhi(m', 2814749768) >> 15 for every m' < 2^25
+// (2814749768 = ceil(2^47/50000); exhaustively checked in
+// tests/test_oracle.py::test_fixed_point_colour_terms).  The offset's 300 is
+// removed together with the +128 level shift (-172).  m' also identifies the
+// double-rounding corner: (U,V) = (-200,200) is the only grid point with
+// m' = 11,300,000.
+constexpr int kGOffset = 15000000;
+constexpr unsigned kGMagic = 2814749768u;
+constexpr int kGSpecial = 11300000;
+
+__host__ __device__ __forceinline__ int g_mprime(int u, int v) { return mul24(u, -17207) + mul24(v, -35707) + kGOffset; }
+
+__host__ __device__ __forceinline__ int g_term_from_m(int mp)
 {
-    const int m = mul24(u, -17207) + mul24(v, -35707);
-    const int q0 = __float2int_rd(__builtin_fmaf(static_cast<float>(m), 2.0e-5f, -5.0e-5f));
-    const int r = m + mul24(q0, -50000);
-    return q0 + (r >= 50000 ? 129 : 128);
+#if defined(__HIP_DEVICE_COMPILE__)
+    const unsigned hi = __umulhi(static_cast<unsigned>(mp), kGMagic);
+#else
+    const unsigned hi = static_cast<unsigned>((static_cast<unsigned long long>(static_cast<unsigned>(mp)) * kGMagic) >> 32);
+#endif
+    return static_cast<int>(hi >> 15) - 172;
 }
 
 __device__ __forceinline__ ChromaTerms chroma_terms(int u, int v)
@@ -145,8 +158,9 @@ __device__ __forceinline__ ChromaTerms chroma_terms(int u, int v)
     ChromaTerms t;
     t.rq = r_term(v);
     t.bq = b_term(u);
-    t.gq = g_term(u, v);
-    t.special = (u == -200) & (v == 200);
+    const int mp = g_mprime(u, v);
+    t.gq = g_term_from_m(mp);
+    t.special = mp == kGSpecial;
     return t;
 }
 

@@ -94,20 +94,38 @@ def test_oracle_csc_exhaustive_hash():
     assert h.hexdigest() == O.manifest()["csc_exhaustive_sha256"]
 
 
+RK, RBIAS = 1470091, (128 << 20) + 1048
+BK, BBIAS = 1858077, (128 << 20) + 2097
+GOFF, GMAGIC, GSPECIAL = 15000000, 2814749768, 11300000
+
+
 def integer_csc(y, u, v):
     """numpy model of the kernel's exact-integer colour formulation
-    (csrc/hjd_device.hpp chroma_terms/pixel_bgrx)."""
+    (csrc/hjd_device.hpp r_term / b_term / g_mprime / g_term_from_m / pixels2)."""
     y = y.astype(np.int64); u = u.astype(np.int64); v = v.astype(np.int64)
-    rq = np.floor(v.astype(np.float32) * np.float32(1.402)).astype(np.int64)
-    bq = np.floor(u.astype(np.float32) * np.float32(1.772)).astype(np.int64)
-    n = -(17207 * u + 35707 * v)
-    gq = n // 50000                      # exact floor division
-    special = (u == -200) & (v == 200) & (y >= 188) & (y <= 201)
-    yb = y + 128
-    r = np.clip(yb + rq, 0, 255)
-    g = np.clip(yb + gq - special, 0, 255)
-    b = np.clip(yb + bq, 0, 255)
+    rq = (v * RK + RBIAS) >> 20                       # floor(1.402 v) + 128
+    bq = (u * BK + BBIAS) >> 20                       # floor(1.772 u) + 128
+    mp = -17207 * u - 35707 * v + GOFF
+    gq = ((mp.astype(np.uint64) * np.uint64(GMAGIC)) >> np.uint64(47)).astype(np.int64) - 172
+    special = (mp == GSPECIAL) & (y >= 188) & (y <= 201)
+    r = np.clip(y + rq, 0, 255)
+    g = np.clip(y + gq - special, 0, 255)
+    b = np.clip(y + bq, 0, 255)
     return ((r << 16) | (g << 8) | b).astype(np.uint32)
+
+
+def test_fixed_point_colour_terms():
+    """The constants of the device formulation, exhaustively on their domains."""
+    x = np.arange(-256, 256, dtype=np.int64)
+    assert ((x * RK + RBIAS) >> 20 == np.floor_divide(701 * x, 500) + 128).all()
+    assert ((x * BK + BBIAS) >> 20 == np.floor_divide(443 * x, 250) + 128).all()
+    assert RK < 2 ** 23 and BK < 2 ** 23 and 256 * max(RK, BK) + RBIAS + 4096 < 2 ** 31   # 24-bit multiply, no overflow
+    m = np.arange(0, 1 << 25, dtype=np.uint64)
+    assert ((m * np.uint64(GMAGIC)) >> np.uint64(47) == m // 50000).all()
+    u, v = np.meshgrid(x, x, indexing="ij")
+    mp = -17207 * u - 35707 * v + GOFF
+    assert mp.min() >= 0 and mp.max() < 2 ** 25
+    assert np.argwhere(mp == GSPECIAL).tolist() == [[56, 456]]   # (U,V) = (-200, 200) only
 
 
 def test_integer_csc_formulation_is_exact():

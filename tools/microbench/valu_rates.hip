@@ -1,0 +1,83 @@
+// VALU throughput probe (tuning tool, not product): cycles per wave64
+// instruction per SIMD for the integer/packed ops the pixel kernel uses.
+// 8 independent chains per lane, 256 WGs x 1024 threads (16 waves/CU... 4/SIMD), timed by events.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+
+#define N_ITER 4096
+#define CHAIN 8
+
+template <int OP>
+__global__ __launch_bounds__(256) void probe(uint32_t* out, uint32_t seed)
+{
+    uint32_t a[CHAIN];
+    for (int i = 0; i < CHAIN; ++i) a[i] = seed + threadIdx.x * 7 + i * 13;
+    const uint32_t k = seed | 1;
+    for (int it = 0; it < N_ITER; ++it) {
+#pragma unroll
+        for (int i = 0; i < CHAIN; ++i) {
+            uint32_t x = a[i];
+            if constexpr (OP == 0) asm volatile("v_add_u32 %0, %0, %1" : "+v"(x) : "v"(k));
+            if constexpr (OP == 1) asm volatile("v_mad_i32_i24 %0, %0, %1, %1" : "+v"(x) : "v"(k));
+            if constexpr (OP == 2) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(x) : "v"(k));
+            if constexpr (OP == 3) asm volatile("v_med3_i32 %0, %0, %1, %2" : "+v"(x) : "v"(k), "v"(k + 255));
+            if constexpr (OP == 4) asm volatile("v_pk_add_u16 %0, %0, %1" : "+v"(x) : "v"(k));
+            if constexpr (OP == 5) asm volatile("v_perm_b32 %0, %0, %1, %1" : "+v"(x) : "v"(k));
+            if constexpr (OP == 6) asm volatile("v_cvt_f32_i32 %0, %0" : "+v"(x));
+            if constexpr (OP == 7) asm volatile("v_fma_f32 %0, %0, %1, %1" : "+v"(x) : "v"(k));
+            if constexpr (OP == 8) asm volatile("v_pk_max_i16 %0, %0, %1" : "+v"(x) : "v"(k));
+            if constexpr (OP == 9) asm volatile("v_ashrrev_i32 %0, 3, %0" : "+v"(x));
+            if constexpr (OP == 10) asm volatile("v_mul_i32_i24 %0, %0, %1" : "+v"(x) : "v"(k));
+            if constexpr (OP == 11) asm volatile("v_cvt_flr_i32_f32 %0, %0" : "+v"(x));
+            if constexpr (OP == 12) asm volatile("v_lshl_add_u32 %0, %0, 2, %1" : "+v"(x) : "v"(k));
+            if constexpr (OP == 13) asm volatile("v_add3_u32 %0, %0, %1, %1" : "+v"(x) : "v"(k));
+            a[i] = x;
+        }
+    }
+    uint32_t s = 0;
+    for (int i = 0; i < CHAIN; ++i) s ^= a[i];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
+template <int OP>
+float run(uint32_t* out, int blocks, const char* name)
+{
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
+    hipLaunchKernelGGL(probe<OP>, dim3(blocks), dim3(256), 0, 0, out, 1u);
+    (void)hipEventRecord(e0);
+    hipLaunchKernelGGL(probe<OP>, dim3(blocks), dim3(256), 0, 0, out, 3u);
+    (void)hipEventRecord(e1);
+    (void)hipEventSynchronize(e1);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    // instructions per SIMD: blocks*4 waves spread over 256 CUs x 4 SIMDs
+    const double waves_per_simd = blocks * 4.0 / (256 * 4);
+    const double instr = waves_per_simd * N_ITER * CHAIN;
+    const double clk = 2.1e9;   // approx; also print ns per instr
+    printf("%-20s %8.3f ms  %.2f ns/instr/SIMD  ~%.2f cyc@2.1GHz\n", name, ms, ms * 1e6 / instr, ms * 1e-3 * clk / instr);
+    return ms;
+}
+
+int main()
+{
+    uint32_t* out;
+    const int blocks = 256 * 4;   // 4 WG/CU of 4 waves = 4 waves per SIMD
+    (void)hipMalloc(&out, blocks * 256 * 4);
+    run<0>(out, blocks, "v_add_u32");
+    run<1>(out, blocks, "v_mad_i32_i24");
+    run<2>(out, blocks, "v_mul_lo_u32");
+    run<3>(out, blocks, "v_med3_i32");
+    run<4>(out, blocks, "v_pk_add_u16");
+    run<5>(out, blocks, "v_perm_b32");
+    run<6>(out, blocks, "v_cvt_f32_i32");
+    run<7>(out, blocks, "v_fma_f32");
+    run<8>(out, blocks, "v_pk_max_i16");
+    run<9>(out, blocks, "v_ashrrev_i32");
+    run<10>(out, blocks, "v_mul_i32_i24");
+    run<11>(out, blocks, "v_cvt_flr_i32_f32");
+    run<12>(out, blocks, "v_lshl_add_u32");
+    run<13>(out, blocks, "v_add3_u32");
+    return 0;
+}
