@@ -95,7 +95,8 @@ int hjd_plan_create(hjd_ctx* ctx, const hjd_frame* frames, int nframes, int inpu
                     const int32_t* qtables, int nq, hjd_plan** out);
 int hjd_plan_destroy(hjd_plan* plan);
 /* Tuning hook: kernel variant bits (0 = default).  bit 0: plain instead of
- * non-temporal output stores.  Results are identical for every variant. */
+ * non-temporal output stores; bit 1: workgroup-interleaved task order.
+ * Results are identical for every variant. */
 int hjd_plan_set_variant(hjd_plan* plan, int variant);
 int64_t hjd_plan_tasks(const hjd_plan* plan);      /* work items (strips) */
 int64_t hjd_plan_pixels(const hjd_plan* plan);     /* visible pixels */
@@ -105,7 +106,9 @@ int64_t hjd_plan_coef_bytes(const hjd_plan* plan); /* algorithmic input bytes */
  * Enqueue the fused decode of every frame of the plan on `stream` (async).
  * d_coefs: coefficient buffer (int16 or int32 per the plan's format);
  * d_out: output buffer (frames at their out_offset).  Both 16-byte aligned.
- * grid_blocks: persistent grid size in 256-thread workgroups (0 = default).
+ * grid_blocks: grid size in 256-thread workgroups; 0 = default (short task
+ * chunks per wave over many more groups than are resident, which keeps the
+ * resident waves inside a narrow window of the batch).
  * The input is never modified (the reference kernel's in-place IDCT,
  * src/idct8x8.cl:136-155, is not reproduced).
  */

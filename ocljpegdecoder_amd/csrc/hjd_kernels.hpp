@@ -54,12 +54,14 @@ __device__ __forceinline__ int zz_of_natural(int n)
     return kInv[n];
 }
 
+// Cross-lane hand-off through the wave's private LDS slice.  The DS
+// instructions of one wave execute in issue order, so a ds_read issued after a
+// ds_write sees its data without any s_waitcnt; this only stops the compiler
+// from reordering LDS accesses across the point (it still inserts the counted
+// lgkmcnt waits where read results are consumed).
 __device__ __forceinline__ void wave_lds_sync()
 {
-    // LDS ops of one wave execute in order; this stops the compiler from
-    // moving LDS accesses across the point and waits for outstanding ones.
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
@@ -133,6 +135,10 @@ __device__ __forceinline__ TaskGeom task_geom(const FrameCursor& c, int64_t task
 // Kernel variants (hjd_plan_set_variant): bit 0 = plain instead of
 // non-temporal 16-byte output stores.
 constexpr int kVarPlainStores = 1;
+// bit 1: workgroup-interleaved task order (wave w of a group takes tasks
+// 4q + w of the group's contiguous quad range) instead of one contiguous range
+// per wave: the group's 4 waves then write adjacent 512-byte row segments.
+constexpr int kVarWgInterleave = 2;
 // Ablation bits: compiled into the tuning-only library (HJD_ABLATION, see
 // tools/build_native.py --ablation); their outputs are deliberately wrong.
 constexpr int kAblNoStore = 4, kAblNoColour = 8, kAblNoIdct = 16;
@@ -262,35 +268,50 @@ __device__ __forceinline__ constexpr int round_component(int i)
 // LDS slots; kFmt 1: int32 natural rows read straight from global memory.
 // Samples end up as int16 row-major in the block slots.
 template <int kSampling, int kFmt>
+__device__ __forceinline__ void load_round(const char* __restrict__ slots, int lane, int i, const int (&zoff)[8],
+                                           const uint32_t (&q)[3][4], const int* __restrict__ src32, int nblk,
+                                           int (&v)[8])
+{
+    const int g = lane >> 3, r = lane & 7;
+    const int b = 6 * g + i;
+    const int comp = round_component<kSampling>(i);
+    if constexpr (kFmt == 0) {
+        const char* blk = slots + b * kSlotBytes;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const int coef = *reinterpret_cast<const short*>(blk + zoff[c]);
+            const uint32_t qq = q[comp][c >> 1];   // two 16-bit factors per VGPR
+            const int qc = (c & 1) ? static_cast<int>(qq >> 16) : static_cast<int>(qq & 0xffffu);
+            v[c] = mul24(coef, qc);   // dequant (src/decoder.cpp:340)
+        }
+    } else {
+        int4 lo = make_int4(0, 0, 0, 0), hi = lo;
+        if (b < nblk) {   // lanes past the strip's last block compute on zeros
+            const int4* p = reinterpret_cast<const int4*>(src32 + b * 64 + r * 8);
+            lo = p[0];
+            hi = p[1];
+        }
+        v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
+        v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+    }
+}
+
+// IDCT of the task's 48 blocks (6 rounds).  kFmt 0: int16 zigzag staged in the
+// LDS slots; kFmt 1: int32 natural rows read straight from global memory.
+// Samples end up as int16 row-major in the block slots.  The next round's
+// coefficient gathers are issued before this round's column math, so their
+// LDS latency overlaps it.
+template <int kSampling, int kFmt>
 __device__ __forceinline__ void idct_stage(char* __restrict__ slots, char* __restrict__ rowbuf, int lane,
                                            const int (&zoff)[8], const uint32_t (&q)[3][4],
                                            const int* __restrict__ src32, int nblk)
 {
     const int g = lane >> 3, r = lane & 7;
+    int v[8];
+    load_round<kSampling, kFmt>(slots, lane, 0, zoff, q, src32, nblk, v);
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
         const int b = 6 * g + i;
-        const int comp = round_component<kSampling>(i);
-        int v[8];
-        if constexpr (kFmt == 0) {
-            const char* blk = slots + b * kSlotBytes;
-#pragma unroll
-            for (int c = 0; c < 8; ++c) {
-                const int coef = *reinterpret_cast<const short*>(blk + zoff[c]);
-                const uint32_t qq = q[comp][c >> 1];   // two 16-bit factors per VGPR
-                const int qc = (c & 1) ? static_cast<int>(qq >> 16) : static_cast<int>(qq & 0xffffu);
-                v[c] = mul24(coef, qc);   // dequant (src/decoder.cpp:340)
-            }
-        } else {
-            int4 lo = make_int4(0, 0, 0, 0), hi = lo;
-            if (b < nblk) {   // lanes past the strip's last block compute on zeros
-                const int4* p = reinterpret_cast<const int4*>(src32 + b * 64 + r * 8);
-                lo = p[0];
-                hi = p[1];
-            }
-            v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
-            v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
-        }
         idct8<false>(v);
         {
             int4* dst = reinterpret_cast<int4*>(rowbuf + g * kRowBufBlock + r * kRowStride);
@@ -298,16 +319,18 @@ __device__ __forceinline__ void idct_stage(char* __restrict__ slots, char* __res
             dst[1] = make_int4(v[4], v[5], v[6], v[7]);
         }
         wave_lds_sync();
+        int c8[8];
         {
             const char* col = rowbuf + g * kRowBufBlock + r * 4;
 #pragma unroll
-            for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const int*>(col + k * kRowStride);
+            for (int k = 0; k < 8; ++k) c8[k] = *reinterpret_cast<const int*>(col + k * kRowStride);
         }
-        idct8<true>(v);
+        if (i + 1 < 6) load_round<kSampling, kFmt>(slots, lane, i + 1, zoff, q, src32, nblk, v);
+        idct8<true>(c8);
         {
             char* blk = slots + b * kSlotBytes + r * 2;   // column r
 #pragma unroll
-            for (int k = 0; k < 8; ++k) *reinterpret_cast<short*>(blk + k * 16) = static_cast<short>(v[k]);
+            for (int k = 0; k < 8; ++k) *reinterpret_cast<short*>(blk + k * 16) = static_cast<short>(c8[k]);
         }
         wave_lds_sync();
     }
@@ -330,12 +353,24 @@ __global__ __launch_bounds__(kGroupThreads, 4) void decode_kernel(const void* __
     char* rowbuf = slots + kTaskBlocks * kSlotBytes;
     const int r = lane & 7;
 
-    // this wave's contiguous task range
-    const int64_t nwaves = static_cast<int64_t>(gridDim.x) * kWavesPerGroup;
-    const int64_t gw = static_cast<int64_t>(blockIdx.x) * kWavesPerGroup + wave;
-    const int64_t chunk = total_tasks / nwaves, rem = total_tasks % nwaves;
-    const int64_t t_begin = gw * chunk + min(gw, rem);
-    const int64_t t_end = t_begin + chunk + (gw < rem ? 1 : 0);
+    // this wave's task sequence: t_begin, t_begin + t_step, ... (< t_end)
+    int64_t t_begin, t_end, t_step;
+    if constexpr ((kVariant & kVarWgInterleave) != 0) {
+        const int64_t nquads = (total_tasks + kWavesPerGroup - 1) / kWavesPerGroup;
+        const int64_t chunk = nquads / gridDim.x, rem = nquads % gridDim.x;
+        const int64_t qb = static_cast<int64_t>(blockIdx.x) * chunk + min<int64_t>(blockIdx.x, rem);
+        const int64_t qe = qb + chunk + (blockIdx.x < rem ? 1 : 0);
+        t_begin = qb * kWavesPerGroup + wave;
+        t_end = min<int64_t>(qe * kWavesPerGroup, total_tasks);
+        t_step = kWavesPerGroup;
+    } else {
+        const int64_t nwaves = static_cast<int64_t>(gridDim.x) * kWavesPerGroup;
+        const int64_t gw = static_cast<int64_t>(blockIdx.x) * kWavesPerGroup + wave;
+        const int64_t chunk = total_tasks / nwaves, rem = total_tasks % nwaves;
+        t_begin = gw * chunk + min(gw, rem);
+        t_end = t_begin + chunk + (gw < rem ? 1 : 0);
+        t_step = 1;
+    }
     if (t_begin >= t_end) return;
 
     int zoff[8];
@@ -371,7 +406,7 @@ __global__ __launch_bounds__(kGroupThreads, 4) void decode_kernel(const void* __
         __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0): see the edge-strip drain below
     }
 
-    for (int64_t task = t_begin; task < t_end; ++task) {
+    for (int64_t task = t_begin; task < t_end; task += t_step) {
         const FrameCursor cc = pc;
         const TaskGeom tg = task_geom<kSampling>(cc, task);
         if constexpr (kFmt == 0) {
@@ -393,12 +428,13 @@ __global__ __launch_bounds__(kGroupThreads, 4) void decode_kernel(const void* __
                 *reinterpret_cast<int4*>(slots + (j >> 3) * kSlotBytes + (j & 7) * 16) = pre[k];
             }
             wave_lds_sync();
-            if (task + 1 < t_end) {
-                if (task + 1 >= pc.end) cursor_load(pc, frames, nframes, total_tasks, pc.idx + 1);
-                prefetch(task_geom<kSampling>(pc, task + 1));
+            if (task + t_step < t_end) {
+                while (task + t_step >= pc.end) cursor_load(pc, frames, nframes, total_tasks, pc.idx + 1);
+                prefetch(task_geom<kSampling>(pc, task + t_step));
             }
         } else {
-            if (task + 1 < t_end && task + 1 >= pc.end) cursor_load(pc, frames, nframes, total_tasks, pc.idx + 1);
+            if (task + t_step < t_end)
+                while (task + t_step >= pc.end) cursor_load(pc, frames, nframes, total_tasks, pc.idx + 1);
         }
 
         if constexpr ((kVariant & kAblNoIdct) == 0)

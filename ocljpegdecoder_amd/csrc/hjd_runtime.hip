@@ -83,6 +83,7 @@ struct hjd_plan {
 
 static int geometry(int width, int height, int sampling, int& mcu_w, int& mcu_h, int& bpm, int& mpx);
 static int default_grid_cu(int num_cu, int64_t work_waves);
+static int decode_grid(int sampling, int fmt, int64_t tasks);
 
 int hjd_internal::ctx_num_cu(const hjd_ctx* ctx) { return ctx->num_cu; }
 
@@ -116,8 +117,9 @@ int hjd_internal::launch_decode(int device, int num_cu, int sampling, int input_
                                 int nframes, int64_t tasks, void* d_out, void* stream, int grid_blocks)
 {
     HJD_HIP(hipSetDevice(device));
-    const int grid = grid_blocks > 0 ? grid_blocks : default_grid_cu(num_cu, tasks);
     const int fmt = input_format == HJD_IN_Q16_ZIGZAG ? 0 : 1;
+    (void)num_cu;
+    const int grid = grid_blocks > 0 ? grid_blocks : decode_grid(sampling, fmt, tasks);
 #ifdef HJD_ABLATION
     if (fmt == 0 && variant > 1) {
         using KA = void (*)(const void*, const int*, const FrameDev*, int, int64_t, uint8_t*);
@@ -138,12 +140,15 @@ int hjd_internal::launch_decode(int device, int num_cu, int sampling, int input_
         return HJD_OK;
     }
 #endif
-    const int key = (sampling == HJD_YUV420 ? 4 : 0) | (fmt << 1) | (variant & 1);
+    const int key = (sampling == HJD_YUV420 ? 8 : 0) | (fmt << 2) | (variant & 3);
     using K = void (*)(const void*, const int*, const FrameDev*, int, int64_t, uint8_t*);
-    static const K kTable[8] = {
-        hjd::decode_kernel<0, 0, 0>, hjd::decode_kernel<0, 0, 1>, hjd::decode_kernel<0, 1, 0>,
-        hjd::decode_kernel<0, 1, 1>, hjd::decode_kernel<1, 0, 0>, hjd::decode_kernel<1, 0, 1>,
-        hjd::decode_kernel<1, 1, 0>, hjd::decode_kernel<1, 1, 1>};
+    static const K kTable[16] = {
+        hjd::decode_kernel<0, 0, 0>, hjd::decode_kernel<0, 0, 1>, hjd::decode_kernel<0, 0, 2>,
+        hjd::decode_kernel<0, 0, 3>, hjd::decode_kernel<0, 1, 0>, hjd::decode_kernel<0, 1, 1>,
+        hjd::decode_kernel<0, 1, 2>, hjd::decode_kernel<0, 1, 3>, hjd::decode_kernel<1, 0, 0>,
+        hjd::decode_kernel<1, 0, 1>, hjd::decode_kernel<1, 0, 2>, hjd::decode_kernel<1, 0, 3>,
+        hjd::decode_kernel<1, 1, 0>, hjd::decode_kernel<1, 1, 1>, hjd::decode_kernel<1, 1, 2>,
+        hjd::decode_kernel<1, 1, 3>};
     hipLaunchKernelGGL(kTable[key], dim3(grid), dim3(hjd::kGroupThreads), 0, static_cast<hipStream_t>(stream),
                        d_coefs, d_qt_nat, reinterpret_cast<const FrameDev*>(d_frames), nframes, tasks,
                        static_cast<uint8_t*>(d_out));
@@ -317,7 +322,7 @@ int hjd_plan_set_variant(hjd_plan* plan, int variant)
 #ifdef HJD_ABLATION
     if (variant < 0 || variant > 31) return fail(HJD_E_INVALID, "unknown kernel variant %d", variant);
 #else
-    if (variant < 0 || variant > 1) return fail(HJD_E_INVALID, "unknown kernel variant %d", variant);
+    if (variant < 0 || variant > 3) return fail(HJD_E_INVALID, "unknown kernel variant %d", variant);
 #endif
     plan->variant = variant;
     return HJD_OK;
@@ -333,6 +338,22 @@ static int default_grid_cu(int num_cu, int64_t work_waves)
     const int64_t cap = static_cast<int64_t>(num_cu) * 4;
     const int64_t need = (work_waves + hjd::kWavesPerGroup - 1) / hjd::kWavesPerGroup;
     return static_cast<int>(std::max<int64_t>(1, std::min(cap, need)));
+}
+
+// Grid of the fused kernel: short contiguous task chunks per wave and many
+// more workgroups than fit at once (measured on MI355X, profiles/
+// r01_tune_grid_*.json): the hardware dispatches groups in order, so the
+// resident waves always work inside a narrow window of the batch and HBM sees
+// far better locality than with 4096 persistent waves spread over the whole
+// batch (4:2:0 +12 %, 4:4:4 +13 % over one persistent wave per slot).  The
+// heavier 4:4:4 tasks still profit from the one-task-ahead prefetch, so their
+// waves take ~8 tasks; 4:2:0 waves take one.
+static int decode_grid(int sampling, int fmt, int64_t tasks)
+{
+    const int64_t per_wave = (sampling == HJD_YUV420 && fmt == 0) ? 1 : 8;
+    const int64_t waves = (tasks + per_wave - 1) / per_wave;
+    const int64_t groups = (waves + hjd::kWavesPerGroup - 1) / hjd::kWavesPerGroup;
+    return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(groups, int64_t(1) << 24)));
 }
 
 static int default_grid(const hjd_ctx* ctx, int64_t work_waves)
