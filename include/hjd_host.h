@@ -73,6 +73,49 @@ int hjd_stream_submit(hjd_stream* s, const uint8_t* data, size_t size, void* d_o
  * be NULL) receives {images, pixels, host_decode_ns, h2d_bytes, kernel_launches}. */
 int hjd_stream_sync(hjd_stream* s, int64_t stats[5]);
 
+/* ---- GPU entropy decoding ----------------------
+ * Replaces the single-threaded scan decode of the reference
+ * (src/decoder.cpp:221-365) with a parallel one on the GPU.  The host only
+ * parses headers and copies each scan into pinned memory without byte
+ * stuffing / RST markers (memcpy speed); the Huffman decode runs on the GPU as
+ * a self-synchronising parallel decode verified from the frame start, so its
+ * coefficients are identical to hjd_jpeg_decode_coefs on every valid file
+ * (DESIGN.md s10).  The fused pixel kernel follows on the same stream. */
+typedef struct hjd_gdec hjd_gdec;
+
+/* Capacity: max_frames JPEGs per call whose entropy-coded bytes total at most
+ * max_scan_bytes and whose coefficient blocks total at most max_blocks.
+ * sub_bits = bits per parallel subsequence (0 = default 1024; >= 32). */
+int hjd_gdec_create(hjd_ctx* ctx, int max_frames, int64_t max_scan_bytes, int64_t max_blocks, int sub_bits,
+                    hjd_gdec** out);
+int hjd_gdec_destroy(hjd_gdec* g);
+
+/* Decode n JPEGs to BGRX in device memory (d_outs[i], row pitch pitches[i];
+ * 16-byte aligned).  Asynchronous on `stream` (hipStream_t, NULL = default);
+ * the input bytes may be reused as soon as the call returns.  A later call on
+ * the same object waits for this call's uploads first. */
+int hjd_gdec_decode(hjd_gdec* g, const uint8_t* const* datas, const size_t* sizes, int n, void* const* d_outs,
+                    const int32_t* pitches, void* stream);
+
+/* Entropy decode only: int16 quantised zigzag coefficients (the HJD_IN_Q16_ZIGZAG
+ * layout), frame i at block block_offsets[i] of d_coefs (16-byte aligned). */
+int hjd_gdec_decode_coefs(hjd_gdec* g, const uint8_t* const* datas, const size_t* sizes, int n, int16_t* d_coefs,
+                          int64_t* block_offsets, void* stream);
+
+/* Wait for the last call.  status[i] (may be NULL): 0 = ok, else
+ * HJD_GDEC_CORRUPT / HJD_GDEC_COUNT bits (HJD_GDEC_SEQUENTIAL is informational).
+ * Returns HJD_E_INVALID if any frame's entropy data was corrupt. */
+int hjd_gdec_sync(hjd_gdec* g, int32_t* status);
+
+#define HJD_GDEC_SEQUENTIAL 1   /* verification fell back to the sequential path */
+#define HJD_GDEC_CORRUPT 2      /* invalid Huffman data on the decoded chain */
+#define HJD_GDEC_COUNT 4        /* fewer blocks than the frame needs */
+
+/* Test hook (no GPU): runs the same parallel algorithm on the host, one frame,
+ * and writes its coefficients.  Not a decode path. */
+int hjd_debug_entropy_emulate(const uint8_t* data, size_t size, int sub_bits, int16_t* coefs, int64_t capacity_blocks,
+                              int32_t* status);
+
 #ifdef __cplusplus
 }
 #endif

@@ -127,6 +127,16 @@ def _bind_host(lib):
         "hjd_stream_destroy": (ctypes.c_int, [vp]),
         "hjd_stream_submit": (ctypes.c_int, [vp, u8p, ctypes.c_size_t, vp, ctypes.c_int32]),
         "hjd_stream_sync": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int64)]),
+        "hjd_gdec_create": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
+                                           ctypes.POINTER(vp)]),
+        "hjd_gdec_destroy": (ctypes.c_int, [vp]),
+        "hjd_gdec_decode": (ctypes.c_int, [vp, ctypes.POINTER(u8p), ctypes.POINTER(ctypes.c_size_t), ctypes.c_int,
+                                           ctypes.POINTER(vp), c_i32p, vp]),
+        "hjd_gdec_decode_coefs": (ctypes.c_int, [vp, ctypes.POINTER(u8p), ctypes.POINTER(ctypes.c_size_t),
+                                                 ctypes.c_int, vp, ctypes.POINTER(ctypes.c_int64), vp]),
+        "hjd_gdec_sync": (ctypes.c_int, [vp, c_i32p]),
+        "hjd_debug_entropy_emulate": (ctypes.c_int, [u8p, ctypes.c_size_t, ctypes.c_int,
+                                                     ctypes.POINTER(ctypes.c_int16), ctypes.c_int64, c_i32p]),
     })
     for name, (res, args) in sigs.items():
         fn = getattr(lib, name, None)

@@ -1,0 +1,975 @@
+// hjd_entropy.hip -- GPU entropy decoding of baseline JPEG scans (include/hjd_host.h,
+// SURVEY.md s8(f) rank 3).
+//
+// Host side (per JPEG, at memcpy speed): parse the header, build the device
+// Huffman tables, copy the entropy-coded segment into pinned memory while
+// removing byte stuffing (FF00 -> FF) and RST markers, recording where each
+// restart interval ends.  Device side (one batch of frames per launch chain):
+//   ent_sync_kernel   each thread decodes its S-bit subsequence from a guessed
+//                     entry, then the workgroup iterates entry(k+1) = run(entry(k))
+//                     in LDS until nothing changes (256 subsequences per group);
+//   ent_link_kernel   one wave per group boundary re-runs the group's first
+//                     subsequences from the previous group's exit until the two
+//                     chains meet, then reduces the group's statistics;
+//   ent_fallback_kernel  frames whose chains did not meet inside a group are
+//                     redone sequentially (never seen on real data; correct anyway);
+//   ent_write_kernel  ordered segmented scan of the statistics (block index, DC
+//                     predictors) and a final run per subsequence that writes
+//                     whole int16 zigzag blocks (staged in LDS) in MCU-major order;
+// then the fused pixel kernel (hjd_kernels.hpp) turns the blocks into BGRX.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "hjd.h"
+#include "hjd_entropy.hpp"
+#include "hjd_host.h"
+#include "hjd_internal.h"
+
+using hjd_internal::FrameRecord;
+using hjd_internal::set_error;
+using namespace hjd::ent;
+
+#define HJD_HIP(expr)                                                                          \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess) return set_error(HJD_E_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+namespace {
+
+constexpr int kZigzag[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
+                             12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
+                             35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+                             58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+
+constexpr size_t kDataPad = 16;      // readable bytes after each frame's bit string
+constexpr size_t kAlign = 256;
+
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// ---------------------------------------------------------------------------
+// Host preparation
+// ---------------------------------------------------------------------------
+
+// Canonical Huffman code (T.81 C.2 / F.2.2.3) -> first-level LUT + MAXCODE.
+int build_lut(HuffLut& t, const uint8_t counts[16], const uint8_t* syms, int nsym)
+{
+    memset(&t, 0, sizeof(t));
+    int code = 0, k = 0;
+    for (int len = 1; len <= 16; ++len) {
+        const int n = counts[len - 1];
+        const int first = code;
+        for (int i = 0; i < n; ++i, ++k, ++code) {
+            if (k >= nsym || code >= (1 << len)) return -1;
+            t.vals[k] = syms[k];
+            if (len <= kLutBits) {
+                const int shift = kLutBits - len;
+                for (int r = 0; r < (1 << shift); ++r)
+                    t.lut[(code << shift) | r] = static_cast<uint16_t>((len << 8) | syms[k]);
+            }
+        }
+        t.maxcode[len] = n ? code - 1 : -1;
+        t.delta[len] = (k - n) - first;   // valptr - mincode
+        code <<= 1;
+    }
+    t.maxcode[0] = -1;
+    return 0;
+}
+
+// Copy an entropy-coded segment without byte stuffing and RST markers.  Ends
+// at the first marker that is not RSTn (normally EOI) or at the end of the
+// buffer.  seg_end receives the destuffed BIT offset where each restart
+// interval ends (the last one = total length).
+int destuff(const uint8_t* p, const uint8_t* end, uint8_t* out, size_t cap, std::vector<uint32_t>& seg_end,
+            size_t& out_len)
+{
+    uint8_t* q = out;
+    uint8_t* const qend = out + cap;
+    int nrst = 0;
+    seg_end.clear();
+    while (p < end) {
+        const uint8_t* f = static_cast<const uint8_t*>(memchr(p, 0xFF, static_cast<size_t>(end - p)));
+        const uint8_t* run_end = f ? f : end;
+        const size_t n = static_cast<size_t>(run_end - p);
+        if (q + n > qend) return set_error(HJD_E_INVALID, "scan larger than the staging capacity");
+        memcpy(q, p, n);
+        q += n;
+        p = run_end;
+        if (!f) break;
+        if (p + 1 >= end) break;                       // truncated at FF
+        const uint8_t b = p[1];
+        if (b == 0x00) {                               // stuffed FF
+            if (q >= qend) return set_error(HJD_E_INVALID, "scan larger than the staging capacity");
+            *q++ = 0xFF;
+            p += 2;
+        } else if (b == 0xFF) {                        // fill byte before a marker
+            p += 1;
+        } else if (b >= 0xD0 && b <= 0xD7) {           // RSTn (src/decoder.cpp:288-307)
+            if (b != 0xD0 + (nrst & 7))
+                return set_error(HJD_E_INVALID, "expected RST%d, found RST%d", nrst & 7, b - 0xD0);
+            seg_end.push_back(static_cast<uint32_t>((q - out) * 8));
+            ++nrst;
+            p += 2;
+        } else {
+            break;                                     // EOI (or another marker): end of scan
+        }
+    }
+    seg_end.push_back(static_cast<uint32_t>((q - out) * 8));
+    out_len = static_cast<size_t>(q - out);
+    return HJD_OK;
+}
+
+// Host-side result of preparing one JPEG.
+struct Prepared {
+    int rc = HJD_OK;
+    int width = 0, height = 0, sampling = 0, bpm = 0;
+    int64_t nblocks = 0;
+    uint32_t data_bits = 0;
+    size_t data_off = 0;       // in the batch data area
+    int ntab = 0;
+    HuffLut tabs[kMaxTables];
+    uint16_t jinfo[6] = {0, 0, 0, 0, 0, 0};
+    std::vector<uint32_t> seg_end;
+    int32_t qt[3][64];         // zigzag
+    void* d_out = nullptr;
+    int32_t pitch = 0;
+};
+
+int prepare(const uint8_t* data, size_t size, uint8_t* dst, size_t cap, Prepared& pf)
+{
+    hjd_internal::ScanHeader h;
+    int rc = hjd_internal::parse_scan_header(data, size, &h);
+    if (rc) return rc;
+    pf.width = h.width;
+    pf.height = h.height;
+    pf.sampling = h.sampling;
+    pf.bpm = h.bpm;
+    pf.nblocks = h.nblocks;
+    memcpy(pf.qt, h.qt, sizeof(pf.qt));
+    // tables referenced by the scan, deduplicated into slots
+    int slot_of[2][4];
+    for (auto& a : slot_of)
+        for (int& v : a) v = -1;
+    pf.ntab = 0;
+    for (int j = 0; j < h.bpm; ++j) {
+        const int ids[2] = {h.jdc[j], h.jac[j]};
+        int slot[2];
+        for (int cls = 0; cls < 2; ++cls) {
+            int& s = slot_of[cls][ids[cls]];
+            if (s < 0) {
+                if (pf.ntab >= kMaxTables) return set_error(HJD_E_INVALID, "too many Huffman tables");
+                s = pf.ntab++;
+                if (build_lut(pf.tabs[s], h.counts[cls][ids[cls]], h.symbols[cls][ids[cls]], h.nsym[cls][ids[cls]]))
+                    return set_error(HJD_E_INVALID, "invalid Huffman table");
+            }
+            slot[cls] = s;
+        }
+        pf.jinfo[j] = static_cast<uint16_t>(jinfo_make(slot[0], slot[1], h.jcomp[j], h.jslot[j]));
+    }
+    size_t len = 0;
+    if (h.scan_offset > size) return set_error(HJD_E_INVALID, "scan offset past the end of the file");
+    rc = destuff(data + h.scan_offset, data + size, dst, cap, pf.seg_end, len);
+    if (rc) return rc;
+    if (len == 0) return set_error(HJD_E_INVALID, "empty scan");
+    if (len >= (1u << 28)) return set_error(HJD_E_INVALID, "scan too large for one frame (>= 256 MiB)");
+    const int64_t nmcu = static_cast<int64_t>(h.mcu_w) * h.mcu_h;
+    const int64_t want = h.restart_interval > 0 ? (nmcu + h.restart_interval - 1) / h.restart_interval : 1;
+    if (static_cast<int64_t>(pf.seg_end.size()) != want)
+        return set_error(HJD_E_INVALID, "%zu restart intervals in the scan, %lld expected", pf.seg_end.size(),
+                         static_cast<long long>(want));
+    if (h.nblocks >= (1ll << 31)) return set_error(HJD_E_INVALID, "frame too large");
+    memset(dst + len, 0xFF, kDataPad);
+    pf.data_bits = static_cast<uint32_t>(len * 8);
+    return HJD_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Batch layout.  The header (frames | tables | segment ends | group->frame map |
+// pixel-kernel records | natural-order qtables) is laid out compactly per batch
+// at offset 0; the destuffed scans live at the fixed offset `data`.  Pinned
+// staging and the device blob use the same layout, so one copy moves each part.
+// ---------------------------------------------------------------------------
+struct Caps {
+    int max_frames;
+    int64_t max_scan_bytes, max_blocks;
+    int sub_bits;
+    int64_t max_subs, max_wgs, max_segs;
+    size_t hdr_cap, data;
+};
+
+Caps make_caps(int max_frames, int64_t max_scan_bytes, int64_t max_blocks, int sub_bits)
+{
+    Caps c;
+    c.max_frames = max_frames;
+    c.max_scan_bytes = max_scan_bytes;
+    c.max_blocks = max_blocks;
+    c.sub_bits = sub_bits;
+    c.max_subs = (max_scan_bytes * 8 + sub_bits - 1) / sub_bits + max_frames;
+    c.max_wgs = (c.max_subs + kGroupSubs - 1) / kGroupSubs + max_frames;
+    c.max_segs = max_blocks / 3 + max_frames;
+    const size_t per_frame = sizeof(EntFrame) + sizeof(HuffLut) * kMaxTables + sizeof(FrameRecord) + 192 * 4;
+    c.hdr_cap = align_up(per_frame * max_frames + 4 * static_cast<size_t>(c.max_segs + c.max_wgs) + 8 * kAlign, kAlign);
+    c.data = c.hdr_cap;
+    return c;
+}
+
+struct HdrOffsets {
+    size_t frames, tabs, seg, wg, recs, qt, used;
+};
+
+// Device-side view of a batch (kernel argument).
+struct EntBatchDev {
+    const EntFrame* frames;
+    const HuffLut* tabs;
+    const uint32_t* seg_end;
+    const uint32_t* wg_frame;
+    const uint8_t* data;
+    uint64_t* entries;
+    SubStats* stats;
+    uint64_t* xlast;
+    SubStats* agg;
+    uint32_t* status;
+    int16_t* coefs;
+    uint32_t nframes, nwg, sub_bits, pad;
+};
+
+__host__ __device__ __forceinline__ RunCtx make_ctx(const EntBatchDev& b, const EntFrame& F, const HuffLut* tabs)
+{
+    RunCtx c;
+    c.data = b.data + F.data_off;
+    c.seg_end = b.seg_end + F.seg_base;
+    c.tabs = tabs;
+    c.nseg = F.nseg;
+    c.data_bits = F.data_bits;
+    c.bpm = F.bpm;
+    c.jinfo_q = F.jinfo[0] | (static_cast<uint64_t>(F.jinfo[1]) << 16) | (static_cast<uint64_t>(F.jinfo[2]) << 32) |
+                (static_cast<uint64_t>(F.jinfo[3]) << 48);
+    c.jinfo_hi = F.jinfo[4] | (static_cast<uint32_t>(F.jinfo[5]) << 16);
+    return c;
+}
+
+__host__ __device__ __forceinline__ uint64_t guess_entry(const RunCtx& c, uint32_t start)
+{
+    return pack_state(start, 0, 0, find_segment(c.seg_end, c.nseg, start));
+}
+
+// ---------------------------------------------------------------------------
+// Kernels (gfx950)
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ void load_tables(HuffLut* lds, const HuffLut* g, int ntab, int tid, int nthreads)
+{
+    const u32x4* src = reinterpret_cast<const u32x4*>(g);
+    u32x4* dst = reinterpret_cast<u32x4*>(lds);
+    const int n = ntab * static_cast<int>(sizeof(HuffLut) / 16);
+    for (int i = tid; i < n; i += nthreads) dst[i] = src[i];
+}
+
+__device__ __forceinline__ SubStats shfl_down_stats(const SubStats& s, int d)
+{
+    SubStats r;
+    r.nblk = __shfl_down(s.nblk, d);
+    r.dc[0] = __shfl_down(s.dc[0], d);
+    r.dc[1] = __shfl_down(s.dc[1], d);
+    r.dc[2] = __shfl_down(s.dc[2], d);
+    r.flags = __shfl_down(s.flags, d);
+    r.pad[0] = r.pad[1] = r.pad[2] = 0;
+    return r;
+}
+
+// Ordered reduction of n statistics (one wave; result in lane 0).
+__device__ __forceinline__ SubStats wave_reduce_stats(const SubStats* v, int n, int lane)
+{
+    const int per = (n + 63) / 64;
+    SubStats acc = stats_identity();
+    for (int i = 0; i < per; ++i) {
+        const int k = lane * per + i;
+        if (k < n) acc = stats_combine(acc, v[k]);
+    }
+    for (int d = 1; d < 64; d <<= 1) {
+        const SubStats o = shfl_down_stats(acc, d);
+        if ((lane & (2 * d - 1)) == 0 && lane + d < 64) acc = stats_combine(acc, o);
+    }
+    return acc;
+}
+
+__global__ __launch_bounds__(kGroupSubs) void ent_sync_kernel(EntBatchDev b)
+{
+    __shared__ HuffLut tabs[kMaxTables];
+    __shared__ uint64_t xs[2][kGroupSubs];
+    const int tid = threadIdx.x;
+    const uint32_t w = blockIdx.x;
+    const uint32_t f = b.wg_frame[w];
+    const EntFrame F = b.frames[f];
+    load_tables(tabs, b.tabs + F.tab_base, F.ntab, tid, kGroupSubs);
+    __syncthreads();
+    const RunCtx c = make_ctx(b, F, tabs);
+    const uint32_t local = (w - F.wg_base) * kGroupSubs + tid;
+    const bool valid = local < F.nsub;
+    const uint32_t stop = (local + 1) * b.sub_bits;
+    uint64_t used = valid ? guess_entry(c, local * b.sub_bits) : 0;
+    SubStats st = stats_identity();
+    uint64_t x = valid ? run<false>(c, used, stop, st, nullptr) : used;
+    xs[0][tid] = x;
+    __syncthreads();
+    for (int r = 0;; ++r) {
+        int changed = 0;
+        if (valid && tid > 0) {
+            const uint64_t e = xs[r & 1][tid - 1];
+            if (!same_state(e, used)) {
+                SubStats s2 = stats_identity();
+                const uint64_t x2 = run<false>(c, e, stop, s2, nullptr);
+                changed = !same_state(x2, x);
+                used = e;
+                st = s2;
+                x = x2;
+            }
+        }
+        xs[(r + 1) & 1][tid] = x;
+        if (!__syncthreads_or(changed)) break;
+    }
+    if (valid) {
+        b.entries[F.sub_base + local] = used;
+        b.stats[F.sub_base + local] = st;
+        const uint32_t last = min(F.nsub - 1, (w - F.wg_base) * kGroupSubs + kGroupSubs - 1);
+        if (local == last) b.xlast[w] = x;
+    }
+}
+
+__global__ __launch_bounds__(64) void ent_link_kernel(EntBatchDev b)
+{
+    __shared__ HuffLut tabs[kMaxTables];
+    const int lane = threadIdx.x;
+    const uint32_t w = blockIdx.x;
+    const uint32_t f = b.wg_frame[w];
+    const EntFrame F = b.frames[f];
+    const uint32_t local0 = (w - F.wg_base) * kGroupSubs;
+    const int n = static_cast<int>(min(static_cast<uint32_t>(kGroupSubs), F.nsub - local0));
+    const uint32_t k0 = F.sub_base + local0;
+    if (w != F.wg_base) {
+        load_tables(tabs, b.tabs + F.tab_base, F.ntab, lane, 64);
+        __syncthreads();
+        if (lane == 0) {
+            const RunCtx c = make_ctx(b, F, tabs);
+            uint64_t cur = b.xlast[w - 1];
+            for (int i = 0; i < n; ++i) {
+                if (same_state(b.entries[k0 + i], cur)) break;   // the chains meet: the rest is verified
+                b.entries[k0 + i] = cur;
+                SubStats st = stats_identity();
+                cur = run<false>(c, cur, (local0 + i + 1) * b.sub_bits, st, nullptr);
+                b.stats[k0 + i] = st;
+                if (i == n - 1 && !same_state(cur, b.xlast[w])) atomicOr(&b.status[f], kStatusFallback);
+            }
+        }
+        __syncthreads();
+    }
+    const SubStats a = wave_reduce_stats(b.stats + k0, n, lane);
+    if (lane == 0) b.agg[w] = a;
+}
+
+__global__ __launch_bounds__(64) void ent_fallback_kernel(EntBatchDev b)
+{
+    __shared__ HuffLut tabs[kMaxTables];
+    const int lane = threadIdx.x;
+    const uint32_t f = blockIdx.x;
+    if (!(b.status[f] & kStatusFallback)) return;
+    const EntFrame F = b.frames[f];
+    load_tables(tabs, b.tabs + F.tab_base, F.ntab, lane, 64);
+    __syncthreads();
+    if (lane == 0) {
+        const RunCtx c = make_ctx(b, F, tabs);
+        uint64_t cur = pack_state(0, 0, 0, 0);
+        for (uint32_t i = 0; i < F.nsub; ++i) {
+            b.entries[F.sub_base + i] = cur;
+            SubStats st = stats_identity();
+            cur = run<false>(c, cur, (i + 1) * b.sub_bits, st, nullptr);
+            b.stats[F.sub_base + i] = st;
+        }
+    }
+    __syncthreads();
+    const uint32_t nwg = (F.nsub + kGroupSubs - 1) / kGroupSubs;
+    for (uint32_t g = 0; g < nwg; ++g) {
+        const int n = static_cast<int>(min(static_cast<uint32_t>(kGroupSubs), F.nsub - g * kGroupSubs));
+        const SubStats a = wave_reduce_stats(b.stats + F.sub_base + g * kGroupSubs, n, lane);
+        if (lane == 0) b.agg[F.wg_base + g] = a;
+    }
+}
+
+// Ordered inclusive scan of one value per thread over the workgroup (LDS).
+__device__ __forceinline__ SubStats block_scan_inclusive(SubStats v, SubStats* buf, int tid)
+{
+    buf[tid] = v;
+    __syncthreads();
+    for (int d = 1; d < kGroupSubs; d <<= 1) {
+        SubStats o = v;
+        if (tid >= d) o = stats_combine(buf[tid - d], v);
+        __syncthreads();
+        buf[tid] = o;
+        v = o;
+        __syncthreads();
+    }
+    return v;
+}
+
+__global__ __launch_bounds__(kGroupSubs) void ent_write_kernel(EntBatchDev b)
+{
+    __shared__ HuffLut tabs[kMaxTables];
+    __shared__ __attribute__((aligned(16))) int16_t stage[kGroupSubs * kStageStride];
+    SubStats* buf = reinterpret_cast<SubStats*>(stage);   // scan scratch, before any block is staged
+    static_assert(sizeof(SubStats) * kGroupSubs <= sizeof(int16_t) * kGroupSubs * kStageStride, "scratch");
+    const int tid = threadIdx.x;
+    const uint32_t w = blockIdx.x;
+    const uint32_t f = b.wg_frame[w];
+    const EntFrame F = b.frames[f];
+    load_tables(tabs, b.tabs + F.tab_base, F.ntab, tid, kGroupSubs);
+    // block index / DC predictors at this group's start: previous groups of the frame
+    const uint32_t npre = w - F.wg_base;
+    SubStats pre = stats_identity();
+    for (uint32_t base = 0; base < npre; base += kGroupSubs) {
+        const SubStats v = base + tid < npre ? b.agg[F.wg_base + base + tid] : stats_identity();
+        const SubStats inc = block_scan_inclusive(v, buf, tid);
+        SubStats total = inc;
+        __syncthreads();
+        if (tid == kGroupSubs - 1) buf[0] = inc;
+        __syncthreads();
+        total = buf[0];
+        __syncthreads();
+        pre = stats_combine(pre, total);
+    }
+    const uint32_t local = npre * kGroupSubs + tid;
+    const bool valid = local < F.nsub;
+    const uint32_t k = F.sub_base + local;
+    const SubStats mine = valid ? b.stats[k] : stats_identity();
+    const SubStats inc = block_scan_inclusive(mine, buf, tid);
+    SubStats excl = tid > 0 ? buf[tid - 1] : stats_identity();
+    __syncthreads();   // scratch reads done before blocks are staged
+    excl = stats_combine(pre, excl);
+    (void)inc;
+    if (!valid) return;
+    const RunCtx c = make_ctx(b, F, tabs);
+    RunOut o;
+    o.coefs = b.coefs + F.coef_off * 64;
+    o.stage = stage + tid * kStageStride;
+    o.blk = static_cast<uint32_t>(excl.nblk);
+    o.nblocks = F.nblocks;
+    o.pred[0] = excl.dc[0];
+    o.pred[1] = excl.dc[1];
+    o.pred[2] = excl.dc[2];
+    SubStats st = stats_identity();
+    run<true>(c, b.entries[k], (local + 1) * b.sub_bits, st, &o);
+    uint32_t bad = (st.flags & kError) ? kStatusCorrupt : 0;
+    if (local == F.nsub - 1 && static_cast<uint32_t>(excl.nblk + st.nblk) < F.nblocks) bad |= kStatusCount;
+    if (bad) atomicOr(&b.status[f], bad);
+}
+
+// ---------------------------------------------------------------------------
+// Host emulation of the four kernels (test hook; same state machine)
+// ---------------------------------------------------------------------------
+void emulate(const EntBatchDev& b)
+{
+    const uint32_t S = b.sub_bits;
+    // sync: per group, phase 1 then the LDS rounds
+    for (uint32_t w = 0; w < b.nwg; ++w) {
+        const EntFrame& F = b.frames[b.wg_frame[w]];
+        const RunCtx c = make_ctx(b, F, b.tabs + F.tab_base);
+        const uint32_t l0 = (w - F.wg_base) * kGroupSubs;
+        const int n = static_cast<int>(std::min<uint32_t>(kGroupSubs, F.nsub - l0));
+        std::vector<uint64_t> used(n), x(n), xs0(n), xs1(n);
+        std::vector<SubStats> st(n, stats_identity());
+        for (int t = 0; t < n; ++t) {
+            used[t] = guess_entry(c, (l0 + t) * S);
+            x[t] = run<false>(c, used[t], (l0 + t + 1) * S, st[t], nullptr);
+            xs0[t] = x[t];
+        }
+        std::vector<uint64_t>* cur = &xs0;
+        std::vector<uint64_t>* nxt = &xs1;
+        for (;;) {
+            bool changed = false;
+            for (int t = 0; t < n; ++t) {
+                if (t > 0 && !same_state((*cur)[t - 1], used[t])) {
+                    SubStats s2 = stats_identity();
+                    const uint64_t x2 = run<false>(c, (*cur)[t - 1], (l0 + t + 1) * S, s2, nullptr);
+                    changed |= !same_state(x2, x[t]);
+                    used[t] = (*cur)[t - 1];
+                    st[t] = s2;
+                    x[t] = x2;
+                }
+                (*nxt)[t] = x[t];
+            }
+            std::swap(cur, nxt);
+            if (!changed) break;
+        }
+        for (int t = 0; t < n; ++t) {
+            b.entries[F.sub_base + l0 + t] = used[t];
+            b.stats[F.sub_base + l0 + t] = st[t];
+        }
+        b.xlast[w] = x[n - 1];
+    }
+    // link
+    for (uint32_t w = 0; w < b.nwg; ++w) {
+        const uint32_t f = b.wg_frame[w];
+        const EntFrame& F = b.frames[f];
+        const RunCtx c = make_ctx(b, F, b.tabs + F.tab_base);
+        const uint32_t l0 = (w - F.wg_base) * kGroupSubs;
+        const int n = static_cast<int>(std::min<uint32_t>(kGroupSubs, F.nsub - l0));
+        const uint32_t k0 = F.sub_base + l0;
+        if (w != F.wg_base) {
+            uint64_t cur = b.xlast[w - 1];
+            for (int i = 0; i < n; ++i) {
+                if (same_state(b.entries[k0 + i], cur)) break;
+                b.entries[k0 + i] = cur;
+                SubStats s = stats_identity();
+                cur = run<false>(c, cur, (l0 + i + 1) * S, s, nullptr);
+                b.stats[k0 + i] = s;
+                if (i == n - 1 && !same_state(cur, b.xlast[w])) b.status[f] |= kStatusFallback;
+            }
+        }
+        SubStats a = stats_identity();
+        for (int i = 0; i < n; ++i) a = stats_combine(a, b.stats[k0 + i]);
+        b.agg[w] = a;
+    }
+    // fallback
+    for (uint32_t f = 0; f < b.nframes; ++f) {
+        if (!(b.status[f] & kStatusFallback)) continue;
+        const EntFrame& F = b.frames[f];
+        const RunCtx c = make_ctx(b, F, b.tabs + F.tab_base);
+        uint64_t cur = pack_state(0, 0, 0, 0);
+        for (uint32_t i = 0; i < F.nsub; ++i) {
+            b.entries[F.sub_base + i] = cur;
+            SubStats s = stats_identity();
+            cur = run<false>(c, cur, (i + 1) * S, s, nullptr);
+            b.stats[F.sub_base + i] = s;
+        }
+        const uint32_t nwg = (F.nsub + kGroupSubs - 1) / kGroupSubs;
+        for (uint32_t g = 0; g < nwg; ++g) {
+            SubStats a = stats_identity();
+            for (uint32_t i = g * kGroupSubs; i < std::min<uint32_t>(F.nsub, (g + 1) * kGroupSubs); ++i)
+                a = stats_combine(a, b.stats[F.sub_base + i]);
+            b.agg[F.wg_base + g] = a;
+        }
+    }
+    // write
+    std::vector<int16_t> stage(kStageStride);
+    for (uint32_t f = 0; f < b.nframes; ++f) {
+        const EntFrame& F = b.frames[f];
+        const RunCtx c = make_ctx(b, F, b.tabs + F.tab_base);
+        SubStats pre = stats_identity();
+        for (uint32_t i = 0; i < F.nsub; ++i) {
+            RunOut o;
+            o.coefs = b.coefs + F.coef_off * 64;
+            o.stage = stage.data();
+            o.blk = static_cast<uint32_t>(pre.nblk);
+            o.nblocks = F.nblocks;
+            o.pred[0] = pre.dc[0];
+            o.pred[1] = pre.dc[1];
+            o.pred[2] = pre.dc[2];
+            SubStats s = stats_identity();
+            run<true>(c, b.entries[F.sub_base + i], (i + 1) * S, s, &o);
+            if (s.flags & kError) b.status[f] |= kStatusCorrupt;
+            if (i == F.nsub - 1 && static_cast<uint32_t>(pre.nblk + s.nblk) < F.nblocks) b.status[f] |= kStatusCount;
+            pre = stats_combine(pre, b.stats[F.sub_base + i]);
+        }
+    }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// Batch object
+// ---------------------------------------------------------------------------
+struct hjd_gdec {
+    hjd_ctx* ctx = nullptr;
+    int device = 0, num_cu = 256;
+    bool gpu = true;
+    Caps caps{};
+    HdrOffsets H{};
+    uint8_t* h_stage = nullptr;         // pinned (gpu) or malloc (emulation): header + data
+    uint8_t* d_blob = nullptr;
+    uint64_t* d_entries = nullptr;
+    SubStats* d_stats = nullptr;
+    uint64_t* d_xlast = nullptr;
+    SubStats* d_agg = nullptr;
+    uint32_t* d_status = nullptr;
+    uint32_t* h_status = nullptr;       // pinned
+    int16_t* d_coefs = nullptr;
+    hipEvent_t staged = nullptr, done = nullptr;
+    bool pending = false;
+    std::vector<Prepared> frames;
+    size_t data_used = 0;
+    int nframes_issued = 0;
+    int first_error = HJD_OK;
+
+    // host-side work arrays for emulation
+    std::vector<uint64_t> e_entries, e_xlast;
+    std::vector<SubStats> e_stats, e_agg;
+    std::vector<uint32_t> e_status;
+
+    uint8_t* data_area() { return h_stage + caps.data; }
+    size_t data_cap() const { return static_cast<size_t>(caps.max_scan_bytes) + kDataPad * caps.max_frames +
+                                     16 * static_cast<size_t>(caps.max_frames); }
+
+    int wait_staging();
+    int stage_frames(const uint8_t* const* datas, const size_t* sizes, int n);
+    // Lays out and fills the header for the staged frames (pixel records too
+    // when d_outs is given); returns the device view (pointers into `blob`).
+    int assemble(uint8_t* blob, int16_t* coefs, int64_t* block_offsets, void* const* d_outs, const int32_t* pitches,
+                 EntBatchDev& d);
+    // pixel-kernel launch groups (0: 4:4:4, 1: 4:2:0)
+    int nrec[2] = {0, 0};
+    int64_t tasks[2] = {0, 0};
+    uint8_t* out_base[2] = {nullptr, nullptr};
+};
+
+int hjd_gdec::wait_staging()
+{
+    if (gpu && pending) {
+        HJD_HIP(hipSetDevice(device));
+        HJD_HIP(hipEventSynchronize(staged));
+    }
+    return HJD_OK;
+}
+
+int hjd_gdec::stage_frames(const uint8_t* const* datas, const size_t* sizes, int n)
+{
+    if (n <= 0 || n > caps.max_frames) return set_error(HJD_E_INVALID, "batch of %d frames (capacity %d)", n,
+                                                        caps.max_frames);
+    frames.assign(static_cast<size_t>(n), Prepared());
+    data_used = 0;
+    int64_t blocks = 0;
+    for (int i = 0; i < n; ++i) {
+        if (!datas[i]) return set_error(HJD_E_INVALID, "frame %d: NULL data", i);
+        Prepared& p = frames[i];
+        p.data_off = data_used;
+        const size_t cap = data_cap() - data_used;
+        if (cap <= kDataPad) return set_error(HJD_E_INVALID, "scan bytes exceed the batch capacity");
+        int rc = prepare(datas[i], sizes[i], data_area() + data_used, cap - kDataPad, p);
+        if (rc) return set_error(rc, "frame %d: %s", i, hjd_last_error());
+        data_used = align_up(data_used + p.data_bits / 8 + kDataPad, 16);
+        blocks += p.nblocks;
+    }
+    if (blocks > caps.max_blocks)
+        return set_error(HJD_E_INVALID, "batch needs %lld blocks (capacity %lld)", static_cast<long long>(blocks),
+                         static_cast<long long>(caps.max_blocks));
+    return HJD_OK;
+}
+
+int hjd_gdec::assemble(uint8_t* blob, int16_t* coefs, int64_t* block_offsets, void* const* d_outs,
+                       const int32_t* pitches, EntBatchDev& d)
+{
+    const int n = static_cast<int>(frames.size());
+    const uint32_t S = static_cast<uint32_t>(caps.sub_bits);
+    size_t ntab = 0, nseg = 0, nwg = 0;
+    for (const Prepared& p : frames) {
+        ntab += static_cast<size_t>(p.ntab);
+        nseg += p.seg_end.size();
+        const uint32_t ns = (p.data_bits + S - 1) / S;
+        nwg += (ns + kGroupSubs - 1) / kGroupSubs;
+    }
+    HdrOffsets& o = H;
+    o.frames = 0;
+    o.tabs = align_up(sizeof(EntFrame) * n, kAlign);
+    o.seg = align_up(o.tabs + sizeof(HuffLut) * ntab, kAlign);
+    o.wg = align_up(o.seg + 4 * nseg, kAlign);
+    o.recs = align_up(o.wg + 4 * nwg, kAlign);
+    o.qt = align_up(o.recs + (d_outs ? sizeof(FrameRecord) * n : 0), kAlign);
+    o.used = align_up(o.qt + (d_outs ? 192 * 4 * static_cast<size_t>(n) : 0), kAlign);
+    if (o.used > caps.hdr_cap) return set_error(HJD_E_INVALID, "batch header exceeds its capacity");
+
+    EntFrame* ef = reinterpret_cast<EntFrame*>(h_stage + o.frames);
+    HuffLut* tb = reinterpret_cast<HuffLut*>(h_stage + o.tabs);
+    uint32_t* seg = reinterpret_cast<uint32_t*>(h_stage + o.seg);
+    uint32_t* wgf = reinterpret_cast<uint32_t*>(h_stage + o.wg);
+    uint32_t sub_base = 0, wg_base = 0, seg_base = 0, tab_base = 0;
+    uint64_t coef_off = 0;
+    for (int i = 0; i < n; ++i) {
+        const Prepared& p = frames[i];
+        EntFrame F;
+        memset(&F, 0, sizeof(F));
+        F.data_off = p.data_off;
+        F.coef_off = coef_off;
+        F.data_bits = p.data_bits;
+        F.nsub = (p.data_bits + S - 1) / S;
+        F.sub_base = sub_base;
+        F.wg_base = wg_base;
+        F.seg_base = seg_base;
+        F.nseg = static_cast<uint32_t>(p.seg_end.size());
+        F.nblocks = static_cast<uint32_t>(p.nblocks);
+        F.tab_base = tab_base;
+        F.ntab = static_cast<uint8_t>(p.ntab);
+        F.bpm = static_cast<uint8_t>(p.bpm);
+        F.sampling = static_cast<uint8_t>(p.sampling);
+        memcpy(F.jinfo, p.jinfo, sizeof(F.jinfo));
+        ef[i] = F;
+        memcpy(tb + tab_base, p.tabs, sizeof(HuffLut) * p.ntab);
+        memcpy(seg + seg_base, p.seg_end.data(), 4 * p.seg_end.size());
+        const uint32_t nw = (F.nsub + kGroupSubs - 1) / kGroupSubs;
+        for (uint32_t g = 0; g < nw; ++g) wgf[wg_base + g] = static_cast<uint32_t>(i);
+        if (block_offsets) block_offsets[i] = static_cast<int64_t>(coef_off);
+        sub_base += F.nsub;
+        wg_base += nw;
+        seg_base += F.nseg;
+        tab_base += p.ntab;
+        coef_off += p.nblocks;
+    }
+    if (coef_off > static_cast<uint64_t>(caps.max_blocks) || sub_base > caps.max_subs || wg_base > caps.max_wgs)
+        return set_error(HJD_E_INVALID, "batch exceeds the decoder's capacity");
+
+    nrec[0] = nrec[1] = 0;
+    tasks[0] = tasks[1] = 0;
+    out_base[0] = out_base[1] = nullptr;
+    if (d_outs) {   // pixel-kernel records: 4:4:4 frames first, then 4:2:0 (one launch each)
+        FrameRecord* recs = reinterpret_cast<FrameRecord*>(h_stage + o.recs);
+        int32_t* qtn = reinterpret_cast<int32_t*>(h_stage + o.qt);
+        for (int i = 0; i < n; ++i) {
+            const Prepared& p = frames[i];
+            if (!d_outs[i] || !pitches || pitches[i] < 4 * p.width || (pitches[i] & 3) ||
+                (reinterpret_cast<uintptr_t>(d_outs[i]) & 15))
+                return set_error(HJD_E_INVALID, "frame %d: bad output buffer or pitch (16-byte aligned, >= 4*width)", i);
+            ++nrec[p.sampling == HJD_YUV420 ? 1 : 0];
+        }
+        int r[2] = {0, nrec[0]};
+        for (int i = 0; i < n; ++i) {
+            const Prepared& p = frames[i];
+            const int sidx = p.sampling == HJD_YUV420 ? 1 : 0;
+            if (!out_base[sidx]) out_base[sidx] = static_cast<uint8_t*>(d_outs[i]);
+            const int qti[3] = {3 * i, 3 * i + 1, 3 * i + 2};
+            FrameRecord rec;
+            const int64_t t = hjd_internal::make_frame_record(
+                p.width, p.height, p.sampling, static_cast<int64_t>(ef[i].coef_off),
+                static_cast<int64_t>(static_cast<uint8_t*>(d_outs[i]) - out_base[sidx]), pitches[i], qti, &rec);
+            if (t < 0) return static_cast<int>(t);
+            rec.task_begin = tasks[sidx];
+            tasks[sidx] += t;
+            recs[r[sidx]++] = rec;
+            for (int c = 0; c < 3; ++c)
+                for (int k = 0; k < 64; ++k) qtn[(3 * i + c) * 64 + kZigzag[k]] = p.qt[c][k];
+        }
+    }
+
+    d.frames = reinterpret_cast<const EntFrame*>(blob + o.frames);
+    d.tabs = reinterpret_cast<const HuffLut*>(blob + o.tabs);
+    d.seg_end = reinterpret_cast<const uint32_t*>(blob + o.seg);
+    d.wg_frame = reinterpret_cast<const uint32_t*>(blob + o.wg);
+    d.data = blob + caps.data;
+    d.coefs = coefs;
+    d.nframes = static_cast<uint32_t>(n);
+    d.nwg = wg_base;
+    d.sub_bits = S;
+    d.pad = 0;
+    return HJD_OK;
+}
+
+namespace {
+
+int gdec_alloc(hjd_gdec* g)
+{
+    const size_t total = g->caps.data + g->data_cap();
+    if (!g->gpu) {
+        g->h_stage = static_cast<uint8_t*>(calloc(1, total));
+        if (!g->h_stage) return set_error(HJD_E_NOMEM, "staging allocation");
+        return HJD_OK;
+    }
+    HJD_HIP(hipSetDevice(g->device));
+    HJD_HIP(hipHostMalloc(reinterpret_cast<void**>(&g->h_stage), total, hipHostMallocDefault));
+    HJD_HIP(hipHostMalloc(reinterpret_cast<void**>(&g->h_status), 4 * static_cast<size_t>(g->caps.max_frames),
+                          hipHostMallocDefault));
+    HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_blob), total));
+    HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_entries), 8 * static_cast<size_t>(g->caps.max_subs)));
+    HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_stats), sizeof(SubStats) * static_cast<size_t>(g->caps.max_subs)));
+    HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_xlast), 8 * static_cast<size_t>(g->caps.max_wgs)));
+    HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_agg), sizeof(SubStats) * static_cast<size_t>(g->caps.max_wgs)));
+    HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_status), 4 * static_cast<size_t>(g->caps.max_frames)));
+    HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_coefs), 128 * static_cast<size_t>(g->caps.max_blocks)));
+    HJD_HIP(hipEventCreateWithFlags(&g->staged, hipEventDisableTiming));
+    HJD_HIP(hipEventCreateWithFlags(&g->done, hipEventDisableTiming));
+    return HJD_OK;
+}
+
+// Entropy kernels on `stream`; coefficients land in b.coefs.
+int launch_entropy(hjd_gdec* g, const EntBatchDev& b, hipStream_t s)
+{
+    if (b.nwg == 0) return HJD_OK;
+    HJD_HIP(hipMemsetAsync(g->d_status, 0, 4 * static_cast<size_t>(b.nframes), s));
+    hipLaunchKernelGGL(ent_sync_kernel, dim3(b.nwg), dim3(kGroupSubs), 0, s, b);
+    HJD_HIP(hipGetLastError());
+    hipLaunchKernelGGL(ent_link_kernel, dim3(b.nwg), dim3(64), 0, s, b);
+    HJD_HIP(hipGetLastError());
+    hipLaunchKernelGGL(ent_fallback_kernel, dim3(b.nframes), dim3(64), 0, s, b);
+    HJD_HIP(hipGetLastError());
+    hipLaunchKernelGGL(ent_write_kernel, dim3(b.nwg), dim3(kGroupSubs), 0, s, b);
+    HJD_HIP(hipGetLastError());
+    return HJD_OK;
+}
+
+// Stage n JPEGs, upload, run the entropy kernels; optionally the pixel kernel.
+int gdec_run(hjd_gdec* g, const uint8_t* const* datas, const size_t* sizes, int n, void* const* d_outs,
+             const int32_t* pitches, int16_t* coefs_out, int64_t* block_offsets, hipStream_t s)
+{
+    if (!g || !g->gpu || !datas || !sizes) return set_error(HJD_E_INVALID, "NULL argument");
+    int rc = g->wait_staging();
+    if (rc) return rc;
+    rc = g->stage_frames(datas, sizes, n);
+    if (rc) return rc;
+    HJD_HIP(hipSetDevice(g->device));
+    int16_t* coefs = coefs_out ? coefs_out : g->d_coefs;
+    EntBatchDev b;
+    rc = g->assemble(g->d_blob, coefs, block_offsets, d_outs, pitches, b);
+    if (rc) return rc;
+    b.entries = g->d_entries;
+    b.stats = g->d_stats;
+    b.xlast = g->d_xlast;
+    b.agg = g->d_agg;
+    b.status = g->d_status;
+    HJD_HIP(hipMemcpyAsync(g->d_blob, g->h_stage, g->H.used, hipMemcpyHostToDevice, s));
+    HJD_HIP(hipMemcpyAsync(g->d_blob + g->caps.data, g->h_stage + g->caps.data, g->data_used, hipMemcpyHostToDevice, s));
+    HJD_HIP(hipEventRecord(g->staged, s));
+    g->pending = true;
+    rc = launch_entropy(g, b, s);
+    if (rc) return rc;
+    if (d_outs) {
+        int r0 = 0;
+        for (int sidx = 0; sidx < 2; ++sidx) {
+            if (!g->nrec[sidx]) continue;
+            rc = hjd_internal::launch_decode(
+                g->device, g->num_cu, sidx == 1 ? HJD_YUV420 : HJD_YUV444, HJD_IN_Q16_ZIGZAG, 0, coefs,
+                reinterpret_cast<const int32_t*>(g->d_blob + g->H.qt),
+                reinterpret_cast<const FrameRecord*>(g->d_blob + g->H.recs) + r0, g->nrec[sidx], g->tasks[sidx],
+                g->out_base[sidx], s, 0);
+            if (rc) return rc;
+            r0 += g->nrec[sidx];
+        }
+    }
+    HJD_HIP(hipMemcpyAsync(g->h_status, g->d_status, 4 * static_cast<size_t>(n), hipMemcpyDeviceToHost, s));
+    HJD_HIP(hipEventRecord(g->done, s));
+    g->nframes_issued = n;
+    return HJD_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hjd_gdec_create(hjd_ctx* ctx, int max_frames, int64_t max_scan_bytes, int64_t max_blocks, int sub_bits,
+                    hjd_gdec** out)
+{
+    if (!ctx || !out || max_frames <= 0 || max_scan_bytes <= 0 || max_blocks <= 0)
+        return set_error(HJD_E_INVALID, "invalid gdec arguments");
+    if (sub_bits == 0) sub_bits = kDefaultSubBits;
+    if (sub_bits < 32 || sub_bits > (1 << 20)) return set_error(HJD_E_INVALID, "sub_bits out of range [32, 2^20]");
+    *out = nullptr;
+    hjd_gdec* g = new (std::nothrow) hjd_gdec;
+    if (!g) return set_error(HJD_E_NOMEM, "gdec allocation");
+    g->ctx = ctx;
+    g->device = hjd_ctx_device(ctx);
+    g->num_cu = hjd_internal::ctx_num_cu(ctx);
+    g->caps = make_caps(max_frames, max_scan_bytes, max_blocks, sub_bits);
+    const int rc = gdec_alloc(g);
+    if (rc) {
+        hjd_gdec_destroy(g);
+        return rc;
+    }
+    *out = g;
+    return HJD_OK;
+}
+
+int hjd_gdec_destroy(hjd_gdec* g)
+{
+    if (!g) return HJD_OK;
+    if (!g->gpu) {
+        free(g->h_stage);
+        delete g;
+        return HJD_OK;
+    }
+    (void)hipSetDevice(g->device);
+    if (g->done) (void)hipEventSynchronize(g->done);
+    if (g->h_stage) (void)hipHostFree(g->h_stage);
+    if (g->h_status) (void)hipHostFree(g->h_status);
+    void* dev[] = {g->d_blob, g->d_entries, g->d_stats, g->d_xlast, g->d_agg, g->d_status, g->d_coefs};
+    for (void* p : dev)
+        if (p) (void)hipFree(p);
+    if (g->staged) (void)hipEventDestroy(g->staged);
+    if (g->done) (void)hipEventDestroy(g->done);
+    delete g;
+    return HJD_OK;
+}
+
+int hjd_gdec_decode(hjd_gdec* g, const uint8_t* const* datas, const size_t* sizes, int n, void* const* d_outs,
+                    const int32_t* pitches, void* stream)
+{
+    if (!d_outs) return set_error(HJD_E_INVALID, "d_outs is NULL");
+    return gdec_run(g, datas, sizes, n, d_outs, pitches, nullptr, nullptr, static_cast<hipStream_t>(stream));
+}
+
+int hjd_gdec_decode_coefs(hjd_gdec* g, const uint8_t* const* datas, const size_t* sizes, int n, int16_t* d_coefs,
+                          int64_t* block_offsets, void* stream)
+{
+    if (!d_coefs || (reinterpret_cast<uintptr_t>(d_coefs) & 15))
+        return set_error(HJD_E_INVALID, "d_coefs must be a 16-byte aligned device pointer");
+    return gdec_run(g, datas, sizes, n, nullptr, nullptr, d_coefs, block_offsets, static_cast<hipStream_t>(stream));
+}
+
+int hjd_gdec_sync(hjd_gdec* g, int32_t* status)
+{
+    if (!g || !g->gpu) return set_error(HJD_E_INVALID, "gdec is NULL");
+    if (!g->pending) return HJD_OK;
+    HJD_HIP(hipSetDevice(g->device));
+    HJD_HIP(hipEventSynchronize(g->done));
+    int bad = 0;
+    for (int i = 0; i < g->nframes_issued; ++i) {
+        const uint32_t s = g->h_status[i] & ~kStatusFallback;
+        if (status) status[i] = static_cast<int32_t>(g->h_status[i]);
+        if (s) ++bad;
+    }
+    g->pending = false;
+    if (bad) return set_error(HJD_E_INVALID, "%d of %d frames had corrupt entropy data", bad, g->nframes_issued);
+    return HJD_OK;
+}
+
+int hjd_debug_entropy_emulate(const uint8_t* data, size_t size, int sub_bits, int16_t* coefs,
+                              int64_t capacity_blocks, int32_t* status)
+{
+    if (!data || !coefs) return set_error(HJD_E_INVALID, "NULL argument");
+    if (sub_bits == 0) sub_bits = kDefaultSubBits;
+    if (sub_bits < 32 || sub_bits > (1 << 20)) return set_error(HJD_E_INVALID, "sub_bits out of range [32, 2^20]");
+    hjd_gdec g;
+    g.gpu = false;
+    g.caps = make_caps(1, static_cast<int64_t>(size), std::max<int64_t>(capacity_blocks, 1), sub_bits);
+    int rc = gdec_alloc(&g);
+    if (rc) return rc;
+    struct Free {
+        hjd_gdec* g;
+        ~Free() { free(g->h_stage); g->h_stage = nullptr; }
+    } guard{&g};
+    const uint8_t* datas[1] = {data};
+    const size_t sizes[1] = {size};
+    rc = g.stage_frames(datas, sizes, 1);
+    if (rc) return rc;
+    if (g.frames[0].nblocks > capacity_blocks)
+        return set_error(HJD_E_INVALID, "capacity %lld < %lld blocks", static_cast<long long>(capacity_blocks),
+                         static_cast<long long>(g.frames[0].nblocks));
+    EntBatchDev b;
+    rc = g.assemble(g.h_stage, coefs, nullptr, nullptr, nullptr, b);
+    if (rc) return rc;
+    const int64_t total = g.frames[0].nblocks;
+    g.e_entries.assign(static_cast<size_t>(g.caps.max_subs), 0);
+    g.e_stats.assign(static_cast<size_t>(g.caps.max_subs), stats_identity());
+    g.e_xlast.assign(static_cast<size_t>(g.caps.max_wgs), 0);
+    g.e_agg.assign(static_cast<size_t>(g.caps.max_wgs), stats_identity());
+    g.e_status.assign(1, 0);
+    b.entries = g.e_entries.data();
+    b.stats = g.e_stats.data();
+    b.xlast = g.e_xlast.data();
+    b.agg = g.e_agg.data();
+    b.status = g.e_status.data();
+    memset(coefs, 0, static_cast<size_t>(total) * 128);
+    emulate(b);
+    if (status) *status = static_cast<int32_t>(g.e_status[0]);
+    if (g.e_status[0] & ~kStatusFallback) return set_error(HJD_E_INVALID, "corrupt entropy data (status %u)", g.e_status[0]);
+    return HJD_OK;
+}
+
+}  // extern "C"

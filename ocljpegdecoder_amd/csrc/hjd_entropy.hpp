@@ -1,0 +1,388 @@
+// hjd_entropy.hpp -- GPU entropy (Huffman) decoding of baseline JPEG scans:
+// the state machine shared by the gfx950 kernels (hjd_entropy.hip) and the
+// host emulation used by the CPU tests.
+//
+// What it replaces: the reference decodes the whole scan on one host thread
+// (src/decoder.cpp:221-365: DC/AC symbol loop :221-260, restart handling
+// :288-307, MCU/block order :308-344; bit reader src/bitstream.h:310-365;
+// Huffman lookup src/huffman.h:277-314).  SURVEY.md s8(f) rank 3.
+//
+// Parallel formulation (self-synchronising decode, our design):
+//   * the host strips byte stuffing and RST markers while copying the scan
+//     into pinned memory; the device sees one contiguous bit string per frame
+//     plus the bit offset where each restart interval ("segment") ends;
+//   * the bit string is cut into fixed "subsequences" of S bits; the decoder
+//     state at a unit boundary (before a DC or AC Huffman symbol) is
+//     (pos, j = block of the MCU, z = next coefficient index);
+//   * the ENTRY of subsequence k is the first unit boundary at pos >= k*S; a
+//     RUN decodes from an entry until the first unit boundary >= (k+1)*S and
+//     returns that state (the EXIT), which is the next subsequence's entry;
+//   * runs started from a guessed entry (k*S, 0, 0) usually fall into step
+//     with the true decode within a few hundred bits (JPEG Huffman codes
+//     self-synchronise); the kernels then verify the chain entry(k+1) ==
+//     run(entry(k)) from the known frame start, re-running only where it
+//     breaks, so the result never depends on the guess being right;
+//   * segment ends are found without counting MCUs: at a unit boundary with
+//     fewer than 8 bits left in the segment and all of them 1 (the T.81
+//     F.1.2.3 pad), the segment is over -- no Huffman code is all ones, so
+//     valid data can never look like that earlier.
+#pragma once
+#include <stdint.h>
+
+#ifndef __HIPCC__
+#define __host__
+#define __device__
+#define __forceinline__ inline
+#endif
+
+namespace hjd {
+namespace ent {
+
+constexpr int kLutBits = 10;                    // first-level lookup width
+constexpr int kMaxTables = 6;                   // DC+AC per component at most
+constexpr int kGroupSubs = 256;                 // subsequences per workgroup (one per thread)
+constexpr int kDefaultSubBits = 1024;           // S
+constexpr int kStageStride = 72;                // int16 per lane in the block staging buffer (144 B)
+
+// One Huffman table in device form (2448 B, 16-B multiple).
+struct HuffLut {
+    uint16_t lut[1 << kLutBits];   // (len << 8) | symbol for codes <= kLutBits bits, 0: longer code
+    int32_t maxcode[17];           // largest code of each length, -1 if none (T.81 F.2.2.3)
+    int32_t delta[17];             // valptr[len] - mincode[len]
+    uint8_t vals[256];
+    uint8_t pad[8];
+};
+static_assert(sizeof(HuffLut) == 2448, "HuffLut layout");
+
+// Per-frame record of an entropy batch (device, 64 B).
+struct EntFrame {
+    uint64_t data_off;    // byte offset of the destuffed bit string in the batch data area (16-B aligned)
+    uint64_t coef_off;    // first output block in the coefficient buffer
+    uint32_t data_bits;   // destuffed length in bits (= end of the last segment)
+    uint32_t nsub;        // subsequences of this frame
+    uint32_t sub_base;    // first global subsequence index
+    uint32_t wg_base;     // first global workgroup index (kGroupSubs subsequences each)
+    uint32_t seg_base;    // first entry in the segment-end table
+    uint32_t nseg;        // restart intervals (1 without DRI)
+    uint32_t nblocks;     // blocks the scan must produce
+    uint32_t tab_base;    // first HuffLut of this frame
+    uint8_t ntab, bpm, sampling, pad0;
+    uint16_t jinfo[6];    // per bitstream block j of an MCU: dc slot | ac slot << 3 | comp << 6 | out slot << 8
+};
+static_assert(sizeof(EntFrame) == 64, "EntFrame layout");
+
+// Per-subsequence statistics of a run; combined with an ordered, segmented
+// operator to get each subsequence's block index and DC predictors.
+struct SubStats {
+    int32_t nblk;      // DC units decoded (= blocks started)
+    int32_t dc[3];     // sum of DC differences per component since the last reset in this run
+    uint32_t flags;    // kReset | kError
+    uint32_t pad[3];
+};
+static_assert(sizeof(SubStats) == 32, "SubStats layout");
+
+constexpr uint32_t kReset = 1;      // a restart (or the frame start) happened inside the run
+constexpr uint32_t kError = 2;      // invalid symbol / overrun (fatal only for the verified chain)
+
+// Frame status bits (device -> host).
+constexpr uint32_t kStatusFallback = 1;   // verification needed the sequential path
+constexpr uint32_t kStatusCorrupt = 2;    // invalid entropy data on the verified chain
+constexpr uint32_t kStatusCount = 4;      // block count != expected
+
+__host__ __device__ __forceinline__ SubStats stats_identity()
+{
+    SubStats s;
+    s.nblk = 0;
+    s.dc[0] = s.dc[1] = s.dc[2] = 0;
+    s.flags = 0;
+    s.pad[0] = s.pad[1] = s.pad[2] = 0;
+    return s;
+}
+
+// a then b
+__host__ __device__ __forceinline__ SubStats stats_combine(const SubStats& a, const SubStats& b)
+{
+    SubStats r;
+    r.nblk = a.nblk + b.nblk;
+    const bool rb = (b.flags & kReset) != 0;
+    for (int c = 0; c < 3; ++c) r.dc[c] = rb ? b.dc[c] : a.dc[c] + b.dc[c];
+    r.flags = a.flags | b.flags;
+    r.pad[0] = r.pad[1] = r.pad[2] = 0;
+    return r;
+}
+
+// ---- decoder state --------------------------------------------------------
+// bits 0-31 pos, 32-38 z, 39-41 j, 42-63 segment index (a hint, not compared)
+constexpr uint64_t kStateMask = (1ull << 42) - 1;
+
+__host__ __device__ __forceinline__ uint64_t pack_state(uint32_t pos, uint32_t j, uint32_t z, uint32_t seg)
+{
+    return static_cast<uint64_t>(pos) | (static_cast<uint64_t>(z) << 32) | (static_cast<uint64_t>(j) << 39) |
+           (static_cast<uint64_t>(seg) << 42);
+}
+__host__ __device__ __forceinline__ uint32_t st_pos(uint64_t s) { return static_cast<uint32_t>(s); }
+__host__ __device__ __forceinline__ uint32_t st_z(uint64_t s) { return static_cast<uint32_t>(s >> 32) & 127; }
+__host__ __device__ __forceinline__ uint32_t st_j(uint64_t s) { return static_cast<uint32_t>(s >> 39) & 7; }
+__host__ __device__ __forceinline__ uint32_t st_seg(uint64_t s) { return static_cast<uint32_t>(s >> 42); }
+__host__ __device__ __forceinline__ bool same_state(uint64_t a, uint64_t b) { return ((a ^ b) & kStateMask) == 0; }
+
+__host__ __device__ __forceinline__ uint32_t bswap32(uint32_t x)
+{
+#ifdef __HIP_DEVICE_COMPILE__
+    return __builtin_amdgcn_perm(0u, x, 0x00010203u);
+#else
+    return __builtin_bswap32(x);
+#endif
+}
+
+// First segment whose end is > pos (nseg if pos is at/after the data end).
+__host__ __device__ __forceinline__ uint32_t find_segment(const uint32_t* seg_end, uint32_t nseg, uint32_t pos)
+{
+    uint32_t lo = 0, hi = nseg;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (seg_end[mid] > pos) hi = mid;
+        else lo = mid + 1;
+    }
+    return lo;
+}
+
+// Bitstream block j of an MCU: scan components in SOS order, H*V blocks each
+// (src/decoder.cpp:308-344); `out slot` is its place in the MCU-major output
+// (Y blocks, then Cb, then Cr, as hjd_frame expects).
+__host__ __device__ __forceinline__ uint32_t jinfo_make(int dc_slot, int ac_slot, int comp, int out_slot)
+{
+    return static_cast<uint32_t>(dc_slot | (ac_slot << 3) | (comp << 6) | (out_slot << 8));
+}
+
+// Everything a run needs about its frame.  `tabs` points at the frame's
+// tables (LDS on the device), `data` at its destuffed bytes (4-B aligned).
+struct RunCtx {
+    const uint8_t* data;
+    const uint32_t* seg_end;   // bit offsets, nseg entries
+    const HuffLut* tabs;
+    uint32_t nseg, data_bits;
+    int bpm;
+    uint64_t jinfo_q;    // jinfo[0..3], 16 bits each
+    uint32_t jinfo_hi;   // jinfo[4..5]
+};
+
+// Blend (not select) between the two words so the context stays in registers.
+__host__ __device__ __forceinline__ uint32_t jinfo_of(const RunCtx& c, uint32_t j)
+{
+    const uint64_t m = 0ull - static_cast<uint64_t>(j < 4);
+    const uint64_t q = (c.jinfo_q & m) | (static_cast<uint64_t>(c.jinfo_hi) & ~m);
+    return static_cast<uint32_t>(q >> ((j & 3) * 16)) & 0xFFFF;
+}
+
+// Output side of a write-mode run.
+struct RunOut {
+    int16_t* coefs;        // frame's first block
+    int16_t* stage;        // this lane's 64-coefficient staging slot
+    uint32_t blk;          // index of the next block this run owns
+    uint32_t nblocks;
+    int32_t pred[3];
+};
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__host__ __device__ __forceinline__ void zero_block(int16_t* stage)
+{
+    u32x4* p = reinterpret_cast<u32x4*>(stage);
+    const u32x4 zv = {0u, 0u, 0u, 0u};
+    for (int q = 0; q < 8; ++q) p[q] = zv;
+}
+
+__host__ __device__ __forceinline__ void copy_block(int16_t* dst, const int16_t* stage)
+{
+    const u32x4* s = reinterpret_cast<const u32x4*>(stage);
+    u32x4* d = reinterpret_cast<u32x4*>(dst);
+    for (int q = 0; q < 8; ++q) d[q] = s[q];
+}
+
+__host__ __device__ __forceinline__ uint32_t load_word(const uint8_t* d, uint32_t wi)
+{
+    return bswap32(reinterpret_cast<const uint32_t*>(d)[wi]);
+}
+
+__host__ __device__ __forceinline__ uint32_t funnel(uint32_t w0, uint32_t w1, uint32_t off)
+{
+    return static_cast<uint32_t>(((static_cast<uint64_t>(w0) << 32) | w1) >> (32 - off));
+}
+
+// Decode one run: from `entry` until the first unit boundary >= stop (write
+// mode: and until the block this run owns is complete).  Accumulates `st`
+// (must start as the identity).  Returns the exit state.  Per-component sums
+// live in scalars (selects, not indexed arrays: no scratch on the device).
+template <bool kWrite>
+__host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry, uint32_t stop, SubStats& st,
+                                                 RunOut* out)
+{
+    uint32_t pos = st_pos(entry);
+    uint32_t z = st_z(entry);
+    uint32_t j = st_j(entry);
+    uint32_t seg = st_seg(entry);
+    int32_t nblk = st.nblk, d0 = st.dc[0], d1 = st.dc[1], d2 = st.dc[2];
+    uint32_t flags = st.flags;
+    int32_t p0 = 0, p1 = 0, p2 = 0;
+    uint32_t blk = 0;
+    if (kWrite) {
+        p0 = out->pred[0];
+        p1 = out->pred[1];
+        p2 = out->pred[2];
+        blk = out->blk;
+    }
+    uint64_t result;
+    if (seg >= c.nseg) {
+        result = pack_state(c.data_bits, 0, 0, c.nseg);
+    } else {
+        // An entry exactly at a segment start restarts the DC prediction itself:
+        // (e, seg s-1) and (e, seg s) compare equal, and only the former reaches
+        // the restart through the jump below.
+        if (pos == 0 || (seg > 0 && pos == c.seg_end[seg - 1])) {
+            flags |= kReset;
+            d0 = d1 = d2 = 0;
+            p0 = p1 = p2 = 0;
+        }
+        uint32_t seg_end = c.seg_end[seg];
+        uint32_t wi = pos >> 5;
+        uint32_t w0 = load_word(c.data, wi), w1 = load_word(c.data, wi + 1);
+        bool owned = false;                            // write mode: current block started in this run
+        uint32_t ji = jinfo_of(c, j);
+        result = 0;
+        bool done = false;
+        while (!done) {
+            if (pos >= stop && (!kWrite || !owned)) break;
+            const uint32_t nwi = pos >> 5;
+            if (nwi != wi) {
+                if (nwi == wi + 1) {
+                    w0 = w1;
+                    w1 = load_word(c.data, nwi + 1);
+                } else {
+                    w0 = load_word(c.data, nwi);
+                    w1 = load_word(c.data, nwi + 1);
+                }
+                wi = nwi;
+            }
+            const uint32_t peek = funnel(w0, w1, pos & 31);
+            // ---- restart-interval end: < 8 bits left, all ones (or overrun) ----
+            const int32_t left = static_cast<int32_t>(seg_end - pos);
+            if (left < 8) {
+                const bool ones = left <= 0 || (peek >> (32 - left)) == (1u << left) - 1;
+                if (ones) {
+                    if (left < 0 || (kWrite && owned)) flags |= kError;   // overrun / block cut by the pad
+                    pos = seg_end;
+                    ++seg;
+                    j = 0;
+                    z = 0;
+                    ji = jinfo_of(c, 0);
+                    owned = false;
+                    flags |= kReset;
+                    d0 = d1 = d2 = 0;
+                    p0 = p1 = p2 = 0;
+                    if (seg >= c.nseg) {
+                        result = pack_state(c.data_bits, 0, 0, c.nseg);
+                        done = true;
+                    } else {
+                        seg_end = c.seg_end[seg];
+                    }
+                    continue;
+                }
+            }
+            // ---- one Huffman symbol + its extra bits ----
+            const uint32_t comp = (ji >> 6) & 3;
+            const bool dc = z == 0;
+            const HuffLut& t = c.tabs[dc ? (ji & 7) : ((ji >> 3) & 7)];
+            const uint32_t e = t.lut[peek >> (32 - kLutBits)];
+            uint32_t len, sym;
+            if (e != 0) {
+                len = e >> 8;
+                sym = e & 0xFF;
+            } else {
+                len = 16;
+                sym = 0;
+                bool found = false;
+                for (uint32_t l = kLutBits + 1; l <= 16; ++l) {
+                    const int32_t code = static_cast<int32_t>(peek >> (32 - l));
+                    if (code <= t.maxcode[l]) {
+                        len = l;
+                        sym = t.vals[(code + t.delta[l]) & 255];
+                        found = true;
+                        break;
+                    }
+                }
+                if (!found) flags |= kError;   // consumes 16 bits as a zero symbol
+            }
+            const uint32_t s = sym & 15;
+            const uint32_t r = dc ? 0 : sym >> 4;
+            if (dc && sym > 11) flags |= kError;
+            int32_t v = 0;
+            if (s) {
+                const uint32_t bits = (peek << len) >> (32 - s);
+                v = bits < (1u << (s - 1)) ? static_cast<int32_t>(bits) - static_cast<int32_t>((1u << s) - 1)
+                                           : static_cast<int32_t>(bits);
+            }
+            pos += len + s;
+            if (dc) {
+                nblk += 1;
+                d0 += comp == 0 ? v : 0;
+                d1 += comp == 1 ? v : 0;
+                d2 += comp == 2 ? v : 0;
+                if (kWrite) {
+                    owned = true;
+                    p0 += comp == 0 ? v : 0;
+                    p1 += comp == 1 ? v : 0;
+                    p2 += comp == 2 ? v : 0;
+                    zero_block(out->stage);
+                    out->stage[0] = static_cast<int16_t>(comp == 0 ? p0 : (comp == 1 ? p1 : p2));
+                }
+                z = 1;
+            } else if (s == 0) {
+                z = r == 15 ? z + 16 : 64;       // ZRL / EOB
+            } else {
+                z += r;
+                if (z > 63) {
+                    flags |= kError;
+                    z = 64;
+                } else {
+                    if (kWrite && owned) out->stage[z] = static_cast<int16_t>(v);
+                    ++z;
+                }
+            }
+            if (z >= 64) {
+                if (kWrite && owned) {
+                    // MCU-major destination; on valid data blk % bpm == j.  Blocks past
+                    // the frame's count are ignored (as the host decoder stops there).
+                    const uint32_t dst = blk - j + (ji >> 8);
+                    if (blk < out->nblocks) {
+                        if (dst < out->nblocks && blk % static_cast<uint32_t>(c.bpm) == j)
+                            copy_block(out->coefs + static_cast<uint64_t>(dst) * 64, out->stage);
+                        else
+                            flags |= kError;   // a restart interval ended inside an MCU
+                    }
+                    blk += 1;
+                    owned = false;
+                }
+                z = 0;
+                j = j + 1 == static_cast<uint32_t>(c.bpm) ? 0 : j + 1;
+                ji = jinfo_of(c, j);
+            }
+        }
+        if (!done) result = pack_state(pos, j, z, seg);
+    }
+    st.nblk = nblk;
+    st.dc[0] = d0;
+    st.dc[1] = d1;
+    st.dc[2] = d2;
+    st.flags = flags;
+    if (kWrite) {
+        out->pred[0] = p0;
+        out->pred[1] = p1;
+        out->pred[2] = p2;
+        out->blk = blk;
+    }
+    return result;
+}
+
+}  // namespace ent
+}  // namespace hjd

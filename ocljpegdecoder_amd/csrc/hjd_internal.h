@@ -29,6 +29,20 @@ int launch_decode(int device, int num_cu, int sampling, int input_format, int va
                   const int32_t* d_qt_nat, const FrameRecord* d_frames, int nframes, int64_t tasks, void* d_out,
                   void* stream, int grid_blocks);
 
+// Parsed baseline-JPEG header as the GPU entropy path needs it (jpeg_host.cpp).
+struct ScanHeader {
+    int width, height, sampling, restart_interval, mcu_w, mcu_h, bpm;
+    int64_t nblocks;
+    size_t scan_offset;          // first byte of entropy-coded data
+    int32_t qt[3][64];           // per frame component, zigzag (file) order
+    int jcomp[6], jdc[6], jac[6], jslot[6];   // per bitstream block of an MCU
+    bool table_defined[2][4];    // [class: 0 DC, 1 AC][id]
+    uint8_t counts[2][4][16];
+    uint8_t symbols[2][4][256];
+    int nsym[2][4];
+};
+int parse_scan_header(const uint8_t* data, size_t size, ScanHeader* h);
+
 // hjd_ctx accessors for the other translation units
 int ctx_num_cu(const struct ::hjd_ctx* ctx);
 

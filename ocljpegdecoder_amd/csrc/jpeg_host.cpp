@@ -22,6 +22,8 @@ namespace {
 
 struct HuffTable {
     bool defined = false;
+    uint8_t counts[16];      // the DHT spec, kept for the GPU tables (hjd_entropy.hip)
+    int nsym = 0;
     uint16_t fast[512];      // (length << 8) | symbol for codes of <= 9 bits; 0 = slow path
     int32_t maxcode[18];     // largest code of each length (-1: none)
     int32_t valptr[17];
@@ -51,6 +53,8 @@ inline int be16(const uint8_t* p) { return (p[0] << 8) | p[1]; }
 int build_table(HuffTable& t, const uint8_t counts[16], const uint8_t* symbols, int nsym)
 {
     memset(t.fast, 0, sizeof(t.fast));
+    memcpy(t.counts, counts, 16);
+    t.nsym = nsym;
     int code = 0, k = 0;
     for (int len = 1; len <= 16; ++len) {
         const int n = counts[len - 1];
@@ -355,6 +359,50 @@ int decode_one(const uint8_t* data, size_t size, hjd_jpeg_info* info, int16_t* c
 }
 
 }  // namespace
+
+int hjd_internal::parse_scan_header(const uint8_t* data, size_t size, ScanHeader* h)
+{
+    if (!data || !h) return set_error(HJD_E_INVALID, "NULL argument");
+    Frame f;
+    int rc = parse(data, size, f);
+    if (rc) return rc;
+    hjd_jpeg_info info;
+    fill_info(f, &info);
+    h->width = f.width;
+    h->height = f.height;
+    h->sampling = f.sampling;
+    h->restart_interval = f.restart_interval;
+    h->mcu_w = info.mcu_w;
+    h->mcu_h = info.mcu_h;
+    h->nblocks = info.nblocks;
+    h->scan_offset = f.scan_offset;
+    memcpy(h->qt, info.qt, sizeof(h->qt));
+    // bitstream block order of one MCU (src/decoder.cpp:308-344): scan components
+    // in SOS order, H*V blocks each; output slot = Y blocks, then Cb, then Cr.
+    const int nblk_c[3] = {f.comp[0].h * f.comp[0].v, 1, 1};
+    const int blk_base[3] = {0, nblk_c[0], nblk_c[0] + 1};
+    int j = 0;
+    for (int si = 0; si < 3; ++si) {
+        const int c = f.scan_order[si];
+        for (int b = 0; b < nblk_c[c]; ++b, ++j) {
+            h->jcomp[j] = c;
+            h->jdc[j] = f.comp[c].td;
+            h->jac[j] = f.comp[c].ta;
+            h->jslot[j] = blk_base[c] + b;
+        }
+    }
+    h->bpm = j;
+    for (int cls = 0; cls < 2; ++cls)
+        for (int id = 0; id < 4; ++id) {
+            const HuffTable& t = cls ? f.ac[id] : f.dc[id];
+            h->table_defined[cls][id] = t.defined;
+            if (!t.defined) continue;
+            memcpy(h->counts[cls][id], t.counts, 16);
+            memcpy(h->symbols[cls][id], t.vals, static_cast<size_t>(t.nsym));
+            h->nsym[cls][id] = t.nsym;
+        }
+    return HJD_OK;
+}
 
 extern "C" {
 

@@ -5,6 +5,8 @@
     pixels = decode_jpeg(ctx, data)           # host Huffman + fused HIP kernel, BGRX on the device
     with JpegStream(ctx, max_blocks) as st:   # Huffman workers || H2D || kernel
         st.submit(data, out_tensor); st.sync()
+    gd = GpuDecoder(ctx, max_frames, max_scan_bytes, max_blocks)   # Huffman decode ON the GPU
+        gd.decode([data, ...], [out_tensor, ...]); gd.sync()
 """
 from __future__ import annotations
 
@@ -147,3 +149,97 @@ class JpegStream:
             self.close()
         except Exception:
             pass
+
+
+def _byte_arrays(datas: Sequence[bytes]):
+    bufs = [d if isinstance(d, ctypes.Array) else _buf(d) for d in datas]
+    arr_d = (_u8p * len(bufs))(*[ctypes.cast(b, _u8p) for b in bufs])
+    arr_s = (ctypes.c_size_t * len(bufs))(*[len(b) for b in bufs])
+    return bufs, arr_d, arr_s
+
+
+def _stream_handle(stream):
+    if stream is None:
+        return None
+    return stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
+
+
+class GpuDecoder:
+    """hjd_gdec: JPEG bytes -> Huffman decode on the GPU -> fused pixel kernel.
+
+    The host only parses headers and copies the scans (without byte stuffing)
+    into pinned memory; the entropy decode is a verified parallel decode on
+    the device, bit-identical to decode_coefs()."""
+
+    def __init__(self, ctx, max_frames: int, max_scan_bytes: int, max_blocks: int, sub_bits: int = 0):
+        self.lib = _lib.load()
+        self.ctx = ctx
+        h = ctypes.c_void_p()
+        check(self.lib.hjd_gdec_create(ctx.handle, int(max_frames), int(max_scan_bytes), int(max_blocks),
+                                       int(sub_bits), ctypes.byref(h)), "hjd_gdec_create")
+        self.handle = h
+        self._n = 0
+
+    def decode(self, datas: Sequence[bytes], outs, stream=None):
+        """outs: contiguous device tensors (H, W) int32 (or (H, pitch/4))."""
+        _keep, arr_d, arr_s = _byte_arrays(datas)
+        n = len(datas)
+        if len(outs) != n:
+            raise ValueError("one output per JPEG")
+        for o in outs:
+            if not (o.is_cuda and o.is_contiguous()):
+                raise ValueError("outputs must be contiguous device tensors")
+        ptrs = (ctypes.c_void_p * n)(*[o.data_ptr() for o in outs])
+        pitches = (ctypes.c_int32 * n)(*[o.shape[-1] * o.element_size() for o in outs])
+        check(self.lib.hjd_gdec_decode(self.handle, arr_d, arr_s, n, ptrs, pitches, _stream_handle(stream)),
+              "hjd_gdec_decode")
+        self._n = n
+
+    def decode_coefs(self, datas: Sequence[bytes], coefs, stream=None) -> List[int]:
+        """Entropy decode only into `coefs` (int16 device tensor, [blocks][64]);
+        returns each frame's first block."""
+        _keep, arr_d, arr_s = _byte_arrays(datas)
+        n = len(datas)
+        if not (coefs.is_cuda and coefs.is_contiguous() and coefs.element_size() == 2):
+            raise ValueError("coefs must be a contiguous int16 device tensor")
+        offs = (ctypes.c_int64 * n)()
+        check(self.lib.hjd_gdec_decode_coefs(self.handle, arr_d, arr_s, n, coefs.data_ptr(), offs,
+                                             _stream_handle(stream)), "hjd_gdec_decode_coefs")
+        self._n = n
+        return list(offs)
+
+    def sync(self, raise_on_error: bool = True) -> List[int]:
+        status = (ctypes.c_int32 * max(self._n, 1))()
+        rc = self.lib.hjd_gdec_sync(self.handle, status)
+        if raise_on_error:
+            check(rc, "hjd_gdec_sync")
+        return list(status)[: self._n]
+
+    def close(self):
+        if self.handle:
+            self.lib.hjd_gdec_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def emulate_entropy(data: bytes, sub_bits: int = 0):
+    """Test hook: the GPU entropy algorithm run on the host (no GPU) ->
+    (int16 [nblocks][64] coefficients, status bits)."""
+    lib = _lib.load()
+    info = parse(data)
+    coefs = np.zeros((info.nblocks, 64), np.int16)
+    status = ctypes.c_int32(0)
+    check(lib.hjd_debug_entropy_emulate(_buf(data), len(data), int(sub_bits), coefs.ctypes.data_as(_i16p),
+                                        info.nblocks, ctypes.byref(status)), "hjd_debug_entropy_emulate")
+    return coefs, status.value

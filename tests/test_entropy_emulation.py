@@ -1,0 +1,117 @@
+"""CPU: the GPU entropy-decode algorithm (self-synchronising parallel decode,
+DESIGN.md s10), run on the host through the test hook
+hjd_debug_entropy_emulate with the same state machine the kernels use
+(csrc/hjd_entropy.hpp), must reproduce the host Huffman decoder's
+coefficients exactly -- and those are pinned to the reference's own
+mcu_data (tests/test_jpeg_host.py).  Subsequence sizes from 32 bits up force
+every boundary case: entries inside codes, inside padding, exactly on restart
+boundaries, and chains that only meet in the sequential fallback."""
+import io
+import os
+
+import numpy as np
+import pytest
+
+import oracle_py as O
+
+
+def _pil(w, h, q, sub, seed, noise=20.0, **kw):
+    from PIL import Image
+    rng = np.random.default_rng(seed)
+    x = np.linspace(0, 255, w)[None, :, None]
+    y = np.linspace(0, 255, h)[:, None, None]
+    img = np.clip(x * [1, 0, 0.5] + y * [0, 1, 0.5] + rng.normal(0, noise, (h, w, 3)), 0, 255).astype(np.uint8)
+    b = io.BytesIO()
+    Image.fromarray(img).save(b, format="JPEG", quality=q, subsampling=sub, **kw)
+    return b.getvalue()
+
+
+@pytest.mark.parametrize("sub_bits", [32, 64, 100, 1024, 4096])
+def test_golden_files(hjd, sub_bits):
+    for name in O.golden_cases():
+        data = open(os.path.join(O.GOLDEN, name + ".jpg"), "rb").read()
+        ref, _ = hjd.decode_coefs(data)
+        got, status = hjd.emulate_entropy(data, sub_bits)
+        np.testing.assert_array_equal(got, ref, err_msg=f"{name} S={sub_bits}")
+        assert status & ~1 == 0
+
+
+def test_reference_sample_mcu_hash(hjd):
+    """The emulated decode of the reference's sample, dequantised, hashes to
+    the reference's mcu_data."""
+    import hashlib
+    data = open(os.path.join(O.GOLDEN, "JPEG_example_JPG_RIP_050.jpg"), "rb").read()
+    info = hjd.parse(data)
+    coefs, _ = hjd.emulate_entropy(data, 256)
+    nat = O.dequant_natural(coefs, info.qt, info.sampling)
+    assert hashlib.sha256(nat.astype("<i4").tobytes()).hexdigest() == (
+        "c25806f5238c8ec7c2a4846cf6b67c5b567fd268599591392baf77e91023924e")
+
+
+CASES = [
+    ("640x480 q90 4:2:0", dict(w=640, h=480, q=90, sub=2)),
+    ("640x480 q90 4:4:4", dict(w=640, h=480, q=90, sub=0)),
+    ("600x400 q100 4:4:4", dict(w=600, h=400, q=100, sub=0)),
+    ("640x480 q40 4:2:0", dict(w=640, h=480, q=40, sub=2)),
+    ("640x480 DRI 1 MCU", dict(w=640, h=480, q=90, sub=2, restart_marker_blocks=1)),
+    ("640x480 DRI 3 MCUs", dict(w=640, h=480, q=95, sub=0, restart_marker_blocks=3)),
+    ("640x480 DRI 1 row", dict(w=640, h=480, q=90, sub=0, restart_marker_rows=1)),
+    ("640x480 optimized", dict(w=640, h=480, q=75, sub=2, optimize=True)),
+    ("1x1", dict(w=1, h=1, q=90, sub=2)),
+    ("17x9 DRI 1", dict(w=17, h=9, q=90, sub=0, restart_marker_blocks=1)),
+]
+
+
+@pytest.mark.parametrize("name,kw", CASES, ids=[c[0] for c in CASES])
+@pytest.mark.parametrize("sub_bits", [32, 160, 1024, 2048])
+def test_synthetic(hjd, name, kw, sub_bits):
+    kw = dict(kw)
+    data = _pil(kw.pop("w"), kw.pop("h"), kw.pop("q"), kw.pop("sub"), seed=len(name) * 31 + sub_bits, **kw)
+    ref, _ = hjd.decode_coefs(data)
+    got, status = hjd.emulate_entropy(data, sub_bits)
+    np.testing.assert_array_equal(got, ref)
+    assert status & ~1 == 0
+
+
+def test_random_sweep(hjd):
+    """Seeded random files x subsequence sizes, including pure-noise content
+    (the worst case for self-synchronisation)."""
+    from PIL import Image
+    rng = np.random.default_rng(2024)
+    done = 0
+    while done < 150:
+        w, h = int(rng.integers(8, 200)), int(rng.integers(8, 160))
+        kw = {}
+        r = int(rng.integers(0, 3))
+        if r == 1:
+            kw["restart_marker_blocks"] = int(rng.integers(1, 9))
+        elif r == 2:
+            kw["restart_marker_rows"] = 1
+        img = (rng.integers(0, 256, (h, w, 3), dtype=np.uint8) if rng.integers(0, 3) == 0 else
+               np.clip(rng.normal(128, rng.uniform(0, 60), (h, w, 3)), 0, 255).astype(np.uint8))
+        b = io.BytesIO()
+        try:
+            Image.fromarray(img).save(b, format="JPEG", quality=int(rng.integers(20, 101)),
+                                      subsampling=int(rng.choice([0, 2])), **kw)
+        except OSError:
+            continue
+        data = b.getvalue()
+        sub_bits = int(rng.choice([32, 33, 64, 127, 256, 1000, 1024]))
+        ref, _ = hjd.decode_coefs(data)
+        got, status = hjd.emulate_entropy(data, sub_bits)
+        np.testing.assert_array_equal(got, ref, err_msg=f"{w}x{h} {kw} S={sub_bits}")
+        done += 1
+
+
+def test_corrupt_inputs_rejected(hjd):
+    data = _pil(64, 48, 90, 2, seed=3, restart_marker_blocks=2)
+    # wrong RST sequence number
+    i = data.index(b"\xff\xd1")
+    bad = data[:i] + b"\xff\xd3" + data[i + 2:]
+    with pytest.raises(hjd._lib.HjdError):
+        hjd.emulate_entropy(bad)
+    # scan cut short: fewer blocks than the frame needs
+    info = hjd.parse(data)
+    cut = data[: info.scan_offset + 40] + b"\xff\xd9"
+    with pytest.raises(hjd._lib.HjdError):
+        hjd.emulate_entropy(cut)

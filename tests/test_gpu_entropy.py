@@ -1,0 +1,155 @@
+"""GPU: Huffman decode on the device (hjd_gdec) through the C
+ABI.  Coefficients must equal the host decoder's exactly (that decoder is
+pinned to the reference's mcu_data in tests/test_jpeg_host.py); pixels must
+equal the reference's BGRX on the golden files and the oracle elsewhere."""
+import io
+import os
+
+import numpy as np
+import pytest
+
+import oracle_py as O
+from test_entropy_emulation import _pil
+
+pytestmark = pytest.mark.gpu
+
+
+def _golden_bytes():
+    return [(n, open(os.path.join(O.GOLDEN, n + ".jpg"), "rb").read()) for n in O.golden_cases()]
+
+
+def _coefs_gpu(hjd, ctx, datas, sub_bits=0):
+    import torch
+    infos = [hjd.parse(d) for d in datas]
+    total = sum(i.nblocks for i in infos)
+    coefs = torch.full((total, 64), 0x5A5A, dtype=torch.int16, device="cuda")
+    with hjd.GpuDecoder(ctx, len(datas), sum(len(d) for d in datas), total, sub_bits) as gd:
+        offs = gd.decode_coefs(datas, coefs)
+        status = gd.sync()
+    host = coefs.cpu().numpy()
+    return [host[o:o + i.nblocks] for o, i in zip(offs, infos)], status
+
+
+@pytest.mark.parametrize("sub_bits", [32, 256, 1024])
+def test_golden_coefficients(hjd, ctx, sub_bits):
+    cases = _golden_bytes()
+    got, status = _coefs_gpu(hjd, ctx, [d for _, d in cases], sub_bits)
+    for (name, d), g, s in zip(cases, got, status):
+        ref, _ = hjd.decode_coefs(d)
+        np.testing.assert_array_equal(g, ref, err_msg=f"{name} S={sub_bits}")
+        assert s & ~1 == 0
+
+
+def test_golden_pixels_match_reference(hjd, ctx):
+    import torch
+    cases = _golden_bytes()
+    datas = [d for _, d in cases]
+    exp = [O.load_case(n)["bgrx"] for n, _ in cases]
+    outs = [torch.full(e.shape, -1, dtype=torch.int32, device="cuda") for e in exp]
+    infos = [hjd.parse(d) for d in datas]
+    with hjd.GpuDecoder(ctx, len(datas), sum(map(len, datas)), sum(i.nblocks for i in infos)) as gd:
+        gd.decode(datas, outs)
+        gd.sync()
+    for (n, _), o, e in zip(cases, outs, exp):
+        np.testing.assert_array_equal(o.cpu().numpy().view(np.uint32), e, err_msg=n)
+
+
+SYN = [
+    dict(w=1920, h=1080, q=90, sub=2),
+    dict(w=1280, h=720, q=90, sub=0),
+    dict(w=1000, h=700, q=100, sub=0),
+    dict(w=800, h=600, q=40, sub=2),
+    dict(w=1024, h=768, q=90, sub=2, restart_marker_blocks=1),
+    dict(w=1024, h=768, q=95, sub=0, restart_marker_blocks=5),
+    dict(w=1024, h=768, q=90, sub=2, restart_marker_rows=1),
+    dict(w=1024, h=768, q=75, sub=2, optimize=True),
+    dict(w=1, h=1, q=90, sub=2),
+    dict(w=33, h=17, q=90, sub=0, restart_marker_blocks=1),
+]
+
+
+@pytest.mark.parametrize("sub_bits", [64, 1024])
+def test_mixed_batch_coefficients(hjd, ctx, sub_bits):
+    datas = []
+    for i, kw in enumerate(SYN):
+        kw = dict(kw)
+        datas.append(_pil(kw.pop("w"), kw.pop("h"), kw.pop("q"), kw.pop("sub"), seed=100 + i, **kw))
+    got, status = _coefs_gpu(hjd, ctx, datas, sub_bits)
+    for i, (d, g) in enumerate(zip(datas, got)):
+        ref, _ = hjd.decode_coefs(d)
+        np.testing.assert_array_equal(g, ref, err_msg=f"case {i} {SYN[i]} S={sub_bits}")
+    assert all(s & ~1 == 0 for s in status)
+
+
+def test_mixed_batch_pixels_match_oracle(hjd, ctx):
+    import torch
+    datas = []
+    for i, kw in enumerate(SYN):
+        kw = dict(kw)
+        datas.append(_pil(kw.pop("w"), kw.pop("h"), kw.pop("q"), kw.pop("sub"), seed=200 + i, **kw))
+    infos = [hjd.parse(d) for d in datas]
+    outs = [torch.full((i.height, i.width), -1, dtype=torch.int32, device="cuda") for i in infos]
+    with hjd.GpuDecoder(ctx, len(datas), sum(map(len, datas)), sum(i.nblocks for i in infos)) as gd:
+        gd.decode(datas, outs)
+        gd.sync()
+    for d, o, info in zip(datas, outs, infos):
+        coefs, _ = hjd.decode_coefs(d)
+        exp = O.decode_q16(coefs, info.qt, info.width, info.height, info.sampling)
+        np.testing.assert_array_equal(o.cpu().numpy().view(np.uint32), exp)
+
+
+def test_4k_frames(hjd, ctx):
+    """Full-size 4K frames (BASELINE configs[4] input), both samplings."""
+    datas = [_pil(3840, 2160, 90, 2, seed=7), _pil(3840, 2160, 90, 0, seed=8)]
+    got, status = _coefs_gpu(hjd, ctx, datas)
+    for d, g in zip(datas, got):
+        ref, _ = hjd.decode_coefs(d)
+        np.testing.assert_array_equal(g, ref)
+    assert all(s == 0 for s in status)
+
+
+def test_repeated_calls_reuse_staging(hjd, ctx):
+    """Back-to-back calls on one decoder (the second waits for the first's
+    uploads); results stay exact."""
+    import torch
+    datas = [_pil(640, 480, 90, 2, seed=s) for s in range(4)]
+    infos = [hjd.parse(d) for d in datas]
+    outs = [[torch.empty((i.height, i.width), dtype=torch.int32, device="cuda") for i in infos] for _ in range(3)]
+    with hjd.GpuDecoder(ctx, 4, sum(map(len, datas)), sum(i.nblocks for i in infos)) as gd:
+        for k in range(3):
+            gd.decode(datas, outs[k])
+        gd.sync()
+    for k in range(3):
+        for d, o, info in zip(datas, outs[k], infos):
+            coefs, _ = hjd.decode_coefs(d)
+            exp = O.decode_q16(coefs, info.qt, info.width, info.height, info.sampling)
+            np.testing.assert_array_equal(o.cpu().numpy().view(np.uint32), exp)
+
+
+def test_corrupt_scan_reported(hjd, ctx):
+    """A scan cut short decodes without faulting and is reported per frame."""
+    import torch
+    good = _pil(256, 128, 90, 2, seed=1)
+    info = hjd.parse(good)
+    cut = good[: info.scan_offset + 300] + b"\xff\xd9"
+    coefs = torch.zeros((2 * info.nblocks, 64), dtype=torch.int16, device="cuda")
+    with hjd.GpuDecoder(ctx, 2, 2 * len(good), 2 * info.nblocks) as gd:
+        gd.decode_coefs([good, cut], coefs)
+        status = gd.sync(raise_on_error=False)
+        assert status[0] & ~1 == 0 and status[1] & ~1 != 0
+        with pytest.raises(hjd._lib.HjdError):
+            gd.decode_coefs([good, cut], coefs)
+            gd.sync()
+
+
+def test_capacity_errors(hjd, ctx):
+    import torch
+    d = _pil(256, 128, 90, 2, seed=2)
+    info = hjd.parse(d)
+    coefs = torch.zeros((info.nblocks, 64), dtype=torch.int16, device="cuda")
+    with hjd.GpuDecoder(ctx, 1, len(d), info.nblocks) as gd:
+        with pytest.raises(hjd._lib.HjdError):
+            gd.decode_coefs([d, d], coefs)           # too many frames
+    with hjd.GpuDecoder(ctx, 2, len(d) // 2, 2 * info.nblocks) as gd:
+        with pytest.raises(hjd._lib.HjdError):
+            gd.decode_coefs([d], coefs)              # too many scan bytes
