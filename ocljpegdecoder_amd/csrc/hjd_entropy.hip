@@ -5,17 +5,19 @@
 // Huffman tables, copy the entropy-coded segment into pinned memory while
 // removing byte stuffing (FF00 -> FF) and RST markers, recording where each
 // restart interval ends.  Device side (one batch of frames per launch chain):
-//   ent_sync_kernel   each thread decodes its S-bit subsequence from a guessed
-//                     entry, then the workgroup iterates entry(k+1) = run(entry(k))
-//                     in LDS until nothing changes (256 subsequences per group);
-//   ent_link_kernel   one wave per group boundary re-runs the group's first
-//                     subsequences from the previous group's exit until the two
-//                     chains meet, then reduces the group's statistics;
-//   ent_fallback_kernel  frames whose chains did not meet inside a group are
-//                     redone sequentially (never seen on real data; correct anyway);
+//   ent_sync_kernel   a group stages its bit window in LDS; each thread decodes
+//                     its S-bit subsequence from a guessed entry, then the group
+//                     iterates entry(k+1) = run(entry(k)) until nothing changes.
+//                     Groups own 248 subsequences and also decode the 8 before
+//                     them ("warm-up"), shared with the previous group;
+//   ent_link_kernel   one thread per group: the chains of consecutive groups are
+//                     joined if some warm-up entry equals the predecessor's entry
+//                     for the same subsequence (a pure comparison, no decoding);
+//   ent_fallback_kernel  frames with an unjoined boundary are redone sequentially
+//                     (not seen on real data at the default S; correct anyway);
 //   ent_write_kernel  ordered segmented scan of the statistics (block index, DC
 //                     predictors) and a final run per subsequence that writes
-//                     whole int16 zigzag blocks (staged in LDS) in MCU-major order;
+//                     int16 zigzag blocks straight to HBM in MCU-major order;
 // then the fused pixel kernel (hjd_kernels.hpp) turns the blocks into BGRX.
 #include <hip/hip_runtime.h>
 
@@ -209,7 +211,7 @@ Caps make_caps(int max_frames, int64_t max_scan_bytes, int64_t max_blocks, int s
     c.max_blocks = max_blocks;
     c.sub_bits = sub_bits;
     c.max_subs = (max_scan_bytes * 8 + sub_bits - 1) / sub_bits + max_frames;
-    c.max_wgs = (c.max_subs + kGroupSubs - 1) / kGroupSubs + max_frames;
+    c.max_wgs = (c.max_subs + kOwn - 1) / kOwn + max_frames;
     c.max_segs = max_blocks / 3 + max_frames;
     const size_t per_frame = sizeof(EntFrame) + sizeof(HuffLut) * kMaxTables + sizeof(FrameRecord) + 192 * 4;
     c.hdr_cap = align_up(per_frame * max_frames + 4 * static_cast<size_t>(c.max_segs + c.max_wgs) + 8 * kAlign, kAlign);
@@ -230,7 +232,7 @@ struct EntBatchDev {
     const uint8_t* data;
     uint64_t* entries;
     SubStats* stats;
-    uint64_t* xlast;
+    uint64_t* wentries;   // [group][kWarm] warm-up entries
     SubStats* agg;
     uint32_t* status;
     int16_t* coefs;
@@ -249,6 +251,9 @@ __host__ __device__ __forceinline__ RunCtx make_ctx(const EntBatchDev& b, const 
     c.jinfo_q = F.jinfo[0] | (static_cast<uint64_t>(F.jinfo[1]) << 16) | (static_cast<uint64_t>(F.jinfo[2]) << 32) |
                 (static_cast<uint64_t>(F.jinfo[3]) << 48);
     c.jinfo_hi = F.jinfo[4] | (static_cast<uint32_t>(F.jinfo[5]) << 16);
+    c.win = nullptr;
+    c.win_start = 0;
+    c.win_words = 0;
     return c;
 }
 
@@ -256,6 +261,17 @@ __host__ __device__ __forceinline__ uint64_t guess_entry(const RunCtx& c, uint32
 {
     return pack_state(start, 0, 0, find_segment(c.seg_end, c.nseg, start));
 }
+
+__host__ __device__ __forceinline__ uint32_t frame_groups(uint32_t nsub) { return (nsub + kOwn - 1) / kOwn; }
+
+// Subsequence handled by thread t of frame group gl (may be < 0 or >= nsub).
+__host__ __device__ __forceinline__ int64_t group_sub(uint32_t gl, int t)
+{
+    return static_cast<int64_t>(gl) * kOwn - kWarm + t;
+}
+
+// Readable words of a frame's bit string (the host pads 16 bytes).
+__host__ __device__ __forceinline__ uint32_t readable_words(const EntFrame& F) { return (F.data_bits / 8 + 16) / 4; }
 
 // ---------------------------------------------------------------------------
 // Kernels (gfx950)
@@ -269,6 +285,44 @@ __device__ __forceinline__ void load_tables(HuffLut* lds, const HuffLut* g, int 
     for (int i = tid; i < n; i += nthreads) dst[i] = src[i];
 }
 
+// Stage words [start, start + n) of the frame's bit string into the padded LDS
+// window (byte-swapped once here instead of per read).  start % 4 == 0.
+__host__ __device__ __forceinline__ void stage_window(uint32_t* win, const EntFrame& F, const uint8_t* data,
+                                                      uint32_t start, uint32_t n, int tid, int nthreads)
+{
+    const uint32_t readable = readable_words(F);
+    const uint32_t* g = reinterpret_cast<const uint32_t*>(data);
+    for (uint32_t i = static_cast<uint32_t>(tid) * 4; i < n; i += static_cast<uint32_t>(nthreads) * 4) {
+        const uint32_t wi = start + i;
+        uint32_t v[4];
+        if (wi + 4 <= readable) {
+            const u32x4 q = *reinterpret_cast<const u32x4*>(g + wi);
+            v[0] = q.x;
+            v[1] = q.y;
+            v[2] = q.z;
+            v[3] = q.w;
+        } else {
+            for (int e = 0; e < 4; ++e) v[e] = wi + e < readable ? g[wi + e] : 0xFFFFFFFFu;
+        }
+        uint32_t* row = win + i + (i >> 5);
+        for (int e = 0; e < 4; ++e) row[e] = bswap32(v[e]);
+    }
+}
+
+// Window of group gl: from its first subsequence to its last + margin.
+__host__ __device__ __forceinline__ void group_window(const EntFrame& F, uint32_t gl, uint32_t S, uint32_t& start,
+                                                      uint32_t& n)
+{
+    const int64_t k0 = group_sub(gl, 0);
+    const uint32_t first = k0 < 0 ? 0u : static_cast<uint32_t>(k0);
+    const int64_t lastk = k0 + kGroupSubs < static_cast<int64_t>(F.nsub) ? k0 + kGroupSubs : F.nsub;   // exclusive
+    const uint32_t last = static_cast<uint32_t>(lastk);
+    start = (static_cast<uint32_t>((static_cast<uint64_t>(first) * S) >> 5)) & ~3u;
+    const uint32_t end = static_cast<uint32_t>((static_cast<uint64_t>(last) * S + 95) >> 5);
+    const uint32_t want = ((end - start) + 3) & ~3u;
+    n = want < static_cast<uint32_t>(kWinRaw) ? want : static_cast<uint32_t>(kWinRaw);
+}
+
 __device__ __forceinline__ SubStats shfl_down_stats(const SubStats& s, int d)
 {
     SubStats r;
@@ -279,124 +333,6 @@ __device__ __forceinline__ SubStats shfl_down_stats(const SubStats& s, int d)
     r.flags = __shfl_down(s.flags, d);
     r.pad[0] = r.pad[1] = r.pad[2] = 0;
     return r;
-}
-
-// Ordered reduction of n statistics (one wave; result in lane 0).
-__device__ __forceinline__ SubStats wave_reduce_stats(const SubStats* v, int n, int lane)
-{
-    const int per = (n + 63) / 64;
-    SubStats acc = stats_identity();
-    for (int i = 0; i < per; ++i) {
-        const int k = lane * per + i;
-        if (k < n) acc = stats_combine(acc, v[k]);
-    }
-    for (int d = 1; d < 64; d <<= 1) {
-        const SubStats o = shfl_down_stats(acc, d);
-        if ((lane & (2 * d - 1)) == 0 && lane + d < 64) acc = stats_combine(acc, o);
-    }
-    return acc;
-}
-
-__global__ __launch_bounds__(kGroupSubs) void ent_sync_kernel(EntBatchDev b)
-{
-    __shared__ HuffLut tabs[kMaxTables];
-    __shared__ uint64_t xs[2][kGroupSubs];
-    const int tid = threadIdx.x;
-    const uint32_t w = blockIdx.x;
-    const uint32_t f = b.wg_frame[w];
-    const EntFrame F = b.frames[f];
-    load_tables(tabs, b.tabs + F.tab_base, F.ntab, tid, kGroupSubs);
-    __syncthreads();
-    const RunCtx c = make_ctx(b, F, tabs);
-    const uint32_t local = (w - F.wg_base) * kGroupSubs + tid;
-    const bool valid = local < F.nsub;
-    const uint32_t stop = (local + 1) * b.sub_bits;
-    uint64_t used = valid ? guess_entry(c, local * b.sub_bits) : 0;
-    SubStats st = stats_identity();
-    uint64_t x = valid ? run<false>(c, used, stop, st, nullptr) : used;
-    xs[0][tid] = x;
-    __syncthreads();
-    for (int r = 0;; ++r) {
-        int changed = 0;
-        if (valid && tid > 0) {
-            const uint64_t e = xs[r & 1][tid - 1];
-            if (!same_state(e, used)) {
-                SubStats s2 = stats_identity();
-                const uint64_t x2 = run<false>(c, e, stop, s2, nullptr);
-                changed = !same_state(x2, x);
-                used = e;
-                st = s2;
-                x = x2;
-            }
-        }
-        xs[(r + 1) & 1][tid] = x;
-        if (!__syncthreads_or(changed)) break;
-    }
-    if (valid) {
-        b.entries[F.sub_base + local] = used;
-        b.stats[F.sub_base + local] = st;
-        const uint32_t last = min(F.nsub - 1, (w - F.wg_base) * kGroupSubs + kGroupSubs - 1);
-        if (local == last) b.xlast[w] = x;
-    }
-}
-
-__global__ __launch_bounds__(64) void ent_link_kernel(EntBatchDev b)
-{
-    __shared__ HuffLut tabs[kMaxTables];
-    const int lane = threadIdx.x;
-    const uint32_t w = blockIdx.x;
-    const uint32_t f = b.wg_frame[w];
-    const EntFrame F = b.frames[f];
-    const uint32_t local0 = (w - F.wg_base) * kGroupSubs;
-    const int n = static_cast<int>(min(static_cast<uint32_t>(kGroupSubs), F.nsub - local0));
-    const uint32_t k0 = F.sub_base + local0;
-    if (w != F.wg_base) {
-        load_tables(tabs, b.tabs + F.tab_base, F.ntab, lane, 64);
-        __syncthreads();
-        if (lane == 0) {
-            const RunCtx c = make_ctx(b, F, tabs);
-            uint64_t cur = b.xlast[w - 1];
-            for (int i = 0; i < n; ++i) {
-                if (same_state(b.entries[k0 + i], cur)) break;   // the chains meet: the rest is verified
-                b.entries[k0 + i] = cur;
-                SubStats st = stats_identity();
-                cur = run<false>(c, cur, (local0 + i + 1) * b.sub_bits, st, nullptr);
-                b.stats[k0 + i] = st;
-                if (i == n - 1 && !same_state(cur, b.xlast[w])) atomicOr(&b.status[f], kStatusFallback);
-            }
-        }
-        __syncthreads();
-    }
-    const SubStats a = wave_reduce_stats(b.stats + k0, n, lane);
-    if (lane == 0) b.agg[w] = a;
-}
-
-__global__ __launch_bounds__(64) void ent_fallback_kernel(EntBatchDev b)
-{
-    __shared__ HuffLut tabs[kMaxTables];
-    const int lane = threadIdx.x;
-    const uint32_t f = blockIdx.x;
-    if (!(b.status[f] & kStatusFallback)) return;
-    const EntFrame F = b.frames[f];
-    load_tables(tabs, b.tabs + F.tab_base, F.ntab, lane, 64);
-    __syncthreads();
-    if (lane == 0) {
-        const RunCtx c = make_ctx(b, F, tabs);
-        uint64_t cur = pack_state(0, 0, 0, 0);
-        for (uint32_t i = 0; i < F.nsub; ++i) {
-            b.entries[F.sub_base + i] = cur;
-            SubStats st = stats_identity();
-            cur = run<false>(c, cur, (i + 1) * b.sub_bits, st, nullptr);
-            b.stats[F.sub_base + i] = st;
-        }
-    }
-    __syncthreads();
-    const uint32_t nwg = (F.nsub + kGroupSubs - 1) / kGroupSubs;
-    for (uint32_t g = 0; g < nwg; ++g) {
-        const int n = static_cast<int>(min(static_cast<uint32_t>(kGroupSubs), F.nsub - g * kGroupSubs));
-        const SubStats a = wave_reduce_stats(b.stats + F.sub_base + g * kGroupSubs, n, lane);
-        if (lane == 0) b.agg[F.wg_base + g] = a;
-    }
 }
 
 // Ordered inclusive scan of one value per thread over the workgroup (LDS).
@@ -415,84 +351,190 @@ __device__ __forceinline__ SubStats block_scan_inclusive(SubStats v, SubStats* b
     return v;
 }
 
-__global__ __launch_bounds__(kGroupSubs) void ent_write_kernel(EntBatchDev b)
+__global__ __launch_bounds__(kGroupSubs) void ent_sync_kernel(EntBatchDev b)
 {
     __shared__ HuffLut tabs[kMaxTables];
-    __shared__ __attribute__((aligned(16))) int16_t stage[kGroupSubs * kStageStride];
-    SubStats* buf = reinterpret_cast<SubStats*>(stage);   // scan scratch, before any block is staged
-    static_assert(sizeof(SubStats) * kGroupSubs <= sizeof(int16_t) * kGroupSubs * kStageStride, "scratch");
+    __shared__ uint32_t win[kWinLds];
+    __shared__ uint64_t xs[2][kGroupSubs];
     const int tid = threadIdx.x;
     const uint32_t w = blockIdx.x;
     const uint32_t f = b.wg_frame[w];
     const EntFrame F = b.frames[f];
+    const uint32_t gl = w - F.wg_base;
+    const uint32_t S = b.sub_bits;
+    RunCtx c = make_ctx(b, F, tabs);
+    group_window(F, gl, S, c.win_start, c.win_words);
     load_tables(tabs, b.tabs + F.tab_base, F.ntab, tid, kGroupSubs);
-    // block index / DC predictors at this group's start: previous groups of the frame
-    const uint32_t npre = w - F.wg_base;
+    stage_window(win, F, c.data, c.win_start, c.win_words, tid, kGroupSubs);
+    c.win = win;
+    __syncthreads();
+    const int64_t k = group_sub(gl, tid);
+    const bool valid = k >= 0 && k < static_cast<int64_t>(F.nsub);
+    const bool has_pred = valid && tid > 0 && k > 0;
+    const uint32_t ku = static_cast<uint32_t>(k);
+    const uint32_t stop = (ku + 1) * S;
+    uint64_t used = valid ? guess_entry(c, ku * S) : 0;
+    SubStats st = stats_identity();
+    uint64_t x = valid ? run<false>(c, used, stop, st, nullptr) : used;
+    xs[0][tid] = x;
+    __syncthreads();
+    for (int r = 0;; ++r) {
+        int changed = 0;
+        if (has_pred) {
+            const uint64_t e = xs[r & 1][tid - 1];
+            if (!same_state(e, used)) {
+                SubStats s2 = stats_identity();
+                const uint64_t x2 = run<false>(c, e, stop, s2, nullptr);
+                changed = !same_state(x2, x);
+                used = e;
+                st = s2;
+                x = x2;
+            }
+        }
+        xs[(r + 1) & 1][tid] = x;
+        if (!__syncthreads_or(changed)) break;
+    }
+    const bool own = valid && tid >= kWarm;
+    if (own) {
+        b.entries[F.sub_base + ku] = used;
+        b.stats[F.sub_base + ku] = st;
+    } else if (tid < kWarm) {
+        b.wentries[static_cast<uint64_t>(w) * kWarm + tid] = used;   // 0 for invalid (frame start group)
+    }
+    // statistics of the owned range (scratch reuses the window)
+    SubStats* buf = reinterpret_cast<SubStats*>(win);
+    static_assert(sizeof(SubStats) * kGroupSubs <= sizeof(uint32_t) * kWinLds, "scan scratch");
+    const SubStats total = block_scan_inclusive(own ? st : stats_identity(), buf, tid);
+    if (tid == kGroupSubs - 1) b.agg[w] = total;
+}
+
+__global__ __launch_bounds__(256) void ent_link_kernel(EntBatchDev b)
+{
+    const uint32_t w = blockIdx.x * 256 + threadIdx.x;
+    if (w >= b.nwg) return;
+    const uint32_t f = b.wg_frame[w];
+    const EntFrame F = b.frames[f];
+    const uint32_t gl = w - F.wg_base;
+    if (gl == 0) return;
+    bool joined = false;
+    for (int t = 0; t < kWarm && !joined; ++t) {
+        const uint64_t k = static_cast<uint64_t>(group_sub(gl, t));
+        joined = same_state(b.wentries[static_cast<uint64_t>(w) * kWarm + t], b.entries[F.sub_base + k]);
+    }
+    if (!joined) atomicOr(&b.status[f], kStatusFallback);
+}
+
+__global__ __launch_bounds__(64) void ent_fallback_kernel(EntBatchDev b)
+{
+    __shared__ HuffLut tabs[kMaxTables];
+    __shared__ SubStats red[64];
+    const int lane = threadIdx.x;
+    const uint32_t f = blockIdx.x;
+    if (!(b.status[f] & kStatusFallback)) return;
+    const EntFrame F = b.frames[f];
+    load_tables(tabs, b.tabs + F.tab_base, F.ntab, lane, 64);
+    __syncthreads();
+    if (lane == 0) {
+        const RunCtx c = make_ctx(b, F, tabs);
+        uint64_t cur = pack_state(0, 0, 0, 0);
+        for (uint32_t i = 0; i < F.nsub; ++i) {
+            b.entries[F.sub_base + i] = cur;
+            SubStats st = stats_identity();
+            cur = run<false>(c, cur, (i + 1) * b.sub_bits, st, nullptr);
+            b.stats[F.sub_base + i] = st;
+        }
+        for (uint32_t g = 0; g < frame_groups(F.nsub); ++g) {
+            SubStats a = stats_identity();
+            for (uint32_t i = g * kOwn; i < min(F.nsub, (g + 1) * kOwn); ++i) a = stats_combine(a, b.stats[F.sub_base + i]);
+            b.agg[F.wg_base + g] = a;
+        }
+    }
+    (void)red;
+}
+
+__global__ __launch_bounds__(kGroupSubs) void ent_write_kernel(EntBatchDev b)
+{
+    __shared__ HuffLut tabs[kMaxTables];
+    __shared__ uint32_t win[kWinLds];
+    SubStats* buf = reinterpret_cast<SubStats*>(win);   // scan scratch, before the window is staged
+    const int tid = threadIdx.x;
+    const uint32_t w = blockIdx.x;
+    const uint32_t f = b.wg_frame[w];
+    const EntFrame F = b.frames[f];
+    const uint32_t gl = w - F.wg_base;
+    const uint32_t S = b.sub_bits;
+    load_tables(tabs, b.tabs + F.tab_base, F.ntab, tid, kGroupSubs);
+    // block index / DC predictors at this group's start: all previous groups of the frame
     SubStats pre = stats_identity();
-    for (uint32_t base = 0; base < npre; base += kGroupSubs) {
-        const SubStats v = base + tid < npre ? b.agg[F.wg_base + base + tid] : stats_identity();
-        const SubStats inc = block_scan_inclusive(v, buf, tid);
-        SubStats total = inc;
-        __syncthreads();
-        if (tid == kGroupSubs - 1) buf[0] = inc;
-        __syncthreads();
-        total = buf[0];
+    for (uint32_t base = 0; base < gl; base += kGroupSubs) {
+        const SubStats v = base + tid < gl ? b.agg[F.wg_base + base + tid] : stats_identity();
+        block_scan_inclusive(v, buf, tid);
+        const SubStats total = buf[kGroupSubs - 1];
         __syncthreads();
         pre = stats_combine(pre, total);
     }
-    const uint32_t local = npre * kGroupSubs + tid;
-    const bool valid = local < F.nsub;
-    const uint32_t k = F.sub_base + local;
-    const SubStats mine = valid ? b.stats[k] : stats_identity();
-    const SubStats inc = block_scan_inclusive(mine, buf, tid);
-    SubStats excl = tid > 0 ? buf[tid - 1] : stats_identity();
-    __syncthreads();   // scratch reads done before blocks are staged
-    excl = stats_combine(pre, excl);
-    (void)inc;
-    if (!valid) return;
-    const RunCtx c = make_ctx(b, F, tabs);
+    const int64_t k = group_sub(gl, tid);
+    const bool own = tid >= kWarm && k < static_cast<int64_t>(F.nsub);
+    const uint32_t ku = static_cast<uint32_t>(k);
+    const SubStats mine = own ? b.stats[F.sub_base + ku] : stats_identity();
+    block_scan_inclusive(mine, buf, tid);
+    const SubStats excl = stats_combine(pre, tid > 0 ? buf[tid - 1] : stats_identity());
+    RunCtx c = make_ctx(b, F, tabs);
+    group_window(F, gl, S, c.win_start, c.win_words);
+    __syncthreads();   // scratch reads done before the window overwrites it
+    stage_window(win, F, c.data, c.win_start, c.win_words, tid, kGroupSubs);
+    c.win = win;
+    __syncthreads();
+    if (!own) return;
     RunOut o;
     o.coefs = b.coefs + F.coef_off * 64;
-    o.stage = stage + tid * kStageStride;
     o.blk = static_cast<uint32_t>(excl.nblk);
     o.nblocks = F.nblocks;
     o.pred[0] = excl.dc[0];
     o.pred[1] = excl.dc[1];
     o.pred[2] = excl.dc[2];
     SubStats st = stats_identity();
-    run<true>(c, b.entries[k], (local + 1) * b.sub_bits, st, &o);
+    run<true>(c, b.entries[F.sub_base + ku], (ku + 1) * S, st, &o);
     uint32_t bad = (st.flags & kError) ? kStatusCorrupt : 0;
-    if (local == F.nsub - 1 && static_cast<uint32_t>(excl.nblk + st.nblk) < F.nblocks) bad |= kStatusCount;
+    if (ku == F.nsub - 1 && static_cast<uint32_t>(excl.nblk + st.nblk) < F.nblocks) bad |= kStatusCount;
     if (bad) atomicOr(&b.status[f], bad);
 }
 
 // ---------------------------------------------------------------------------
-// Host emulation of the four kernels (test hook; same state machine)
+// Host emulation of the four kernels (test hook; same state machine and the
+// same group geometry, without the LDS window)
 // ---------------------------------------------------------------------------
 void emulate(const EntBatchDev& b)
 {
     const uint32_t S = b.sub_bits;
-    // sync: per group, phase 1 then the LDS rounds
+    // sync: per group, phase 1 then the rounds
+    std::vector<uint32_t> win(kWinLds);
     for (uint32_t w = 0; w < b.nwg; ++w) {
         const EntFrame& F = b.frames[b.wg_frame[w]];
-        const RunCtx c = make_ctx(b, F, b.tabs + F.tab_base);
-        const uint32_t l0 = (w - F.wg_base) * kGroupSubs;
-        const int n = static_cast<int>(std::min<uint32_t>(kGroupSubs, F.nsub - l0));
-        std::vector<uint64_t> used(n), x(n), xs0(n), xs1(n);
-        std::vector<SubStats> st(n, stats_identity());
-        for (int t = 0; t < n; ++t) {
-            used[t] = guess_entry(c, (l0 + t) * S);
-            x[t] = run<false>(c, used[t], (l0 + t + 1) * S, st[t], nullptr);
+        RunCtx c = make_ctx(b, F, b.tabs + F.tab_base);
+        const uint32_t gl = w - F.wg_base;
+        group_window(F, gl, S, c.win_start, c.win_words);
+        stage_window(win.data(), F, c.data, c.win_start, c.win_words, 0, 1);
+        c.win = win.data();
+        std::vector<uint64_t> used(kGroupSubs, 0), x(kGroupSubs, 0), xs0(kGroupSubs, 0), xs1(kGroupSubs, 0);
+        std::vector<SubStats> st(kGroupSubs, stats_identity());
+        auto valid = [&](int t) { const int64_t k = group_sub(gl, t); return k >= 0 && k < int64_t(F.nsub); };
+        for (int t = 0; t < kGroupSubs; ++t) {
+            if (!valid(t)) continue;
+            const uint32_t k = static_cast<uint32_t>(group_sub(gl, t));
+            used[t] = guess_entry(c, k * S);
+            x[t] = run<false>(c, used[t], (k + 1) * S, st[t], nullptr);
             xs0[t] = x[t];
         }
         std::vector<uint64_t>* cur = &xs0;
         std::vector<uint64_t>* nxt = &xs1;
         for (;;) {
             bool changed = false;
-            for (int t = 0; t < n; ++t) {
-                if (t > 0 && !same_state((*cur)[t - 1], used[t])) {
+            for (int t = 0; t < kGroupSubs; ++t) {
+                const int64_t k = group_sub(gl, t);
+                if (valid(t) && t > 0 && k > 0 && !same_state((*cur)[t - 1], used[t])) {
                     SubStats s2 = stats_identity();
-                    const uint64_t x2 = run<false>(c, (*cur)[t - 1], (l0 + t + 1) * S, s2, nullptr);
+                    const uint64_t x2 = run<false>(c, (*cur)[t - 1], (static_cast<uint32_t>(k) + 1) * S, s2, nullptr);
                     changed |= !same_state(x2, x[t]);
                     used[t] = (*cur)[t - 1];
                     st[t] = s2;
@@ -503,34 +545,31 @@ void emulate(const EntBatchDev& b)
             std::swap(cur, nxt);
             if (!changed) break;
         }
-        for (int t = 0; t < n; ++t) {
-            b.entries[F.sub_base + l0 + t] = used[t];
-            b.stats[F.sub_base + l0 + t] = st[t];
+        SubStats a = stats_identity();
+        for (int t = 0; t < kGroupSubs; ++t) {
+            const bool own = valid(t) && t >= kWarm;
+            const uint32_t k = static_cast<uint32_t>(group_sub(gl, t));
+            if (own) {
+                b.entries[F.sub_base + k] = used[t];
+                b.stats[F.sub_base + k] = st[t];
+                a = stats_combine(a, st[t]);
+            } else if (t < kWarm) {
+                b.wentries[static_cast<uint64_t>(w) * kWarm + t] = used[t];
+            }
         }
-        b.xlast[w] = x[n - 1];
+        b.agg[w] = a;
     }
     // link
     for (uint32_t w = 0; w < b.nwg; ++w) {
         const uint32_t f = b.wg_frame[w];
         const EntFrame& F = b.frames[f];
-        const RunCtx c = make_ctx(b, F, b.tabs + F.tab_base);
-        const uint32_t l0 = (w - F.wg_base) * kGroupSubs;
-        const int n = static_cast<int>(std::min<uint32_t>(kGroupSubs, F.nsub - l0));
-        const uint32_t k0 = F.sub_base + l0;
-        if (w != F.wg_base) {
-            uint64_t cur = b.xlast[w - 1];
-            for (int i = 0; i < n; ++i) {
-                if (same_state(b.entries[k0 + i], cur)) break;
-                b.entries[k0 + i] = cur;
-                SubStats s = stats_identity();
-                cur = run<false>(c, cur, (l0 + i + 1) * S, s, nullptr);
-                b.stats[k0 + i] = s;
-                if (i == n - 1 && !same_state(cur, b.xlast[w])) b.status[f] |= kStatusFallback;
-            }
-        }
-        SubStats a = stats_identity();
-        for (int i = 0; i < n; ++i) a = stats_combine(a, b.stats[k0 + i]);
-        b.agg[w] = a;
+        const uint32_t gl = w - F.wg_base;
+        if (gl == 0) continue;
+        bool joined = false;
+        for (int t = 0; t < kWarm && !joined; ++t)
+            joined = same_state(b.wentries[static_cast<uint64_t>(w) * kWarm + t],
+                                b.entries[F.sub_base + static_cast<uint64_t>(group_sub(gl, t))]);
+        if (!joined) b.status[f] |= kStatusFallback;
     }
     // fallback
     for (uint32_t f = 0; f < b.nframes; ++f) {
@@ -544,24 +583,26 @@ void emulate(const EntBatchDev& b)
             cur = run<false>(c, cur, (i + 1) * S, s, nullptr);
             b.stats[F.sub_base + i] = s;
         }
-        const uint32_t nwg = (F.nsub + kGroupSubs - 1) / kGroupSubs;
-        for (uint32_t g = 0; g < nwg; ++g) {
+        for (uint32_t g = 0; g < frame_groups(F.nsub); ++g) {
             SubStats a = stats_identity();
-            for (uint32_t i = g * kGroupSubs; i < std::min<uint32_t>(F.nsub, (g + 1) * kGroupSubs); ++i)
+            for (uint32_t i = g * kOwn; i < std::min<uint32_t>(F.nsub, (g + 1) * kOwn); ++i)
                 a = stats_combine(a, b.stats[F.sub_base + i]);
             b.agg[F.wg_base + g] = a;
         }
     }
-    // write
-    std::vector<int16_t> stage(kStageStride);
+    // write (group order = subsequence order), each group through its window
     for (uint32_t f = 0; f < b.nframes; ++f) {
         const EntFrame& F = b.frames[f];
-        const RunCtx c = make_ctx(b, F, b.tabs + F.tab_base);
+        RunCtx c = make_ctx(b, F, b.tabs + F.tab_base);
         SubStats pre = stats_identity();
         for (uint32_t i = 0; i < F.nsub; ++i) {
+            if (i % kOwn == 0) {
+                group_window(F, i / kOwn, S, c.win_start, c.win_words);
+                stage_window(win.data(), F, c.data, c.win_start, c.win_words, 0, 1);
+                c.win = win.data();
+            }
             RunOut o;
             o.coefs = b.coefs + F.coef_off * 64;
-            o.stage = stage.data();
             o.blk = static_cast<uint32_t>(pre.nblk);
             o.nblocks = F.nblocks;
             o.pred[0] = pre.dc[0];
@@ -591,7 +632,7 @@ struct hjd_gdec {
     uint8_t* d_blob = nullptr;
     uint64_t* d_entries = nullptr;
     SubStats* d_stats = nullptr;
-    uint64_t* d_xlast = nullptr;
+    uint64_t* d_wentries = nullptr;
     SubStats* d_agg = nullptr;
     uint32_t* d_status = nullptr;
     uint32_t* h_status = nullptr;       // pinned
@@ -604,7 +645,7 @@ struct hjd_gdec {
     int first_error = HJD_OK;
 
     // host-side work arrays for emulation
-    std::vector<uint64_t> e_entries, e_xlast;
+    std::vector<uint64_t> e_entries, e_wentries;
     std::vector<SubStats> e_stats, e_agg;
     std::vector<uint32_t> e_status;
 
@@ -667,7 +708,7 @@ int hjd_gdec::assemble(uint8_t* blob, int16_t* coefs, int64_t* block_offsets, vo
         ntab += static_cast<size_t>(p.ntab);
         nseg += p.seg_end.size();
         const uint32_t ns = (p.data_bits + S - 1) / S;
-        nwg += (ns + kGroupSubs - 1) / kGroupSubs;
+        nwg += frame_groups(ns);
     }
     HdrOffsets& o = H;
     o.frames = 0;
@@ -706,7 +747,7 @@ int hjd_gdec::assemble(uint8_t* blob, int16_t* coefs, int64_t* block_offsets, vo
         ef[i] = F;
         memcpy(tb + tab_base, p.tabs, sizeof(HuffLut) * p.ntab);
         memcpy(seg + seg_base, p.seg_end.data(), 4 * p.seg_end.size());
-        const uint32_t nw = (F.nsub + kGroupSubs - 1) / kGroupSubs;
+        const uint32_t nw = frame_groups(F.nsub);
         for (uint32_t g = 0; g < nw; ++g) wgf[wg_base + g] = static_cast<uint32_t>(i);
         if (block_offsets) block_offsets[i] = static_cast<int64_t>(coef_off);
         sub_base += F.nsub;
@@ -780,7 +821,7 @@ int gdec_alloc(hjd_gdec* g)
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_blob), total));
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_entries), 8 * static_cast<size_t>(g->caps.max_subs)));
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_stats), sizeof(SubStats) * static_cast<size_t>(g->caps.max_subs)));
-    HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_xlast), 8 * static_cast<size_t>(g->caps.max_wgs)));
+    HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_wentries), 8 * kWarm * static_cast<size_t>(g->caps.max_wgs)));
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_agg), sizeof(SubStats) * static_cast<size_t>(g->caps.max_wgs)));
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_status), 4 * static_cast<size_t>(g->caps.max_frames)));
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_coefs), 128 * static_cast<size_t>(g->caps.max_blocks)));
@@ -796,7 +837,7 @@ int launch_entropy(hjd_gdec* g, const EntBatchDev& b, hipStream_t s)
     HJD_HIP(hipMemsetAsync(g->d_status, 0, 4 * static_cast<size_t>(b.nframes), s));
     hipLaunchKernelGGL(ent_sync_kernel, dim3(b.nwg), dim3(kGroupSubs), 0, s, b);
     HJD_HIP(hipGetLastError());
-    hipLaunchKernelGGL(ent_link_kernel, dim3(b.nwg), dim3(64), 0, s, b);
+    hipLaunchKernelGGL(ent_link_kernel, dim3((b.nwg + 255) / 256), dim3(256), 0, s, b);
     HJD_HIP(hipGetLastError());
     hipLaunchKernelGGL(ent_fallback_kernel, dim3(b.nframes), dim3(64), 0, s, b);
     HJD_HIP(hipGetLastError());
@@ -821,7 +862,7 @@ int gdec_run(hjd_gdec* g, const uint8_t* const* datas, const size_t* sizes, int 
     if (rc) return rc;
     b.entries = g->d_entries;
     b.stats = g->d_stats;
-    b.xlast = g->d_xlast;
+    b.wentries = g->d_wentries;
     b.agg = g->d_agg;
     b.status = g->d_status;
     HJD_HIP(hipMemcpyAsync(g->d_blob, g->h_stage, g->H.used, hipMemcpyHostToDevice, s));
@@ -888,7 +929,7 @@ int hjd_gdec_destroy(hjd_gdec* g)
     if (g->done) (void)hipEventSynchronize(g->done);
     if (g->h_stage) (void)hipHostFree(g->h_stage);
     if (g->h_status) (void)hipHostFree(g->h_status);
-    void* dev[] = {g->d_blob, g->d_entries, g->d_stats, g->d_xlast, g->d_agg, g->d_status, g->d_coefs};
+    void* dev[] = {g->d_blob, g->d_entries, g->d_stats, g->d_wentries, g->d_agg, g->d_status, g->d_coefs};
     for (void* p : dev)
         if (p) (void)hipFree(p);
     if (g->staged) (void)hipEventDestroy(g->staged);
@@ -957,12 +998,12 @@ int hjd_debug_entropy_emulate(const uint8_t* data, size_t size, int sub_bits, in
     const int64_t total = g.frames[0].nblocks;
     g.e_entries.assign(static_cast<size_t>(g.caps.max_subs), 0);
     g.e_stats.assign(static_cast<size_t>(g.caps.max_subs), stats_identity());
-    g.e_xlast.assign(static_cast<size_t>(g.caps.max_wgs), 0);
+    g.e_wentries.assign(static_cast<size_t>(g.caps.max_wgs) * kWarm, 0);
     g.e_agg.assign(static_cast<size_t>(g.caps.max_wgs), stats_identity());
     g.e_status.assign(1, 0);
     b.entries = g.e_entries.data();
     b.stats = g.e_stats.data();
-    b.xlast = g.e_xlast.data();
+    b.wentries = g.e_wentries.data();
     b.agg = g.e_agg.data();
     b.status = g.e_status.data();
     memset(coefs, 0, static_cast<size_t>(total) * 128);

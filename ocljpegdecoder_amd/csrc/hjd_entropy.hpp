@@ -41,8 +41,11 @@ namespace ent {
 constexpr int kLutBits = 10;                    // first-level lookup width
 constexpr int kMaxTables = 6;                   // DC+AC per component at most
 constexpr int kGroupSubs = 256;                 // subsequences per workgroup (one per thread)
+constexpr int kWarm = 8;                        // leading subsequences a group shares with its predecessor
+constexpr int kOwn = kGroupSubs - kWarm;        // subsequences a group is responsible for
 constexpr int kDefaultSubBits = 1024;           // S
-constexpr int kStageStride = 72;                // int16 per lane in the block staging buffer (144 B)
+constexpr int kWinRaw = 8320;                   // bit-window words staged in LDS per group (S <= 1024 fits)
+constexpr int kWinLds = kWinRaw + kWinRaw / 32; // one pad word per 32: row stride 33 (conflict-free b32 reads)
 
 // One Huffman table in device form (2448 B, 16-B multiple).
 struct HuffLut {
@@ -165,6 +168,8 @@ struct RunCtx {
     int bpm;
     uint64_t jinfo_q;    // jinfo[0..3], 16 bits each
     uint32_t jinfo_hi;   // jinfo[4..5]
+    const uint32_t* win; // LDS copy of words [win_start, win_start + win_words), byte-swapped, padded rows
+    uint32_t win_start, win_words;
 };
 
 // Blend (not select) between the two words so the context stays in registers.
@@ -178,7 +183,6 @@ __host__ __device__ __forceinline__ uint32_t jinfo_of(const RunCtx& c, uint32_t 
 // Output side of a write-mode run.
 struct RunOut {
     int16_t* coefs;        // frame's first block
-    int16_t* stage;        // this lane's 64-coefficient staging slot
     uint32_t blk;          // index of the next block this run owns
     uint32_t nblocks;
     int32_t pred[3];
@@ -193,16 +197,13 @@ __host__ __device__ __forceinline__ void zero_block(int16_t* stage)
     for (int q = 0; q < 8; ++q) p[q] = zv;
 }
 
-__host__ __device__ __forceinline__ void copy_block(int16_t* dst, const int16_t* stage)
+// Big-endian word wi of the frame's bit string: from the LDS window when
+// staged, else from global memory.
+__host__ __device__ __forceinline__ uint32_t load_word(const RunCtx& c, uint32_t wi)
 {
-    const u32x4* s = reinterpret_cast<const u32x4*>(stage);
-    u32x4* d = reinterpret_cast<u32x4*>(dst);
-    for (int q = 0; q < 8; ++q) d[q] = s[q];
-}
-
-__host__ __device__ __forceinline__ uint32_t load_word(const uint8_t* d, uint32_t wi)
-{
-    return bswap32(reinterpret_cast<const uint32_t*>(d)[wi]);
+    const uint32_t u = wi - c.win_start;
+    if (u < c.win_words) return c.win[u + (u >> 5)];
+    return bswap32(reinterpret_cast<const uint32_t*>(c.data)[wi]);
 }
 
 __host__ __device__ __forceinline__ uint32_t funnel(uint32_t w0, uint32_t w1, uint32_t off)
@@ -246,8 +247,9 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
         }
         uint32_t seg_end = c.seg_end[seg];
         uint32_t wi = pos >> 5;
-        uint32_t w0 = load_word(c.data, wi), w1 = load_word(c.data, wi + 1);
+        uint32_t w0 = load_word(c, wi), w1 = load_word(c, wi + 1);
         bool owned = false;                            // write mode: current block started in this run
+        int16_t* cur = nullptr;                        // write mode: its destination (null: not written)
         uint32_t ji = jinfo_of(c, j);
         result = 0;
         bool done = false;
@@ -257,10 +259,10 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
             if (nwi != wi) {
                 if (nwi == wi + 1) {
                     w0 = w1;
-                    w1 = load_word(c.data, nwi + 1);
+                    w1 = load_word(c, nwi + 1);
                 } else {
-                    w0 = load_word(c.data, nwi);
-                    w1 = load_word(c.data, nwi + 1);
+                    w0 = load_word(c, nwi);
+                    w1 = load_word(c, nwi + 1);
                 }
                 wi = nwi;
             }
@@ -277,6 +279,7 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
                     z = 0;
                     ji = jinfo_of(c, 0);
                     owned = false;
+                    cur = nullptr;
                     flags |= kReset;
                     d0 = d1 = d2 = 0;
                     p0 = p1 = p2 = 0;
@@ -333,8 +336,19 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
                     p0 += comp == 0 ? v : 0;
                     p1 += comp == 1 ? v : 0;
                     p2 += comp == 2 ? v : 0;
-                    zero_block(out->stage);
-                    out->stage[0] = static_cast<int16_t>(comp == 0 ? p0 : (comp == 1 ? p1 : p2));
+                    // MCU-major destination; on valid data blk % bpm == j.  Blocks past
+                    // the frame's count are ignored (as the host decoder stops there).
+                    const uint32_t dst = blk - j + (ji >> 8);
+                    cur = nullptr;
+                    if (blk < out->nblocks) {
+                        if (dst < out->nblocks && blk % static_cast<uint32_t>(c.bpm) == j) {
+                            cur = out->coefs + static_cast<uint64_t>(dst) * 64;
+                            zero_block(cur);
+                            cur[0] = static_cast<int16_t>(comp == 0 ? p0 : (comp == 1 ? p1 : p2));
+                        } else {
+                            flags |= kError;   // a restart interval ended inside an MCU
+                        }
+                    }
                 }
                 z = 1;
             } else if (s == 0) {
@@ -345,23 +359,15 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
                     flags |= kError;
                     z = 64;
                 } else {
-                    if (kWrite && owned) out->stage[z] = static_cast<int16_t>(v);
+                    if (kWrite && cur) cur[z] = static_cast<int16_t>(v);
                     ++z;
                 }
             }
             if (z >= 64) {
                 if (kWrite && owned) {
-                    // MCU-major destination; on valid data blk % bpm == j.  Blocks past
-                    // the frame's count are ignored (as the host decoder stops there).
-                    const uint32_t dst = blk - j + (ji >> 8);
-                    if (blk < out->nblocks) {
-                        if (dst < out->nblocks && blk % static_cast<uint32_t>(c.bpm) == j)
-                            copy_block(out->coefs + static_cast<uint64_t>(dst) * 64, out->stage);
-                        else
-                            flags |= kError;   // a restart interval ended inside an MCU
-                    }
                     blk += 1;
                     owned = false;
+                    cur = nullptr;
                 }
                 z = 0;
                 j = j + 1 == static_cast<uint32_t>(c.bpm) ? 0 : j + 1;
