@@ -48,7 +48,7 @@ constexpr int kZigzag[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18,
                              35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
                              58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
 
-constexpr size_t kDataPad = 16;      // readable bytes after each frame's bit string
+constexpr size_t kDataPad = 32;      // readable bytes after each frame's bit string (one-word-ahead reads)
 constexpr size_t kAlign = 256;
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -233,6 +233,7 @@ struct EntBatchDev {
     uint64_t* entries;
     SubStats* stats;
     uint64_t* wentries;   // [group][kWarm] warm-up entries
+    uint32_t* linked;     // [group] 1 if joined to the previous group's chain
     SubStats* agg;
     uint32_t* status;
     int16_t* coefs;
@@ -251,9 +252,6 @@ __host__ __device__ __forceinline__ RunCtx make_ctx(const EntBatchDev& b, const 
     c.jinfo_q = F.jinfo[0] | (static_cast<uint64_t>(F.jinfo[1]) << 16) | (static_cast<uint64_t>(F.jinfo[2]) << 32) |
                 (static_cast<uint64_t>(F.jinfo[3]) << 48);
     c.jinfo_hi = F.jinfo[4] | (static_cast<uint32_t>(F.jinfo[5]) << 16);
-    c.win = nullptr;
-    c.win_start = 0;
-    c.win_words = 0;
     return c;
 }
 
@@ -270,9 +268,6 @@ __host__ __device__ __forceinline__ int64_t group_sub(uint32_t gl, int t)
     return static_cast<int64_t>(gl) * kOwn - kWarm + t;
 }
 
-// Readable words of a frame's bit string (the host pads 16 bytes).
-__host__ __device__ __forceinline__ uint32_t readable_words(const EntFrame& F) { return (F.data_bits / 8 + 16) / 4; }
-
 // ---------------------------------------------------------------------------
 // Kernels (gfx950)
 // ---------------------------------------------------------------------------
@@ -283,44 +278,6 @@ __device__ __forceinline__ void load_tables(HuffLut* lds, const HuffLut* g, int 
     u32x4* dst = reinterpret_cast<u32x4*>(lds);
     const int n = ntab * static_cast<int>(sizeof(HuffLut) / 16);
     for (int i = tid; i < n; i += nthreads) dst[i] = src[i];
-}
-
-// Stage words [start, start + n) of the frame's bit string into the padded LDS
-// window (byte-swapped once here instead of per read).  start % 4 == 0.
-__host__ __device__ __forceinline__ void stage_window(uint32_t* win, const EntFrame& F, const uint8_t* data,
-                                                      uint32_t start, uint32_t n, int tid, int nthreads)
-{
-    const uint32_t readable = readable_words(F);
-    const uint32_t* g = reinterpret_cast<const uint32_t*>(data);
-    for (uint32_t i = static_cast<uint32_t>(tid) * 4; i < n; i += static_cast<uint32_t>(nthreads) * 4) {
-        const uint32_t wi = start + i;
-        uint32_t v[4];
-        if (wi + 4 <= readable) {
-            const u32x4 q = *reinterpret_cast<const u32x4*>(g + wi);
-            v[0] = q.x;
-            v[1] = q.y;
-            v[2] = q.z;
-            v[3] = q.w;
-        } else {
-            for (int e = 0; e < 4; ++e) v[e] = wi + e < readable ? g[wi + e] : 0xFFFFFFFFu;
-        }
-        uint32_t* row = win + i + (i >> 5);
-        for (int e = 0; e < 4; ++e) row[e] = bswap32(v[e]);
-    }
-}
-
-// Window of group gl: from its first subsequence to its last + margin.
-__host__ __device__ __forceinline__ void group_window(const EntFrame& F, uint32_t gl, uint32_t S, uint32_t& start,
-                                                      uint32_t& n)
-{
-    const int64_t k0 = group_sub(gl, 0);
-    const uint32_t first = k0 < 0 ? 0u : static_cast<uint32_t>(k0);
-    const int64_t lastk = k0 + kGroupSubs < static_cast<int64_t>(F.nsub) ? k0 + kGroupSubs : F.nsub;   // exclusive
-    const uint32_t last = static_cast<uint32_t>(lastk);
-    start = (static_cast<uint32_t>((static_cast<uint64_t>(first) * S) >> 5)) & ~3u;
-    const uint32_t end = static_cast<uint32_t>((static_cast<uint64_t>(last) * S + 95) >> 5);
-    const uint32_t want = ((end - start) + 3) & ~3u;
-    n = want < static_cast<uint32_t>(kWinRaw) ? want : static_cast<uint32_t>(kWinRaw);
 }
 
 __device__ __forceinline__ SubStats shfl_down_stats(const SubStats& s, int d)
@@ -354,19 +311,16 @@ __device__ __forceinline__ SubStats block_scan_inclusive(SubStats v, SubStats* b
 __global__ __launch_bounds__(kGroupSubs) void ent_sync_kernel(EntBatchDev b)
 {
     __shared__ HuffLut tabs[kMaxTables];
-    __shared__ uint32_t win[kWinLds];
     __shared__ uint64_t xs[2][kGroupSubs];
+    __shared__ SubStats buf[kGroupSubs];
     const int tid = threadIdx.x;
     const uint32_t w = blockIdx.x;
     const uint32_t f = b.wg_frame[w];
     const EntFrame F = b.frames[f];
     const uint32_t gl = w - F.wg_base;
     const uint32_t S = b.sub_bits;
-    RunCtx c = make_ctx(b, F, tabs);
-    group_window(F, gl, S, c.win_start, c.win_words);
+    const RunCtx c = make_ctx(b, F, tabs);
     load_tables(tabs, b.tabs + F.tab_base, F.ntab, tid, kGroupSubs);
-    stage_window(win, F, c.data, c.win_start, c.win_words, tid, kGroupSubs);
-    c.win = win;
     __syncthreads();
     const int64_t k = group_sub(gl, tid);
     const bool valid = k >= 0 && k < static_cast<int64_t>(F.nsub);
@@ -401,9 +355,6 @@ __global__ __launch_bounds__(kGroupSubs) void ent_sync_kernel(EntBatchDev b)
     } else if (tid < kWarm) {
         b.wentries[static_cast<uint64_t>(w) * kWarm + tid] = used;   // 0 for invalid (frame start group)
     }
-    // statistics of the owned range (scratch reuses the window)
-    SubStats* buf = reinterpret_cast<SubStats*>(win);
-    static_assert(sizeof(SubStats) * kGroupSubs <= sizeof(uint32_t) * kWinLds, "scan scratch");
     const SubStats total = block_scan_inclusive(own ? st : stats_identity(), buf, tid);
     if (tid == kGroupSubs - 1) b.agg[w] = total;
 }
@@ -415,48 +366,76 @@ __global__ __launch_bounds__(256) void ent_link_kernel(EntBatchDev b)
     const uint32_t f = b.wg_frame[w];
     const EntFrame F = b.frames[f];
     const uint32_t gl = w - F.wg_base;
-    if (gl == 0) return;
+    if (gl == 0) {
+        b.linked[w] = 1;
+        return;
+    }
     bool joined = false;
     for (int t = 0; t < kWarm && !joined; ++t) {
         const uint64_t k = static_cast<uint64_t>(group_sub(gl, t));
         joined = same_state(b.wentries[static_cast<uint64_t>(w) * kWarm + t], b.entries[F.sub_base + k]);
     }
+    b.linked[w] = joined ? 1u : 0u;
     if (!joined) atomicOr(&b.status[f], kStatusFallback);
+}
+
+// Repair of unjoined group boundaries, in order, one lane per flagged frame:
+// from the predecessor's last (verified) subsequence, re-decode forward until
+// the true chain meets the recorded chain again, rewriting entries/statistics
+// on the way; then recompute the aggregates of the groups touched.  Chains are
+// deterministic, so once two agree at a boundary they agree from there on.
+__host__ __device__ __forceinline__ void repair_frame(const EntBatchDev& b, uint32_t f, const HuffLut* tabs)
+{
+    const EntFrame& F = b.frames[f];
+    const RunCtx c = make_ctx(b, F, tabs);
+    const uint32_t ng = frame_groups(F.nsub);
+    uint32_t done = 0;          // subsequences < done are verified
+    uint32_t g_lo = ng, g_hi = 0;
+    for (uint32_t gl = 1; gl < ng; ++gl) {
+        const uint32_t first = gl * kOwn;
+        if (first < done || b.linked[F.wg_base + gl]) continue;
+        uint32_t k = first - 1;
+        uint64_t cur = b.entries[F.sub_base + k];
+        for (;;) {
+            SubStats st = stats_identity();
+            const uint64_t x = run<false>(c, cur, (k + 1) * b.sub_bits, st, nullptr);
+            if (k >= first) {
+                b.entries[F.sub_base + k] = cur;
+                b.stats[F.sub_base + k] = st;
+                const uint32_t g = k / kOwn;
+                g_lo = g < g_lo ? g : g_lo;
+                g_hi = g > g_hi ? g : g_hi;
+            }
+            ++k;
+            if (k >= F.nsub || same_state(x, b.entries[F.sub_base + k])) break;
+            cur = x;
+        }
+        done = k;
+    }
+    for (uint32_t g = g_lo; g <= g_hi && g < ng; ++g) {
+        SubStats a = stats_identity();
+        const uint32_t end = (g + 1) * kOwn < F.nsub ? (g + 1) * kOwn : F.nsub;
+        for (uint32_t i = g * kOwn; i < end; ++i) a = stats_combine(a, b.stats[F.sub_base + i]);
+        b.agg[F.wg_base + g] = a;
+    }
 }
 
 __global__ __launch_bounds__(64) void ent_fallback_kernel(EntBatchDev b)
 {
     __shared__ HuffLut tabs[kMaxTables];
-    __shared__ SubStats red[64];
     const int lane = threadIdx.x;
     const uint32_t f = blockIdx.x;
     if (!(b.status[f] & kStatusFallback)) return;
     const EntFrame F = b.frames[f];
     load_tables(tabs, b.tabs + F.tab_base, F.ntab, lane, 64);
     __syncthreads();
-    if (lane == 0) {
-        const RunCtx c = make_ctx(b, F, tabs);
-        uint64_t cur = pack_state(0, 0, 0, 0);
-        for (uint32_t i = 0; i < F.nsub; ++i) {
-            b.entries[F.sub_base + i] = cur;
-            SubStats st = stats_identity();
-            cur = run<false>(c, cur, (i + 1) * b.sub_bits, st, nullptr);
-            b.stats[F.sub_base + i] = st;
-        }
-        for (uint32_t g = 0; g < frame_groups(F.nsub); ++g) {
-            SubStats a = stats_identity();
-            for (uint32_t i = g * kOwn; i < min(F.nsub, (g + 1) * kOwn); ++i) a = stats_combine(a, b.stats[F.sub_base + i]);
-            b.agg[F.wg_base + g] = a;
-        }
-    }
-    (void)red;
+    if (lane == 0) repair_frame(b, f, tabs);
 }
 
 __global__ __launch_bounds__(kGroupSubs) void ent_write_kernel(EntBatchDev b)
 {
     __shared__ HuffLut tabs[kMaxTables];
-    __shared__ uint32_t win[kWinLds];
-    SubStats* buf = reinterpret_cast<SubStats*>(win);   // scan scratch, before the window is staged
+    __shared__ SubStats buf[kGroupSubs];
     const int tid = threadIdx.x;
     const uint32_t w = blockIdx.x;
     const uint32_t f = b.wg_frame[w];
@@ -479,13 +458,8 @@ __global__ __launch_bounds__(kGroupSubs) void ent_write_kernel(EntBatchDev b)
     const SubStats mine = own ? b.stats[F.sub_base + ku] : stats_identity();
     block_scan_inclusive(mine, buf, tid);
     const SubStats excl = stats_combine(pre, tid > 0 ? buf[tid - 1] : stats_identity());
-    RunCtx c = make_ctx(b, F, tabs);
-    group_window(F, gl, S, c.win_start, c.win_words);
-    __syncthreads();   // scratch reads done before the window overwrites it
-    stage_window(win, F, c.data, c.win_start, c.win_words, tid, kGroupSubs);
-    c.win = win;
-    __syncthreads();
     if (!own) return;
+    const RunCtx c = make_ctx(b, F, tabs);
     RunOut o;
     o.coefs = b.coefs + F.coef_off * 64;
     o.blk = static_cast<uint32_t>(excl.nblk);
@@ -508,14 +482,10 @@ void emulate(const EntBatchDev& b)
 {
     const uint32_t S = b.sub_bits;
     // sync: per group, phase 1 then the rounds
-    std::vector<uint32_t> win(kWinLds);
     for (uint32_t w = 0; w < b.nwg; ++w) {
         const EntFrame& F = b.frames[b.wg_frame[w]];
-        RunCtx c = make_ctx(b, F, b.tabs + F.tab_base);
+        const RunCtx c = make_ctx(b, F, b.tabs + F.tab_base);
         const uint32_t gl = w - F.wg_base;
-        group_window(F, gl, S, c.win_start, c.win_words);
-        stage_window(win.data(), F, c.data, c.win_start, c.win_words, 0, 1);
-        c.win = win.data();
         std::vector<uint64_t> used(kGroupSubs, 0), x(kGroupSubs, 0), xs0(kGroupSubs, 0), xs1(kGroupSubs, 0);
         std::vector<SubStats> st(kGroupSubs, stats_identity());
         auto valid = [&](int t) { const int64_t k = group_sub(gl, t); return k >= 0 && k < int64_t(F.nsub); };
@@ -564,43 +534,22 @@ void emulate(const EntBatchDev& b)
         const uint32_t f = b.wg_frame[w];
         const EntFrame& F = b.frames[f];
         const uint32_t gl = w - F.wg_base;
-        if (gl == 0) continue;
-        bool joined = false;
+        bool joined = gl == 0;
         for (int t = 0; t < kWarm && !joined; ++t)
             joined = same_state(b.wentries[static_cast<uint64_t>(w) * kWarm + t],
                                 b.entries[F.sub_base + static_cast<uint64_t>(group_sub(gl, t))]);
+        b.linked[w] = joined ? 1u : 0u;
         if (!joined) b.status[f] |= kStatusFallback;
     }
-    // fallback
+    // repair
+    for (uint32_t f = 0; f < b.nframes; ++f)
+        if (b.status[f] & kStatusFallback) repair_frame(b, f, b.tabs + b.frames[f].tab_base);
+    // write (group order = subsequence order)
     for (uint32_t f = 0; f < b.nframes; ++f) {
-        if (!(b.status[f] & kStatusFallback)) continue;
         const EntFrame& F = b.frames[f];
         const RunCtx c = make_ctx(b, F, b.tabs + F.tab_base);
-        uint64_t cur = pack_state(0, 0, 0, 0);
-        for (uint32_t i = 0; i < F.nsub; ++i) {
-            b.entries[F.sub_base + i] = cur;
-            SubStats s = stats_identity();
-            cur = run<false>(c, cur, (i + 1) * S, s, nullptr);
-            b.stats[F.sub_base + i] = s;
-        }
-        for (uint32_t g = 0; g < frame_groups(F.nsub); ++g) {
-            SubStats a = stats_identity();
-            for (uint32_t i = g * kOwn; i < std::min<uint32_t>(F.nsub, (g + 1) * kOwn); ++i)
-                a = stats_combine(a, b.stats[F.sub_base + i]);
-            b.agg[F.wg_base + g] = a;
-        }
-    }
-    // write (group order = subsequence order), each group through its window
-    for (uint32_t f = 0; f < b.nframes; ++f) {
-        const EntFrame& F = b.frames[f];
-        RunCtx c = make_ctx(b, F, b.tabs + F.tab_base);
         SubStats pre = stats_identity();
         for (uint32_t i = 0; i < F.nsub; ++i) {
-            if (i % kOwn == 0) {
-                group_window(F, i / kOwn, S, c.win_start, c.win_words);
-                stage_window(win.data(), F, c.data, c.win_start, c.win_words, 0, 1);
-                c.win = win.data();
-            }
             RunOut o;
             o.coefs = b.coefs + F.coef_off * 64;
             o.blk = static_cast<uint32_t>(pre.nblk);
@@ -633,6 +582,7 @@ struct hjd_gdec {
     uint64_t* d_entries = nullptr;
     SubStats* d_stats = nullptr;
     uint64_t* d_wentries = nullptr;
+    uint32_t* d_linked = nullptr;
     SubStats* d_agg = nullptr;
     uint32_t* d_status = nullptr;
     uint32_t* h_status = nullptr;       // pinned
@@ -646,6 +596,7 @@ struct hjd_gdec {
 
     // host-side work arrays for emulation
     std::vector<uint64_t> e_entries, e_wentries;
+    std::vector<uint32_t> e_linked;
     std::vector<SubStats> e_stats, e_agg;
     std::vector<uint32_t> e_status;
 
@@ -822,6 +773,7 @@ int gdec_alloc(hjd_gdec* g)
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_entries), 8 * static_cast<size_t>(g->caps.max_subs)));
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_stats), sizeof(SubStats) * static_cast<size_t>(g->caps.max_subs)));
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_wentries), 8 * kWarm * static_cast<size_t>(g->caps.max_wgs)));
+    HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_linked), 4 * static_cast<size_t>(g->caps.max_wgs)));
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_agg), sizeof(SubStats) * static_cast<size_t>(g->caps.max_wgs)));
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_status), 4 * static_cast<size_t>(g->caps.max_frames)));
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_coefs), 128 * static_cast<size_t>(g->caps.max_blocks)));
@@ -863,6 +815,7 @@ int gdec_run(hjd_gdec* g, const uint8_t* const* datas, const size_t* sizes, int 
     b.entries = g->d_entries;
     b.stats = g->d_stats;
     b.wentries = g->d_wentries;
+    b.linked = g->d_linked;
     b.agg = g->d_agg;
     b.status = g->d_status;
     HJD_HIP(hipMemcpyAsync(g->d_blob, g->h_stage, g->H.used, hipMemcpyHostToDevice, s));
@@ -929,7 +882,7 @@ int hjd_gdec_destroy(hjd_gdec* g)
     if (g->done) (void)hipEventSynchronize(g->done);
     if (g->h_stage) (void)hipHostFree(g->h_stage);
     if (g->h_status) (void)hipHostFree(g->h_status);
-    void* dev[] = {g->d_blob, g->d_entries, g->d_stats, g->d_wentries, g->d_agg, g->d_status, g->d_coefs};
+    void* dev[] = {g->d_blob, g->d_entries, g->d_stats, g->d_wentries, g->d_linked, g->d_agg, g->d_status, g->d_coefs};
     for (void* p : dev)
         if (p) (void)hipFree(p);
     if (g->staged) (void)hipEventDestroy(g->staged);
@@ -970,6 +923,57 @@ int hjd_gdec_sync(hjd_gdec* g, int32_t* status)
     return HJD_OK;
 }
 
+// Tuning hook: for every subsequence start k*S (k >= 1), decode from the guess
+// (k*S, 0, 0) and report after how many bits past k*S its state first equals
+// the true decode's state at the same unit boundary (hist[min(bits/64, nbins-1)];
+// never-synced within max_bits go to the last bin).
+int hjd_debug_entropy_syncstats(const uint8_t* data, size_t size, int sub_bits, int max_bits, int64_t* hist, int nbins)
+{
+    if (!data || !hist || nbins < 2 || sub_bits < 32) return set_error(HJD_E_INVALID, "invalid arguments");
+    std::vector<uint8_t> buf(size + 64);
+    Prepared p;
+    int rc = prepare(data, size, buf.data(), size + 32, p);
+    if (rc) return rc;
+    EntFrame F;
+    memset(&F, 0, sizeof(F));
+    F.data_bits = p.data_bits;
+    F.nseg = static_cast<uint32_t>(p.seg_end.size());
+    F.bpm = static_cast<uint8_t>(p.bpm);
+    memcpy(F.jinfo, p.jinfo, sizeof(F.jinfo));
+    EntBatchDev b;
+    memset(&b, 0, sizeof(b));
+    b.data = buf.data();
+    b.seg_end = p.seg_end.data();
+    const RunCtx c = make_ctx(b, F, p.tabs);
+    // true states at every unit boundary: decode one unit at a time (stop = pos + 1)
+    std::vector<uint16_t> truth(p.data_bits + 1, 0xFFFF);
+    uint64_t cur = pack_state(0, 0, 0, 0);
+    while (st_seg(cur) < F.nseg) {
+        truth[st_pos(cur)] = static_cast<uint16_t>(st_j(cur) << 8 | st_z(cur));
+        SubStats st = stats_identity();
+        const uint64_t nx = run<false>(c, cur, st_pos(cur) + 1, st, nullptr);
+        if (st_pos(nx) <= st_pos(cur) && st_seg(nx) == st_seg(cur)) break;
+        cur = nx;
+    }
+    for (int i = 0; i < nbins; ++i) hist[i] = 0;
+    const uint32_t S = static_cast<uint32_t>(sub_bits);
+    for (uint32_t k = 1; static_cast<uint64_t>(k) * S < p.data_bits; ++k) {
+        uint64_t g = guess_entry(c, k * S);
+        int bin = nbins - 1;
+        while (st_pos(g) < static_cast<uint64_t>(k) * S + static_cast<uint32_t>(max_bits) && st_seg(g) < F.nseg) {
+            const uint32_t q = st_pos(g);
+            if (truth[q] == (st_j(g) << 8 | st_z(g))) {
+                bin = std::min<int>(nbins - 1, static_cast<int>((q - k * S) / 64));
+                break;
+            }
+            SubStats st = stats_identity();
+            g = run<false>(c, g, q + 1, st, nullptr);
+        }
+        hist[bin]++;
+    }
+    return HJD_OK;
+}
+
 int hjd_debug_entropy_emulate(const uint8_t* data, size_t size, int sub_bits, int16_t* coefs,
                               int64_t capacity_blocks, int32_t* status)
 {
@@ -999,11 +1003,13 @@ int hjd_debug_entropy_emulate(const uint8_t* data, size_t size, int sub_bits, in
     g.e_entries.assign(static_cast<size_t>(g.caps.max_subs), 0);
     g.e_stats.assign(static_cast<size_t>(g.caps.max_subs), stats_identity());
     g.e_wentries.assign(static_cast<size_t>(g.caps.max_wgs) * kWarm, 0);
+    g.e_linked.assign(static_cast<size_t>(g.caps.max_wgs), 0);
     g.e_agg.assign(static_cast<size_t>(g.caps.max_wgs), stats_identity());
     g.e_status.assign(1, 0);
     b.entries = g.e_entries.data();
     b.stats = g.e_stats.data();
     b.wentries = g.e_wentries.data();
+    b.linked = g.e_linked.data();
     b.agg = g.e_agg.data();
     b.status = g.e_status.data();
     memset(coefs, 0, static_cast<size_t>(total) * 128);

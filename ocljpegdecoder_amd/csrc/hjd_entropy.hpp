@@ -44,8 +44,6 @@ constexpr int kGroupSubs = 256;                 // subsequences per workgroup (o
 constexpr int kWarm = 8;                        // leading subsequences a group shares with its predecessor
 constexpr int kOwn = kGroupSubs - kWarm;        // subsequences a group is responsible for
 constexpr int kDefaultSubBits = 1024;           // S
-constexpr int kWinRaw = 8320;                   // bit-window words staged in LDS per group (S <= 1024 fits)
-constexpr int kWinLds = kWinRaw + kWinRaw / 32; // one pad word per 32: row stride 33 (conflict-free b32 reads)
 
 // One Huffman table in device form (2448 B, 16-B multiple).
 struct HuffLut {
@@ -168,8 +166,6 @@ struct RunCtx {
     int bpm;
     uint64_t jinfo_q;    // jinfo[0..3], 16 bits each
     uint32_t jinfo_hi;   // jinfo[4..5]
-    const uint32_t* win; // LDS copy of words [win_start, win_start + win_words), byte-swapped, padded rows
-    uint32_t win_start, win_words;
 };
 
 // Blend (not select) between the two words so the context stays in registers.
@@ -197,12 +193,9 @@ __host__ __device__ __forceinline__ void zero_block(int16_t* stage)
     for (int q = 0; q < 8; ++q) p[q] = zv;
 }
 
-// Big-endian word wi of the frame's bit string: from the LDS window when
-// staged, else from global memory.
+// Big-endian word wi of the frame's bit string.
 __host__ __device__ __forceinline__ uint32_t load_word(const RunCtx& c, uint32_t wi)
 {
-    const uint32_t u = wi - c.win_start;
-    if (u < c.win_words) return c.win[u + (u >> 5)];
     return bswap32(reinterpret_cast<const uint32_t*>(c.data)[wi]);
 }
 
@@ -246,8 +239,10 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
             p0 = p1 = p2 = 0;
         }
         uint32_t seg_end = c.seg_end[seg];
+        // w0, w1: the words under pos; w2 = the next one, loaded a word ahead
+        // so its latency overlaps the ~4 symbols decoded from w0/w1.
         uint32_t wi = pos >> 5;
-        uint32_t w0 = load_word(c, wi), w1 = load_word(c, wi + 1);
+        uint32_t w0 = load_word(c, wi), w1 = load_word(c, wi + 1), w2 = load_word(c, wi + 2);
         bool owned = false;                            // write mode: current block started in this run
         int16_t* cur = nullptr;                        // write mode: its destination (null: not written)
         uint32_t ji = jinfo_of(c, j);
@@ -259,11 +254,12 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
             if (nwi != wi) {
                 if (nwi == wi + 1) {
                     w0 = w1;
-                    w1 = load_word(c, nwi + 1);
+                    w1 = w2;
                 } else {
                     w0 = load_word(c, nwi);
                     w1 = load_word(c, nwi + 1);
                 }
+                w2 = load_word(c, nwi + 2);
                 wi = nwi;
             }
             const uint32_t peek = funnel(w0, w1, pos & 31);
