@@ -48,7 +48,7 @@ constexpr int kZigzag[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18,
                              35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
                              58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
 
-constexpr size_t kDataPad = 32;      // readable bytes after each frame's bit string (one-word-ahead reads)
+constexpr size_t kDataPad = 64;      // readable bytes after each frame's bit string (16-B chunks read ahead)
 constexpr size_t kAlign = 256;
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -435,7 +435,9 @@ __global__ __launch_bounds__(64) void ent_fallback_kernel(EntBatchDev b)
 __global__ __launch_bounds__(kGroupSubs) void ent_write_kernel(EntBatchDev b)
 {
     __shared__ HuffLut tabs[kMaxTables];
-    __shared__ SubStats buf[kGroupSubs];
+    __shared__ __attribute__((aligned(16))) int16_t stage[kGroupSubs * kStageStride];
+    SubStats* buf = reinterpret_cast<SubStats*>(stage);   // scan scratch before any block is staged
+    static_assert(sizeof(SubStats) * kGroupSubs <= sizeof(int16_t) * kGroupSubs * kStageStride, "scratch");
     const int tid = threadIdx.x;
     const uint32_t w = blockIdx.x;
     const uint32_t f = b.wg_frame[w];
@@ -458,10 +460,12 @@ __global__ __launch_bounds__(kGroupSubs) void ent_write_kernel(EntBatchDev b)
     const SubStats mine = own ? b.stats[F.sub_base + ku] : stats_identity();
     block_scan_inclusive(mine, buf, tid);
     const SubStats excl = stats_combine(pre, tid > 0 ? buf[tid - 1] : stats_identity());
+    __syncthreads();   // scratch reads done before blocks are staged
     if (!own) return;
     const RunCtx c = make_ctx(b, F, tabs);
     RunOut o;
     o.coefs = b.coefs + F.coef_off * 64;
+    o.stage = stage + tid * kStageStride;
     o.blk = static_cast<uint32_t>(excl.nblk);
     o.nblocks = F.nblocks;
     o.pred[0] = excl.dc[0];
@@ -545,6 +549,7 @@ void emulate(const EntBatchDev& b)
     for (uint32_t f = 0; f < b.nframes; ++f)
         if (b.status[f] & kStatusFallback) repair_frame(b, f, b.tabs + b.frames[f].tab_base);
     // write (group order = subsequence order)
+    alignas(16) int16_t stage[kStageStride];
     for (uint32_t f = 0; f < b.nframes; ++f) {
         const EntFrame& F = b.frames[f];
         const RunCtx c = make_ctx(b, F, b.tabs + F.tab_base);
@@ -552,6 +557,7 @@ void emulate(const EntBatchDev& b)
         for (uint32_t i = 0; i < F.nsub; ++i) {
             RunOut o;
             o.coefs = b.coefs + F.coef_off * 64;
+            o.stage = stage;
             o.blk = static_cast<uint32_t>(pre.nblk);
             o.nblocks = F.nblocks;
             o.pred[0] = pre.dc[0];

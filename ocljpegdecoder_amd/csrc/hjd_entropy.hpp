@@ -43,7 +43,8 @@ constexpr int kMaxTables = 6;                   // DC+AC per component at most
 constexpr int kGroupSubs = 256;                 // subsequences per workgroup (one per thread)
 constexpr int kWarm = 8;                        // leading subsequences a group shares with its predecessor
 constexpr int kOwn = kGroupSubs - kWarm;        // subsequences a group is responsible for
-constexpr int kDefaultSubBits = 1024;           // S
+constexpr int kDefaultSubBits = 2048;           // S
+constexpr int kStageStride = 72;                // int16 per lane in the block staging buffer (144 B)
 
 // One Huffman table in device form (2448 B, 16-B multiple).
 struct HuffLut {
@@ -179,6 +180,7 @@ __host__ __device__ __forceinline__ uint32_t jinfo_of(const RunCtx& c, uint32_t 
 // Output side of a write-mode run.
 struct RunOut {
     int16_t* coefs;        // frame's first block
+    int16_t* stage;        // this lane's 64-coefficient staging slot (LDS on the device)
     uint32_t blk;          // index of the next block this run owns
     uint32_t nblocks;
     int32_t pred[3];
@@ -193,11 +195,73 @@ __host__ __device__ __forceinline__ void zero_block(int16_t* stage)
     for (int q = 0; q < 8; ++q) p[q] = zv;
 }
 
-// Big-endian word wi of the frame's bit string.
-__host__ __device__ __forceinline__ uint32_t load_word(const RunCtx& c, uint32_t wi)
+__host__ __device__ __forceinline__ void copy_block(int16_t* dst, const int16_t* stage)
 {
-    return bswap32(reinterpret_cast<const uint32_t*>(c.data)[wi]);
+    const u32x4* s = reinterpret_cast<const u32x4*>(stage);
+    u32x4* d = reinterpret_cast<u32x4*>(dst);
+    for (int q = 0; q < 8; ++q) d[q] = s[q];
 }
+
+// Big-endian words of the frame's bit string, read 16 B at a time.
+__host__ __device__ __forceinline__ u32x4 load_chunk(const RunCtx& c, uint32_t ci)
+{
+    u32x4 v = reinterpret_cast<const u32x4*>(c.data)[ci];
+    v.x = bswap32(v.x);
+    v.y = bswap32(v.y);
+    v.z = bswap32(v.z);
+    v.w = bswap32(v.w);
+    return v;
+}
+
+// Per-lane bit window: w0:w1 are the words under the read position; q holds
+// the following words and r the next 16-B chunk, already in flight -- about 18
+// symbols of lead, enough to hide an HBM miss (each lane streams its own lines,
+// so every line crossing misses the caches).  Only fixed register moves, no
+// indexed registers.
+struct BitWindow {
+    uint32_t w0, w1, q0, q1, q2, q3, q4, q5;
+    u32x4 r;
+    uint32_t nq, next, wi;
+
+    __host__ __device__ __forceinline__ void advance(const RunCtx& c)
+    {
+        w0 = w1;
+        w1 = q0;
+        q0 = q1;
+        q1 = q2;
+        q2 = q3;
+        q3 = q4;
+        q4 = q5;
+        ++wi;
+        if (--nq == 0) {
+            q0 = r.x;
+            q1 = r.y;
+            q2 = r.z;
+            q3 = r.w;
+            nq = 4;
+            r = load_chunk(c, next++);
+        }
+    }
+
+    __host__ __device__ __forceinline__ void seek(const RunCtx& c, uint32_t word)
+    {
+        const uint32_t ci = word >> 2;
+        const u32x4 a = load_chunk(c, ci), b = load_chunk(c, ci + 1);
+        r = load_chunk(c, ci + 2);
+        next = ci + 3;
+        w0 = a.x;
+        w1 = a.y;
+        q0 = a.z;
+        q1 = a.w;
+        q2 = b.x;
+        q3 = b.y;
+        q4 = b.z;
+        q5 = b.w;
+        nq = 6;
+        wi = ci * 4;
+        for (uint32_t i = 0; i < (word & 3); ++i) advance(c);
+    }
+};
 
 __host__ __device__ __forceinline__ uint32_t funnel(uint32_t w0, uint32_t w1, uint32_t off)
 {
@@ -239,10 +303,8 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
             p0 = p1 = p2 = 0;
         }
         uint32_t seg_end = c.seg_end[seg];
-        // w0, w1: the words under pos; w2 = the next one, loaded a word ahead
-        // so its latency overlaps the ~4 symbols decoded from w0/w1.
-        uint32_t wi = pos >> 5;
-        uint32_t w0 = load_word(c, wi), w1 = load_word(c, wi + 1), w2 = load_word(c, wi + 2);
+        BitWindow bw;
+        bw.seek(c, pos >> 5);
         bool owned = false;                            // write mode: current block started in this run
         int16_t* cur = nullptr;                        // write mode: its destination (null: not written)
         uint32_t ji = jinfo_of(c, j);
@@ -251,18 +313,11 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
         while (!done) {
             if (pos >= stop && (!kWrite || !owned)) break;
             const uint32_t nwi = pos >> 5;
-            if (nwi != wi) {
-                if (nwi == wi + 1) {
-                    w0 = w1;
-                    w1 = w2;
-                } else {
-                    w0 = load_word(c, nwi);
-                    w1 = load_word(c, nwi + 1);
-                }
-                w2 = load_word(c, nwi + 2);
-                wi = nwi;
+            if (nwi != bw.wi) {
+                if (nwi == bw.wi + 1) bw.advance(c);
+                else bw.seek(c, nwi);
             }
-            const uint32_t peek = funnel(w0, w1, pos & 31);
+            const uint32_t peek = funnel(bw.w0, bw.w1, pos & 31);
             // ---- restart-interval end: < 8 bits left, all ones (or overrun) ----
             const int32_t left = static_cast<int32_t>(seg_end - pos);
             if (left < 8) {
@@ -339,8 +394,8 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
                     if (blk < out->nblocks) {
                         if (dst < out->nblocks && blk % static_cast<uint32_t>(c.bpm) == j) {
                             cur = out->coefs + static_cast<uint64_t>(dst) * 64;
-                            zero_block(cur);
-                            cur[0] = static_cast<int16_t>(comp == 0 ? p0 : (comp == 1 ? p1 : p2));
+                            zero_block(out->stage);
+                            out->stage[0] = static_cast<int16_t>(comp == 0 ? p0 : (comp == 1 ? p1 : p2));
                         } else {
                             flags |= kError;   // a restart interval ended inside an MCU
                         }
@@ -355,12 +410,13 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
                     flags |= kError;
                     z = 64;
                 } else {
-                    if (kWrite && cur) cur[z] = static_cast<int16_t>(v);
+                    if (kWrite && cur) out->stage[z] = static_cast<int16_t>(v);
                     ++z;
                 }
             }
             if (z >= 64) {
                 if (kWrite && owned) {
+                    if (cur) copy_block(cur, out->stage);   // 8 x 16-B stores of the finished block
                     blk += 1;
                     owned = false;
                     cur = nullptr;
