@@ -111,6 +111,22 @@ int hjd_gdec_sync(hjd_gdec* g, int32_t* status);
 #define HJD_GDEC_CORRUPT 2      /* invalid Huffman data on the decoded chain */
 #define HJD_GDEC_COUNT 4        /* fewer blocks than the frame needs */
 
+/* ---- GPU-entropy stream: JPEG bytes in, BGRX in HBM out -----------------
+ * Like hjd_stream, but the Huffman decode runs on the GPU: worker threads only
+ * parse + destuff each JPEG into the pinned staging of the open batch (up to
+ * max_frames JPEGs / max_scan_bytes / max_blocks per batch); nslots (2..8)
+ * batches rotate on their own HIP streams so uploads overlap kernels. */
+typedef struct hjd_gstream hjd_gstream;
+int hjd_gstream_create(hjd_ctx* ctx, int max_frames, int64_t max_scan_bytes, int64_t max_blocks, int nslots,
+                       int nthreads, hjd_gstream** out);
+int hjd_gstream_destroy(hjd_gstream* s);
+/* Queue one JPEG (bytes valid until hjd_gstream_sync returns); pixels go to
+ * d_out (device, row pitch out_pitch bytes, 16-byte aligned). */
+int hjd_gstream_submit(hjd_gstream* s, const uint8_t* data, size_t size, void* d_out, int32_t out_pitch);
+/* Flush and wait; returns the first error.  stats (may be NULL):
+ * {images, pixels, host_prep_ns, h2d_bytes, batches}. */
+int hjd_gstream_sync(hjd_gstream* s, int64_t stats[5]);
+
 /* Test hook (no GPU): runs the same parallel algorithm on the host, one frame,
  * and writes its coefficients.  Not a decode path. */
 int hjd_debug_entropy_emulate(const uint8_t* data, size_t size, int sub_bits, int16_t* coefs, int64_t capacity_blocks,

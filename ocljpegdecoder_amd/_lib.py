@@ -135,6 +135,11 @@ def _bind_host(lib):
         "hjd_gdec_decode_coefs": (ctypes.c_int, [vp, ctypes.POINTER(u8p), ctypes.POINTER(ctypes.c_size_t),
                                                  ctypes.c_int, vp, ctypes.POINTER(ctypes.c_int64), vp]),
         "hjd_gdec_sync": (ctypes.c_int, [vp, c_i32p]),
+        "hjd_gstream_create": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
+                                              ctypes.c_int, ctypes.POINTER(vp)]),
+        "hjd_gstream_destroy": (ctypes.c_int, [vp]),
+        "hjd_gstream_submit": (ctypes.c_int, [vp, u8p, ctypes.c_size_t, vp, ctypes.c_int32]),
+        "hjd_gstream_sync": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int64)]),
         "hjd_debug_entropy_emulate": (ctypes.c_int, [u8p, ctypes.c_size_t, ctypes.c_int,
                                                      ctypes.POINTER(ctypes.c_int16), ctypes.c_int64, c_i32p]),
     })

@@ -612,6 +612,9 @@ struct hjd_gdec {
 
     int wait_staging();
     int stage_frames(const uint8_t* const* datas, const size_t* sizes, int n);
+    // Parse + destuff one JPEG into frames[i] / the data area at data_off
+    // (thread-safe for distinct i and disjoint data ranges).
+    int prepare_frame(int i, const uint8_t* data, size_t size, size_t data_off, size_t cap);
     // Lays out and fills the header for the staged frames (pixel records too
     // when d_outs is given); returns the device view (pointers into `blob`).
     int assemble(uint8_t* blob, int16_t* coefs, int64_t* block_offsets, void* const* d_outs, const int32_t* pitches,
@@ -631,6 +634,18 @@ int hjd_gdec::wait_staging()
     return HJD_OK;
 }
 
+int hjd_gdec::prepare_frame(int i, const uint8_t* data, size_t size, size_t data_off, size_t cap)
+{
+    Prepared& p = frames[static_cast<size_t>(i)];
+    p = Prepared();
+    p.data_off = data_off;
+    if (!data) return p.rc = set_error(HJD_E_INVALID, "frame %d: NULL data", i);
+    if (cap <= kDataPad) return p.rc = set_error(HJD_E_INVALID, "scan bytes exceed the batch capacity");
+    int rc = prepare(data, size, data_area() + data_off, cap - kDataPad, p);
+    if (rc) return p.rc = rc;
+    return HJD_OK;
+}
+
 int hjd_gdec::stage_frames(const uint8_t* const* datas, const size_t* sizes, int n)
 {
     if (n <= 0 || n > caps.max_frames) return set_error(HJD_E_INVALID, "batch of %d frames (capacity %d)", n,
@@ -639,15 +654,11 @@ int hjd_gdec::stage_frames(const uint8_t* const* datas, const size_t* sizes, int
     data_used = 0;
     int64_t blocks = 0;
     for (int i = 0; i < n; ++i) {
-        if (!datas[i]) return set_error(HJD_E_INVALID, "frame %d: NULL data", i);
-        Prepared& p = frames[i];
-        p.data_off = data_used;
-        const size_t cap = data_cap() - data_used;
-        if (cap <= kDataPad) return set_error(HJD_E_INVALID, "scan bytes exceed the batch capacity");
-        int rc = prepare(datas[i], sizes[i], data_area() + data_used, cap - kDataPad, p);
+        if (data_used >= data_cap()) return set_error(HJD_E_INVALID, "scan bytes exceed the batch capacity");
+        int rc = prepare_frame(i, datas[i], sizes[i], data_used, data_cap() - data_used);
         if (rc) return set_error(rc, "frame %d: %s", i, hjd_last_error());
-        data_used = align_up(data_used + p.data_bits / 8 + kDataPad, 16);
-        blocks += p.nblocks;
+        data_used = align_up(data_used + frames[i].data_bits / 8 + kDataPad, 16);
+        blocks += frames[i].nblocks;
     }
     if (blocks > caps.max_blocks)
         return set_error(HJD_E_INVALID, "batch needs %lld blocks (capacity %lld)", static_cast<long long>(blocks),
@@ -804,19 +815,16 @@ int launch_entropy(hjd_gdec* g, const EntBatchDev& b, hipStream_t s)
     return HJD_OK;
 }
 
-// Stage n JPEGs, upload, run the entropy kernels; optionally the pixel kernel.
-int gdec_run(hjd_gdec* g, const uint8_t* const* datas, const size_t* sizes, int n, void* const* d_outs,
-             const int32_t* pitches, int16_t* coefs_out, int64_t* block_offsets, hipStream_t s)
+// Upload the staged frames and run the entropy kernels (+ the pixel kernel
+// when d_outs is given) on stream s.
+int gdec_issue(hjd_gdec* g, void* const* d_outs, const int32_t* pitches, int16_t* coefs_out, int64_t* block_offsets,
+               hipStream_t s)
 {
-    if (!g || !g->gpu || !datas || !sizes) return set_error(HJD_E_INVALID, "NULL argument");
-    int rc = g->wait_staging();
-    if (rc) return rc;
-    rc = g->stage_frames(datas, sizes, n);
-    if (rc) return rc;
     HJD_HIP(hipSetDevice(g->device));
+    const int n = static_cast<int>(g->frames.size());
     int16_t* coefs = coefs_out ? coefs_out : g->d_coefs;
     EntBatchDev b;
-    rc = g->assemble(g->d_blob, coefs, block_offsets, d_outs, pitches, b);
+    int rc = g->assemble(g->d_blob, coefs, block_offsets, d_outs, pitches, b);
     if (rc) return rc;
     b.entries = g->d_entries;
     b.stats = g->d_stats;
@@ -847,6 +855,18 @@ int gdec_run(hjd_gdec* g, const uint8_t* const* datas, const size_t* sizes, int 
     HJD_HIP(hipEventRecord(g->done, s));
     g->nframes_issued = n;
     return HJD_OK;
+}
+
+// Stage n JPEGs on the calling thread, then issue.
+int gdec_run(hjd_gdec* g, const uint8_t* const* datas, const size_t* sizes, int n, void* const* d_outs,
+             const int32_t* pitches, int16_t* coefs_out, int64_t* block_offsets, hipStream_t s)
+{
+    if (!g || !g->gpu || !datas || !sizes) return set_error(HJD_E_INVALID, "NULL argument");
+    int rc = g->wait_staging();
+    if (rc) return rc;
+    rc = g->stage_frames(datas, sizes, n);
+    if (rc) return rc;
+    return gdec_issue(g, d_outs, pitches, coefs_out, block_offsets, s);
 }
 
 }  // namespace
@@ -1022,6 +1042,298 @@ int hjd_debug_entropy_emulate(const uint8_t* data, size_t size, int sub_bits, in
     emulate(b);
     if (status) *status = static_cast<int32_t>(g.e_status[0]);
     if (g.e_status[0] & ~kStatusFallback) return set_error(HJD_E_INVALID, "corrupt entropy data (status %u)", g.e_status[0]);
+    return HJD_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// GPU-entropy stream: submit JPEGs one by one; worker threads parse and
+// destuff them into the pinned staging of the open batch (nslots batches
+// rotate, each on its own HIP stream, so one batch's upload overlaps another's
+// kernels); the thread that completes a closed batch issues it.
+// ---------------------------------------------------------------------------
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
+#include <thread>
+
+namespace {
+
+struct GBatch {
+    int slot = 0;
+    int nframes = 0;
+    size_t bytes = 0;
+    int64_t blocks = 0;
+    int prepared = 0;
+    bool closed = false;
+    bool issued = false;
+    std::vector<void*> outs;
+    std::vector<int32_t> pitches;
+};
+
+struct GJob {
+    GBatch* batch;
+    int index;
+    const uint8_t* data;
+    size_t size;
+    size_t data_off;
+    size_t cap;
+};
+
+}  // namespace
+
+struct hjd_gstream {
+    hjd_ctx* ctx = nullptr;
+    int device = 0;
+    std::vector<hjd_gdec*> slots;
+    std::vector<hipStream_t> streams;
+    std::vector<GBatch*> slot_batch;   // batch currently owning each slot (nullptr = free)
+    int next_slot = 0;
+    GBatch* open = nullptr;
+
+    std::mutex mu;
+    std::condition_variable cv_jobs, cv_state;
+    std::deque<GJob> queue;
+    bool stop = false;
+    std::vector<std::thread> workers;
+    int64_t batches_in_flight = 0;     // created and not yet issued
+
+    std::atomic<int64_t> images{0}, pixels{0}, prep_ns{0}, h2d_bytes{0}, batches{0};
+    int first_error = HJD_OK;
+    std::string first_error_msg;
+
+    void record_error(int rc, const std::string& msg)
+    {
+        if (first_error == HJD_OK) {
+            first_error = rc;
+            first_error_msg = msg;
+        }
+    }
+    int open_batch(std::unique_lock<std::mutex>& lk);
+    void issue_locked(GBatch* b);
+    void worker();
+};
+
+// Caller holds mu.  Waits for the next slot's previous batch to be issued and
+// its uploads to finish before reusing the slot's pinned staging.
+int hjd_gstream::open_batch(std::unique_lock<std::mutex>& lk)
+{
+    const int s = next_slot;
+    next_slot = (next_slot + 1) % static_cast<int>(slots.size());
+    cv_state.wait(lk, [&] { return !slot_batch[s] || slot_batch[s]->issued; });
+    if (slot_batch[s]) {
+        delete slot_batch[s];
+        slot_batch[s] = nullptr;
+        hjd_gdec* g = slots[s];
+        if (g->pending) {
+            lk.unlock();
+            const hipError_t e = hipEventSynchronize(g->staged);
+            lk.lock();
+            if (e != hipSuccess) return set_error(HJD_E_HIP, "hipEventSynchronize: %s", hipGetErrorString(e));
+        }
+        // statuses of the slot's previous batch
+        if (g->pending) {
+            lk.unlock();
+            const int rc = hjd_gdec_sync(g, nullptr);
+            const std::string msg = rc ? hjd_last_error() : "";
+            lk.lock();
+            if (rc) record_error(rc, msg);
+        }
+    }
+    GBatch* b = new GBatch;
+    b->slot = s;
+    slot_batch[s] = b;
+    open = b;
+    ++batches_in_flight;
+    return HJD_OK;
+}
+
+// Caller holds mu; b is closed and fully prepared.
+void hjd_gstream::issue_locked(GBatch* b)
+{
+    if (b->issued) return;
+    hjd_gdec* g = slots[b->slot];
+    // drop frames whose preparation failed (already recorded)
+    std::vector<void*> outs;
+    std::vector<int32_t> pitches;
+    std::vector<Prepared> keep;
+    size_t used = 0;
+    for (int i = 0; i < b->nframes; ++i) {
+        Prepared& p = g->frames[i];
+        if (p.rc != HJD_OK) continue;
+        used = std::max(used, align_up(p.data_off + p.data_bits / 8 + kDataPad, 16));
+        images++;
+        pixels += static_cast<int64_t>(p.width) * p.height;
+        keep.push_back(std::move(p));
+        outs.push_back(b->outs[i]);
+        pitches.push_back(b->pitches[i]);
+    }
+    g->frames.swap(keep);
+    g->data_used = used;
+    if (!g->frames.empty()) {
+        const int rc = gdec_issue(g, outs.data(), pitches.data(), nullptr, nullptr, streams[b->slot]);
+        if (rc) record_error(rc, hjd_last_error());
+        h2d_bytes += static_cast<int64_t>(g->H.used + g->data_used);
+        batches++;
+    }
+    b->issued = true;
+    --batches_in_flight;
+    cv_state.notify_all();
+}
+
+void hjd_gstream::worker()
+{
+    (void)hipSetDevice(device);
+    for (;;) {
+        GJob job;
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv_jobs.wait(lk, [&] { return stop || !queue.empty(); });
+            if (queue.empty()) return;
+            job = queue.front();
+            queue.pop_front();
+        }
+        hjd_gdec* g = slots[job.batch->slot];
+        const auto t0 = std::chrono::steady_clock::now();
+        const int rc = g->prepare_frame(job.index, job.data, job.size, job.data_off, job.cap);
+        prep_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+        const std::string msg = rc ? hjd_last_error() : "";
+        std::unique_lock<std::mutex> lk(mu);
+        if (rc) record_error(rc, msg);
+        GBatch* b = job.batch;
+        ++b->prepared;
+        if (b->closed && b->prepared == b->nframes) issue_locked(b);
+        cv_state.notify_all();
+    }
+}
+
+extern "C" {
+
+int hjd_gstream_create(hjd_ctx* ctx, int max_frames, int64_t max_scan_bytes, int64_t max_blocks, int nslots,
+                       int nthreads, hjd_gstream** out)
+{
+    if (!ctx || !out || nslots < 2 || nslots > 8) return set_error(HJD_E_INVALID, "invalid gstream arguments (nslots 2..8)");
+    *out = nullptr;
+    if (nthreads <= 0) nthreads = static_cast<int>(std::max(1u, std::thread::hardware_concurrency()));
+    hjd_gstream* st = new (std::nothrow) hjd_gstream;
+    if (!st) return set_error(HJD_E_NOMEM, "gstream allocation");
+    st->ctx = ctx;
+    st->device = hjd_ctx_device(ctx);
+    st->slots.assign(nslots, nullptr);
+    st->streams.assign(nslots, nullptr);
+    st->slot_batch.assign(nslots, nullptr);
+    for (int s = 0; s < nslots; ++s) {
+        int rc = hjd_gdec_create(ctx, max_frames, max_scan_bytes, max_blocks, 0, &st->slots[s]);
+        if (rc == HJD_OK && hipStreamCreateWithFlags(&st->streams[s], hipStreamNonBlocking) != hipSuccess)
+            rc = set_error(HJD_E_HIP, "hipStreamCreate");
+        if (rc) {
+            hjd_gstream_destroy(st);
+            return rc;
+        }
+    }
+    for (int t = 0; t < nthreads; ++t) st->workers.emplace_back([st] { st->worker(); });
+    *out = st;
+    return HJD_OK;
+}
+
+int hjd_gstream_submit(hjd_gstream* st, const uint8_t* data, size_t size, void* d_out, int32_t out_pitch)
+{
+    if (!st || !data || !d_out || out_pitch <= 0 || (out_pitch & 3) || (reinterpret_cast<uintptr_t>(d_out) & 15))
+        return set_error(HJD_E_INVALID, "invalid submit arguments (d_out must be 16-byte aligned)");
+    hjd_internal::ScanHeader h;
+    int rc = hjd_internal::parse_scan_header(data, size, &h);
+    if (rc) return rc;
+    if (out_pitch < 4 * h.width) return set_error(HJD_E_INVALID, "output pitch too small");
+    const size_t need = align_up(size + kDataPad, 16);
+    std::unique_lock<std::mutex> lk(st->mu);
+    hjd_gdec* g0 = st->slots[0];
+    if (need > g0->data_cap() || h.nblocks > g0->caps.max_blocks)
+        return set_error(HJD_E_INVALID, "JPEG larger than one batch's capacity");
+    if (st->open) {
+        GBatch* b = st->open;
+        hjd_gdec* g = st->slots[b->slot];
+        if (b->nframes == g->caps.max_frames || b->bytes + need > g->data_cap() || b->blocks + h.nblocks > g->caps.max_blocks) {
+            b->closed = true;
+            st->open = nullptr;
+            if (b->prepared == b->nframes) st->issue_locked(b);
+        }
+    }
+    if (!st->open) {
+        rc = st->open_batch(lk);
+        if (rc) return rc;
+    }
+    GBatch* b = st->open;
+    hjd_gdec* g = st->slots[b->slot];
+    if (b->nframes == 0) g->frames.assign(static_cast<size_t>(g->caps.max_frames), Prepared());
+    GJob job{b, b->nframes, data, size, b->bytes, need};
+    b->outs.push_back(d_out);
+    b->pitches.push_back(out_pitch);
+    b->nframes++;
+    b->bytes += need;
+    b->blocks += h.nblocks;
+    st->queue.push_back(job);
+    lk.unlock();
+    st->cv_jobs.notify_one();
+    return HJD_OK;
+}
+
+int hjd_gstream_sync(hjd_gstream* st, int64_t stats[5])
+{
+    if (!st) return set_error(HJD_E_INVALID, "gstream is NULL");
+    {
+        std::unique_lock<std::mutex> lk(st->mu);
+        if (st->open) {
+            GBatch* b = st->open;
+            b->closed = true;
+            st->open = nullptr;
+            if (b->prepared == b->nframes) st->issue_locked(b);
+        }
+        st->cv_state.wait(lk, [&] { return st->batches_in_flight == 0; });
+    }
+    for (size_t s = 0; s < st->slots.size(); ++s) {
+        hjd_gdec* g = st->slots[s];
+        if (!g->pending) continue;
+        const int rc = hjd_gdec_sync(g, nullptr);
+        if (rc) {
+            std::lock_guard<std::mutex> lk(st->mu);
+            st->record_error(rc, hjd_last_error());
+        }
+    }
+    if (stats) {
+        stats[0] = st->images;
+        stats[1] = st->pixels;
+        stats[2] = st->prep_ns;
+        stats[3] = st->h2d_bytes;
+        stats[4] = st->batches;
+    }
+    std::lock_guard<std::mutex> lk(st->mu);
+    if (st->first_error != HJD_OK) {
+        const int rc = st->first_error;
+        st->first_error = HJD_OK;
+        return set_error(rc, "%s", st->first_error_msg.c_str());
+    }
+    return HJD_OK;
+}
+
+int hjd_gstream_destroy(hjd_gstream* st)
+{
+    if (!st) return HJD_OK;
+    (void)hjd_gstream_sync(st, nullptr);
+    {
+        std::lock_guard<std::mutex> lk(st->mu);
+        st->stop = true;
+    }
+    st->cv_jobs.notify_all();
+    for (auto& t : st->workers) t.join();
+    for (size_t s = 0; s < st->slots.size(); ++s) {
+        delete st->slot_batch[s];
+        if (st->slots[s]) hjd_gdec_destroy(st->slots[s]);
+        if (st->streams[s]) (void)hipStreamDestroy(st->streams[s]);
+    }
+    delete st;
     return HJD_OK;
 }
 

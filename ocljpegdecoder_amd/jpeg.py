@@ -7,6 +7,8 @@
         st.submit(data, out_tensor); st.sync()
     gd = GpuDecoder(ctx, max_frames, max_scan_bytes, max_blocks)   # Huffman decode ON the GPU
         gd.decode([data, ...], [out_tensor, ...]); gd.sync()
+    with GpuJpegStream(ctx, 32, 32 << 22, 32 * 194400) as st:      # destuff workers || H2D || GPU Huffman + pixels
+        st.submit(data, out_tensor); st.sync()
 """
 from __future__ import annotations
 
@@ -218,6 +220,55 @@ class GpuDecoder:
     def close(self):
         if self.handle:
             self.lib.hjd_gdec_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class GpuJpegStream:
+    """hjd_gstream: worker threads parse/destuff JPEGs into pinned batches;
+    each batch is Huffman-decoded and converted to BGRX on the GPU."""
+
+    def __init__(self, ctx, max_frames: int, max_scan_bytes: int, max_blocks: int, nslots: int = 3,
+                 nthreads: int = 0):
+        self.lib = _lib.load()
+        self.ctx = ctx
+        h = ctypes.c_void_p()
+        check(self.lib.hjd_gstream_create(ctx.handle, int(max_frames), int(max_scan_bytes), int(max_blocks),
+                                          int(nslots), int(nthreads), ctypes.byref(h)), "hjd_gstream_create")
+        self.handle = h
+        self._keep = []
+
+    def submit(self, data: bytes, out, out_pitch: Optional[int] = None):
+        buf = _buf(data) if not isinstance(data, ctypes.Array) else data
+        self._keep.append(buf)
+        if not (out.is_cuda and out.is_contiguous()):
+            raise ValueError("out must be a contiguous device tensor")
+        out_pitch = out_pitch or out.shape[-1] * out.element_size()
+        check(self.lib.hjd_gstream_submit(self.handle, ctypes.cast(buf, _u8p), len(buf), out.data_ptr(),
+                                          int(out_pitch)), "hjd_gstream_submit")
+
+    def sync(self) -> dict:
+        stats = (ctypes.c_int64 * 5)()
+        rc = self.lib.hjd_gstream_sync(self.handle, stats)
+        self._keep.clear()
+        check(rc, "hjd_gstream_sync")
+        return {"images": stats[0], "pixels": stats[1], "host_prep_ns": stats[2], "h2d_bytes": stats[3],
+                "batches": stats[4]}
+
+    def close(self):
+        if self.handle:
+            self.lib.hjd_gstream_destroy(self.handle)
             self.handle = None
 
     def __enter__(self):

@@ -153,3 +153,57 @@ def test_capacity_errors(hjd, ctx):
     with hjd.GpuDecoder(ctx, 2, len(d) // 2, 2 * info.nblocks) as gd:
         with pytest.raises(hjd._lib.HjdError):
             gd.decode_coefs([d], coefs)              # too many scan bytes
+
+
+@pytest.mark.parametrize("max_frames,nslots,nthreads", [(3, 2, 1), (5, 3, 4), (16, 4, 16)])
+def test_gstream_many_images(hjd, ctx, max_frames, nslots, nthreads):
+    """GPU-entropy stream: many files of mixed geometry through rotating batches;
+    pixels equal the reference's (golden) or the oracle on the host-decoded
+    coefficients."""
+    import torch
+    files = []
+    for name, d in _golden_bytes():
+        files.append((d, O.load_case(name)["bgrx"]))
+    rng = np.random.default_rng(max_frames * 13 + nslots)
+    for i in range(14):
+        w, h = int(rng.integers(1, 900)), int(rng.integers(1, 400))
+        kw = {"restart_marker_blocks": int(rng.integers(1, 9))} if i % 3 == 0 else {}
+        d = _pil(w, h, int(rng.integers(30, 100)), int(rng.choice([0, 2])), seed=i, **kw)
+        coefs, info = hjd.decode_coefs(d)
+        files.append((d, O.decode_q16(coefs, info.qt, info.width, info.height, info.sampling)))
+    files = files * 2
+    infos = [hjd.parse(d) for d, _ in files]
+    cap_bytes = max(len(d) for d, _ in files) * max_frames + (1 << 16)
+    cap_blocks = max(i.nblocks for i in infos) * max_frames
+    outs = [torch.full(e.shape, -1, dtype=torch.int32, device="cuda") for _, e in files]
+    with hjd.GpuJpegStream(ctx, max_frames, cap_bytes, cap_blocks, nslots=nslots, nthreads=nthreads) as st:
+        for (d, _), o in zip(files, outs):
+            st.submit(d, o)
+        stats = st.sync()
+        # the stream stays usable after a sync
+        st.submit(files[0][0], outs[0])
+        st.sync()
+    assert stats["images"] == len(files)
+    assert stats["batches"] >= -(-len(files) // max_frames)
+    for (d, e), o in zip(files, outs):
+        np.testing.assert_array_equal(o.cpu().numpy().view(np.uint32), e)
+
+
+def test_gstream_bad_file_reported(hjd, ctx):
+    import torch
+    good = _pil(200, 100, 90, 2, seed=5)
+    info = hjd.parse(good)
+    cut = good[: info.scan_offset + 200] + b"\xff\xd9"
+    outs = [torch.zeros((100, 200), dtype=torch.int32, device="cuda") for _ in range(3)]
+    with hjd.GpuJpegStream(ctx, 4, 4 * len(good), 4 * info.nblocks, nslots=2, nthreads=2) as st:
+        st.submit(good, outs[0])
+        st.submit(cut, outs[1])
+        st.submit(good, outs[2])
+        with pytest.raises(hjd._lib.HjdError):
+            st.sync()
+        st.submit(good, outs[1])     # usable again
+        st.sync()
+    coefs, _ = hjd.decode_coefs(good)
+    exp = O.decode_q16(coefs, info.qt, info.width, info.height, info.sampling)
+    for o in outs:
+        np.testing.assert_array_equal(o.cpu().numpy().view(np.uint32), exp)
