@@ -221,9 +221,13 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
         st = hjd.JpegStream(ctx, max_blocks, nslots=nthreads + 4, nthreads=nthreads)
         stat_key = "host_decode_ns"
 
+    # ctypes views of the pool made once: submit() then passes pointers (no per-call copy)
+    from ocljpegdecoder_amd.jpeg import _buf
+    pool_c = [_buf(d) for d in pool]
+
     def step():
         for i in range(nf):
-            st.submit(pool[i % len(pool)], outs[i])
+            st.submit(pool_c[i % len(pool_c)], outs[i])
         return st.sync()
 
     for _ in range(args.warmup):
