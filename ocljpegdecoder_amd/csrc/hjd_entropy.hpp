@@ -202,22 +202,18 @@ __host__ __device__ __forceinline__ void copy_block(int16_t* dst, const int16_t*
     for (int q = 0; q < 8; ++q) d[q] = s[q];
 }
 
-// Big-endian words of the frame's bit string, read 16 B at a time.
+// Raw (little-endian) 16-B chunk of the frame's bit string.
 __host__ __device__ __forceinline__ u32x4 load_chunk(const RunCtx& c, uint32_t ci)
 {
-    u32x4 v = reinterpret_cast<const u32x4*>(c.data)[ci];
-    v.x = bswap32(v.x);
-    v.y = bswap32(v.y);
-    v.z = bswap32(v.z);
-    v.w = bswap32(v.w);
-    return v;
+    return reinterpret_cast<const u32x4*>(c.data)[ci];
 }
 
-// Per-lane bit window: w0:w1 are the words under the read position; q holds
-// the following words and r the next 16-B chunk, already in flight -- about 18
-// symbols of lead, enough to hide an HBM miss (each lane streams its own lines,
-// so every line crossing misses the caches).  Only fixed register moves, no
-// indexed registers.
+// Per-lane bit window: w0:w1 are the (byte-swapped) words under the read
+// position; q holds the following words and r the next raw 16-B chunk, still
+// in flight -- about 18 symbols of lead, enough to hide an HBM miss (each lane
+// streams its own lines, so every line crossing misses the caches).  r is only
+// consumed (swapped into q) four word-advances after its load is issued, so
+// the wait lands there; only fixed register moves, no indexed registers.
 struct BitWindow {
     uint32_t w0, w1, q0, q1, q2, q3, q4, q5;
     u32x4 r;
@@ -234,10 +230,10 @@ struct BitWindow {
         q4 = q5;
         ++wi;
         if (--nq == 0) {
-            q0 = r.x;
-            q1 = r.y;
-            q2 = r.z;
-            q3 = r.w;
+            q0 = bswap32(r.x);
+            q1 = bswap32(r.y);
+            q2 = bswap32(r.z);
+            q3 = bswap32(r.w);
             nq = 4;
             r = load_chunk(c, next++);
         }
@@ -249,14 +245,14 @@ struct BitWindow {
         const u32x4 a = load_chunk(c, ci), b = load_chunk(c, ci + 1);
         r = load_chunk(c, ci + 2);
         next = ci + 3;
-        w0 = a.x;
-        w1 = a.y;
-        q0 = a.z;
-        q1 = a.w;
-        q2 = b.x;
-        q3 = b.y;
-        q4 = b.z;
-        q5 = b.w;
+        w0 = bswap32(a.x);
+        w1 = bswap32(a.y);
+        q0 = bswap32(a.z);
+        q1 = bswap32(a.w);
+        q2 = bswap32(b.x);
+        q3 = bswap32(b.y);
+        q4 = bswap32(b.z);
+        q5 = bswap32(b.w);
         nq = 6;
         wi = ci * 4;
         for (uint32_t i = 0; i < (word & 3); ++i) advance(c);
@@ -303,6 +299,7 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
             p0 = p1 = p2 = 0;
         }
         uint32_t seg_end = c.seg_end[seg];
+        if (seg_end < pos) flags |= kError;   // consumed before the window loads are issued
         BitWindow bw;
         bw.seek(c, pos >> 5);
         bool owned = false;                            // write mode: current block started in this run
@@ -339,6 +336,9 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
                         done = true;
                     } else {
                         seg_end = c.seg_end[seg];
+                        // consume the load inside this rare branch, so the loop
+                        // head does not wait for every outstanding memory op
+                        if (seg_end < pos) flags |= kError;
                     }
                     continue;
                 }
