@@ -47,7 +47,7 @@ WORKLOADS = {
                   desc="BASELINE configs[3]: batch of 1024 synthetic 3840x2160 4:4:4 frames, persistent kernel"),
     "fhd420": dict(width=1920, height=1080, sampling=1, frames=1,
                    desc="BASELINE configs[1]: single 1920x1080 4:2:0 frame, one launch (cache/launch bound)"),
-    "stream4k420": dict(width=3840, height=2160, sampling=1, frames=512, entropy="gpu",
+    "stream4k420": dict(width=3840, height=2160, sampling=1, frames=1024, entropy="gpu",
                         desc="BASELINE configs[4] per GPU: stream of 4K 4:2:0 JPEGs (pool of 16 distinct q90 "
                              "files); host parse+destuff workers || pinned H2D || GPU Huffman decode + fused kernel"),
     "stream4k420_host": dict(width=3840, height=2160, sampling=1, frames=128, entropy="host",
@@ -214,8 +214,9 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
     gpu_entropy = wl.get("entropy") == "gpu"
     if gpu_entropy:
         per_batch = int(os.environ.get("HJD_STREAM_BATCH", 64))
+        nslots = int(os.environ.get("HJD_STREAM_SLOTS", 5))
         st = hjd.GpuJpegStream(ctx, per_batch, per_batch * max(len(d) for d in pool) + (1 << 20),
-                               per_batch * max_blocks, nslots=3, nthreads=nthreads)
+                               per_batch * max_blocks, nslots=nslots, nthreads=nthreads)
         stat_key = "host_prep_ns"
     else:
         st = hjd.JpegStream(ctx, max_blocks, nslots=nthreads + 4, nthreads=nthreads)
