@@ -213,8 +213,8 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
     outs = [torch.empty((h, w), dtype=torch.int32, device=dev) for _ in range(nf)]
     gpu_entropy = wl.get("entropy") == "gpu"
     if gpu_entropy:
-        per_batch = int(os.environ.get("HJD_STREAM_BATCH", 64))
-        nslots = int(os.environ.get("HJD_STREAM_SLOTS", 5))
+        per_batch = int(os.environ.get("HJD_STREAM_BATCH", 32))
+        nslots = int(os.environ.get("HJD_STREAM_SLOTS", 6))
         st = hjd.GpuJpegStream(ctx, per_batch, per_batch * max(len(d) for d in pool) + (1 << 20),
                                per_batch * max_blocks, nslots=nslots, nthreads=nthreads)
         stat_key = "host_prep_ns"
