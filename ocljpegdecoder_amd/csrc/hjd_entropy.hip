@@ -237,7 +237,7 @@ struct EntBatchDev {
     SubStats* agg;
     uint32_t* status;
     int16_t* coefs;
-    uint32_t nframes, nwg, sub_bits, pad;
+    uint32_t nframes, nwg, sub_bits, ntab_max;   // ntab_max: tables of the largest frame (dynamic LDS)
 };
 
 __host__ __device__ __forceinline__ RunCtx make_ctx(const EntBatchDev& b, const EntFrame& F, const HuffLut* tabs)
@@ -308,11 +308,34 @@ __device__ __forceinline__ SubStats block_scan_inclusive(SubStats v, SubStats* b
     return v;
 }
 
+// Ordered reduction over one wave's lanes (lane order = subsequence order);
+// the result is valid in lane 0.
+__device__ __forceinline__ SubStats wave_reduce_ordered(SubStats v, int lane)
+{
+    for (int d = 1; d < 64; d <<= 1) {
+        const SubStats o = shfl_down_stats(v, d);
+        if ((lane & (2 * d - 1)) == 0) v = stats_combine(v, o);
+    }
+    return v;
+}
+
+// LDS layout of the sync kernel after the group's tables (dynamic shared memory).
+struct SyncLds {
+    uint64_t x[kGroupSubs];      // current exit of each subsequence
+    uint64_t used[kGroupSubs];   // entry each subsequence was last run from
+    SubStats st[kGroupSubs];     // statistics of that run
+    uint16_t list[2][kGroupSubs];
+    int32_t nlist[2];
+    SubStats wsum[kGroupSubs / 64];
+};
+
+__host__ __device__ constexpr size_t sync_lds_bytes(uint32_t ntab) { return sizeof(HuffLut) * ntab + sizeof(SyncLds); }
+
 __global__ __launch_bounds__(kGroupSubs) void ent_sync_kernel(EntBatchDev b)
 {
-    __shared__ HuffLut tabs[kMaxTables];
-    __shared__ uint64_t xs[2][kGroupSubs];
-    __shared__ SubStats buf[kGroupSubs];
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    HuffLut* tabs = reinterpret_cast<HuffLut*>(smem);
+    SyncLds& L = *reinterpret_cast<SyncLds*>(smem + sizeof(HuffLut) * b.ntab_max);
     const int tid = threadIdx.x;
     const uint32_t w = blockIdx.x;
     const uint32_t f = b.wg_frame[w];
@@ -321,42 +344,84 @@ __global__ __launch_bounds__(kGroupSubs) void ent_sync_kernel(EntBatchDev b)
     const uint32_t S = b.sub_bits;
     const RunCtx c = make_ctx(b, F, tabs);
     load_tables(tabs, b.tabs + F.tab_base, F.ntab, tid, kGroupSubs);
+    if (tid < 2) L.nlist[tid] = 0;
     __syncthreads();
-    const int64_t k = group_sub(gl, tid);
+    const int64_t k0 = group_sub(gl, 0);
+    const int64_t k = k0 + tid;
     const bool valid = k >= 0 && k < static_cast<int64_t>(F.nsub);
-    const bool has_pred = valid && tid > 0 && k > 0;
     const uint32_t ku = static_cast<uint32_t>(k);
-    const uint32_t stop = (ku + 1) * S;
+    // phase 1: every subsequence from its guessed entry
     uint64_t used = valid ? guess_entry(c, ku * S) : 0;
     SubStats st = stats_identity();
-    uint64_t x = valid ? run<false>(c, used, stop, st, nullptr) : used;
-    xs[0][tid] = x;
+    uint64_t x = valid ? run<false>(c, used, (ku + 1) * S, st, nullptr) : used;
+    L.x[tid] = x;
     __syncthreads();
-    for (int r = 0;; ++r) {
-        int changed = 0;
-        if (has_pred) {
-            const uint64_t e = xs[r & 1][tid - 1];
-            if (!same_state(e, used)) {
-                SubStats s2 = stats_identity();
-                const uint64_t x2 = run<false>(c, e, stop, s2, nullptr);
-                changed = !same_state(x2, x);
-                used = e;
-                st = s2;
-                x = x2;
+    // round 0: every subsequence from its predecessor's exit (all lanes busy)
+    bool changed = false;
+    if (valid && tid > 0 && k > 0) {
+        const uint64_t e = L.x[tid - 1];
+        if (!same_state(e, used)) {
+            SubStats s2 = stats_identity();
+            const uint64_t x2 = run<false>(c, e, (ku + 1) * S, s2, nullptr);
+            changed = !same_state(x2, x);
+            used = e;
+            st = s2;
+            x = x2;
+        }
+    }
+    L.used[tid] = used;
+    L.st[tid] = st;
+    __syncthreads();   // everyone has read L.x (old) before it is overwritten
+    L.x[tid] = x;
+    if (changed && tid + 1 < kGroupSubs && k + 1 < static_cast<int64_t>(F.nsub))
+        L.list[0][atomicAdd(&L.nlist[0], 1)] = static_cast<uint16_t>(tid + 1);
+    __syncthreads();
+    // later rounds: only the subsequences whose entry changed, compacted onto the
+    // first lanes, so idle waves do not replay a full decode
+    for (int r = 0;; r ^= 1) {
+        const int n = L.nlist[r];
+        if (n == 0) break;
+        uint64_t x2 = 0, e = 0;
+        SubStats s2 = stats_identity();
+        int item = -1;
+        if (tid < n) {
+            item = L.list[r][tid];
+            e = L.x[item - 1];
+            const uint32_t kk = static_cast<uint32_t>(k0 + item);
+            if (!same_state(e, L.used[item])) x2 = run<false>(c, e, (kk + 1) * S, s2, nullptr);
+            else item = -1;
+        }
+        if (tid == 0) L.nlist[r ^ 1] = 0;
+        __syncthreads();   // all reads of L.x done; the next list is empty
+        if (item >= 0) {
+            L.used[item] = e;
+            L.st[item] = s2;
+            if (!same_state(x2, L.x[item])) {
+                L.x[item] = x2;
+                if (item + 1 < kGroupSubs && k0 + item + 1 < static_cast<int64_t>(F.nsub))
+                    L.list[r ^ 1][atomicAdd(&L.nlist[r ^ 1], 1)] = static_cast<uint16_t>(item + 1);
             }
         }
-        xs[(r + 1) & 1][tid] = x;
-        if (!__syncthreads_or(changed)) break;
+        __syncthreads();
     }
     const bool own = valid && tid >= kWarm;
+    used = L.used[tid];
+    st = L.st[tid];
     if (own) {
         b.entries[F.sub_base + ku] = used;
         b.stats[F.sub_base + ku] = st;
     } else if (tid < kWarm) {
         b.wentries[static_cast<uint64_t>(w) * kWarm + tid] = used;   // 0 for invalid (frame start group)
     }
-    const SubStats total = block_scan_inclusive(own ? st : stats_identity(), buf, tid);
-    if (tid == kGroupSubs - 1) b.agg[w] = total;
+    // statistics of the owned range: ordered reduce per wave, then across waves
+    const SubStats ws = wave_reduce_ordered(own ? st : stats_identity(), tid & 63);
+    if ((tid & 63) == 0) L.wsum[tid >> 6] = ws;
+    __syncthreads();
+    if (tid == 0) {
+        SubStats a = L.wsum[0];
+        for (int i = 1; i < kGroupSubs / 64; ++i) a = stats_combine(a, L.wsum[i]);
+        b.agg[w] = a;
+    }
 }
 
 __global__ __launch_bounds__(256) void ent_link_kernel(EntBatchDev b)
@@ -434,8 +499,9 @@ __global__ __launch_bounds__(64) void ent_fallback_kernel(EntBatchDev b)
 
 __global__ __launch_bounds__(kGroupSubs) void ent_write_kernel(EntBatchDev b)
 {
-    __shared__ HuffLut tabs[kMaxTables];
-    __shared__ __attribute__((aligned(16))) int16_t stage[kGroupSubs * kStageStride];
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    int16_t* stage = reinterpret_cast<int16_t*>(smem);                                  // [256][kStageStride]
+    HuffLut* tabs = reinterpret_cast<HuffLut*>(smem + sizeof(int16_t) * kGroupSubs * kStageStride);
     SubStats* buf = reinterpret_cast<SubStats*>(stage);   // scan scratch before any block is staged
     static_assert(sizeof(SubStats) * kGroupSubs <= sizeof(int16_t) * kGroupSubs * kStageStride, "scratch");
     const int tid = threadIdx.x;
@@ -768,7 +834,8 @@ int hjd_gdec::assemble(uint8_t* blob, int16_t* coefs, int64_t* block_offsets, vo
     d.nframes = static_cast<uint32_t>(n);
     d.nwg = wg_base;
     d.sub_bits = S;
-    d.pad = 0;
+    d.ntab_max = 1;
+    for (const Prepared& p : frames) d.ntab_max = std::max<uint32_t>(d.ntab_max, static_cast<uint32_t>(p.ntab));
     return HJD_OK;
 }
 
@@ -804,13 +871,14 @@ int launch_entropy(hjd_gdec* g, const EntBatchDev& b, hipStream_t s)
 {
     if (b.nwg == 0) return HJD_OK;
     HJD_HIP(hipMemsetAsync(g->d_status, 0, 4 * static_cast<size_t>(b.nframes), s));
-    hipLaunchKernelGGL(ent_sync_kernel, dim3(b.nwg), dim3(kGroupSubs), 0, s, b);
+    hipLaunchKernelGGL(ent_sync_kernel, dim3(b.nwg), dim3(kGroupSubs), sync_lds_bytes(b.ntab_max), s, b);
     HJD_HIP(hipGetLastError());
     hipLaunchKernelGGL(ent_link_kernel, dim3((b.nwg + 255) / 256), dim3(256), 0, s, b);
     HJD_HIP(hipGetLastError());
     hipLaunchKernelGGL(ent_fallback_kernel, dim3(b.nframes), dim3(64), 0, s, b);
     HJD_HIP(hipGetLastError());
-    hipLaunchKernelGGL(ent_write_kernel, dim3(b.nwg), dim3(kGroupSubs), 0, s, b);
+    hipLaunchKernelGGL(ent_write_kernel, dim3(b.nwg), dim3(kGroupSubs),
+                       sizeof(int16_t) * kGroupSubs * kStageStride + sizeof(HuffLut) * b.ntab_max, s, b);
     HJD_HIP(hipGetLastError());
     return HJD_OK;
 }

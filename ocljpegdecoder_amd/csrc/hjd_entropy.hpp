@@ -353,19 +353,22 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
                 len = e >> 8;
                 sym = e & 0xFF;
             } else {
-                len = 16;
-                sym = 0;
-                bool found = false;
-                for (uint32_t l = kLutBits + 1; l <= 16; ++l) {
-                    const int32_t code = static_cast<int32_t>(peek >> (32 - l));
-                    if (code <= t.maxcode[l]) {
-                        len = l;
-                        sym = t.vals[(code + t.delta[l]) & 255];
-                        found = true;
-                        break;
-                    }
+                // Codes longer than the LUT (T.81 F.2.2.3): the length is the first
+                // l with code_l <= MAXCODE[l]; the six compares use independent
+                // loads and selects instead of a dependent loop.
+                static_assert(kLutBits == 10, "long-code lengths 11..16");
+                const int32_t c11 = static_cast<int32_t>(peek >> 21), c12 = static_cast<int32_t>(peek >> 20);
+                const int32_t c13 = static_cast<int32_t>(peek >> 19), c14 = static_cast<int32_t>(peek >> 18);
+                const int32_t c15 = static_cast<int32_t>(peek >> 17), c16 = static_cast<int32_t>(peek >> 16);
+                const bool p11 = c11 <= t.maxcode[11], p12 = c12 <= t.maxcode[12], p13 = c13 <= t.maxcode[13];
+                const bool p14 = c14 <= t.maxcode[14], p15 = c15 <= t.maxcode[15], p16 = c16 <= t.maxcode[16];
+                len = p11 ? 11u : p12 ? 12u : p13 ? 13u : p14 ? 14u : p15 ? 15u : 16u;
+                const int32_t code = static_cast<int32_t>(peek >> (32 - len));
+                sym = t.vals[(code + t.delta[len]) & 255];
+                if (!(p11 || p12 || p13 || p14 || p15 || p16)) {
+                    flags |= kError;   // consumes 16 bits as a zero symbol
+                    sym = 0;
                 }
-                if (!found) flags |= kError;   // consumes 16 bits as a zero symbol
             }
             const uint32_t s = sym & 15;
             const uint32_t r = dc ? 0 : sym >> 4;
