@@ -877,8 +877,9 @@ int launch_entropy(hjd_gdec* g, const EntBatchDev& b, hipStream_t s)
     HJD_HIP(hipGetLastError());
     hipLaunchKernelGGL(ent_fallback_kernel, dim3(b.nframes), dim3(64), 0, s, b);
     HJD_HIP(hipGetLastError());
-    hipLaunchKernelGGL(ent_write_kernel, dim3(b.nwg), dim3(kGroupSubs),
-                       sizeof(int16_t) * kGroupSubs * kStageStride + sizeof(HuffLut) * b.ntab_max, s, b);
+    constexpr size_t kStageBytes = sizeof(int16_t) * kGroupSubs * kStageStride;
+    hipLaunchKernelGGL(ent_write_kernel, dim3(b.nwg), dim3(kGroupSubs), kStageBytes + sizeof(HuffLut) * b.ntab_max, s,
+                       b);
     HJD_HIP(hipGetLastError());
     return HJD_OK;
 }

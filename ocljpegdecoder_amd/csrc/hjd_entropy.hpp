@@ -44,7 +44,7 @@ constexpr int kGroupSubs = 256;                 // subsequences per workgroup (o
 constexpr int kWarm = 8;                        // leading subsequences a group shares with its predecessor
 constexpr int kOwn = kGroupSubs - kWarm;        // subsequences a group is responsible for
 constexpr int kDefaultSubBits = 2048;           // S
-constexpr int kStageStride = 72;                // int16 per lane in the block staging buffer (144 B)
+constexpr int kStageStride = 24;                // int16 per lane in the staging buffer: one 16-coefficient quarter (+pad)
 
 // One Huffman table in device form (2448 B, 16-B multiple).
 struct HuffLut {
@@ -188,18 +188,33 @@ struct RunOut {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-__host__ __device__ __forceinline__ void zero_block(int16_t* stage)
+// Write-mode staging: only the quarter of the block being filled (16
+// coefficients, z order) lives in LDS; quarters are flushed with two 16-B
+// stores as z moves past them, so every block is still written exactly once
+// as 8 x 16 B, while the LDS per lane is 48 B instead of a whole block.
+__host__ __device__ __forceinline__ void zero_quarter(int16_t* stage)
 {
     u32x4* p = reinterpret_cast<u32x4*>(stage);
     const u32x4 zv = {0u, 0u, 0u, 0u};
-    for (int q = 0; q < 8; ++q) p[q] = zv;
+    p[0] = zv;
+    p[1] = zv;
 }
 
-__host__ __device__ __forceinline__ void copy_block(int16_t* dst, const int16_t* stage)
+// Store the staged quarter q to the block, zeros for quarters q+1 .. qn-1,
+// and clear the stage.
+__host__ __device__ __forceinline__ void flush_quarters(int16_t* blk, int16_t* stage, uint32_t q, uint32_t qn)
 {
-    const u32x4* s = reinterpret_cast<const u32x4*>(stage);
-    u32x4* d = reinterpret_cast<u32x4*>(dst);
-    for (int q = 0; q < 8; ++q) d[q] = s[q];
+    u32x4* d = reinterpret_cast<u32x4*>(blk);
+    u32x4* sp = reinterpret_cast<u32x4*>(stage);
+    d[2 * q] = sp[0];
+    d[2 * q + 1] = sp[1];
+    const u32x4 zv = {0u, 0u, 0u, 0u};
+    for (uint32_t i = q + 1; i < qn; ++i) {
+        d[2 * i] = zv;
+        d[2 * i + 1] = zv;
+    }
+    sp[0] = zv;
+    sp[1] = zv;
 }
 
 // Raw (little-endian) 16-B chunk of the frame's bit string.
@@ -304,6 +319,7 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
         bw.seek(c, pos >> 5);
         bool owned = false;                            // write mode: current block started in this run
         int16_t* cur = nullptr;                        // write mode: its destination (null: not written)
+        uint32_t quarter = 0;                          // write mode: quarter of the block being staged
         uint32_t ji = jinfo_of(c, j);
         result = 0;
         bool done = false;
@@ -397,8 +413,9 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
                     if (blk < out->nblocks) {
                         if (dst < out->nblocks && blk % static_cast<uint32_t>(c.bpm) == j) {
                             cur = out->coefs + static_cast<uint64_t>(dst) * 64;
-                            zero_block(out->stage);
+                            zero_quarter(out->stage);
                             out->stage[0] = static_cast<int16_t>(comp == 0 ? p0 : (comp == 1 ? p1 : p2));
+                            quarter = 0;
                         } else {
                             flags |= kError;   // a restart interval ended inside an MCU
                         }
@@ -413,13 +430,20 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
                     flags |= kError;
                     z = 64;
                 } else {
-                    if (kWrite && cur) out->stage[z] = static_cast<int16_t>(v);
+                    if (kWrite && cur) {
+                        const uint32_t qz = z >> 4;
+                        if (qz != quarter) {
+                            flush_quarters(cur, out->stage, quarter, qz);
+                            quarter = qz;
+                        }
+                        out->stage[z & 15] = static_cast<int16_t>(v);
+                    }
                     ++z;
                 }
             }
             if (z >= 64) {
                 if (kWrite && owned) {
-                    if (cur) copy_block(cur, out->stage);   // 8 x 16-B stores of the finished block
+                    if (cur) flush_quarters(cur, out->stage, quarter, 4);   // the rest of the block
                     blk += 1;
                     owned = false;
                     cur = nullptr;

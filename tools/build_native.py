@@ -50,16 +50,24 @@ def _headers():
     return hs
 
 
-def build(verbose: bool = False, force: bool = False, ablation: bool = False) -> str:
+def build(verbose: bool = False, force: bool = False, ablation: bool = False, variant: str = "",
+          defines=()) -> str:
     """ablation=True builds the TUNING-ONLY library build/ablation/libhjd.so with
     -DHJD_ABLATION (stage-skipping kernel variants for tools/tune.py; wrong
-    outputs by design).  Load it with HJD_LIB=build/ablation/libhjd.so."""
+    outputs by design).  Load it with HJD_LIB=build/ablation/libhjd.so.
+    variant="name", defines=("FLAG", ...) builds an A/B library
+    build/variants/<name>/libhjd.so with -DFLAG (tuning only)."""
     global LIBDIR, LIB, OBJDIR
     if ablation:
         LIBDIR = os.path.join(REPO, "build", "ablation")
         LIB = os.path.join(LIBDIR, "libhjd.so")
         OBJDIR = os.path.join(REPO, "build", "obj_ablation")
         COMMON.append("-DHJD_ABLATION")
+    elif variant:
+        LIBDIR = os.path.join(REPO, "build", "variants", variant)
+        LIB = os.path.join(LIBDIR, "libhjd.so")
+        OBJDIR = os.path.join(REPO, "build", "obj_variants", variant)
+        COMMON.extend(f"-D{d}" for d in defines)
     os.makedirs(LIBDIR, exist_ok=True)
     os.makedirs(OBJDIR, exist_ok=True)
     headers = _headers()
@@ -94,4 +102,9 @@ def build(verbose: bool = False, force: bool = False, ablation: bool = False) ->
 
 
 if __name__ == "__main__":
-    print(build(verbose=True, force="--force" in sys.argv, ablation="--ablation" in sys.argv))
+    var, defs = "", []
+    if "--variant" in sys.argv:
+        var = sys.argv[sys.argv.index("--variant") + 1]
+        defs = [a[2:] for a in sys.argv if a.startswith("-D")]
+    print(build(verbose=True, force="--force" in sys.argv, ablation="--ablation" in sys.argv, variant=var,
+                defines=defs))
