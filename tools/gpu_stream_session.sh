@@ -15,6 +15,7 @@ for C in $CFGS; do
   HJD_STREAM_BATCH=$B HJD_STREAM_SLOTS=$S timeout -k 10 600 python bench.py --workload stream4k420 --steps 3 --warmup 1 > $O/stream_b${B}_s${S}.json 2> $O/stream_b${B}_s${S}.err || { echo STREAM FAILED; tail -20 $O/stream_b${B}_s${S}.err; exit 1; }
   echo "batch $B slots $S: $(python3 -c "import json;d=json.load(open('$O/stream_b${B}_s${S}.json'));print(d['value'], d['ms_per_step'], d['end_to_end'])")"
 done
+timeout -k 10 120 python tools/h2d_bw.py | tee $O/h2d.json
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o stream -- python3 $R/bench.py --workload stream4k420 --steps 2 --warmup 1 > $O/kt.json 2> $O/kt.err || { echo PROF FAILED; tail $O/kt.err; exit 1; }
 python3 $R/tools/trace_busy.py $O/kt/stream_kernel_trace.csv
