@@ -50,6 +50,9 @@ WORKLOADS = {
     "stream4k420": dict(width=3840, height=2160, sampling=1, frames=1024, entropy="gpu",
                         desc="BASELINE configs[4] per GPU: stream of 4K 4:2:0 JPEGs (pool of 16 distinct q90 "
                              "files); host parse+destuff workers || pinned H2D || GPU Huffman decode + fused kernel"),
+    "stream4k420_d2h": dict(width=3840, height=2160, sampling=1, frames=256, entropy="gpu", d2h=True,
+                            desc="BASELINE configs[4] per GPU, D2H-on (SURVEY s8(e)): as stream4k420, and every "
+                                 "frame's BGRX copied back to pinned host memory"),
     "stream4k420_host": dict(width=3840, height=2160, sampling=1, frames=128, entropy="host",
                              desc="BASELINE configs[4] per GPU, host-Huffman variant: host Huffman workers || "
                                   "pinned H2D || fused kernel"),
@@ -210,11 +213,17 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
     infos = [hjd.parse(d) for d in pool]
     max_blocks = max(i.nblocks for i in infos)
     ctx = hjd.Context(dev.index)
-    outs = [torch.empty((h, w), dtype=torch.int32, device=dev) for _ in range(nf)]
     gpu_entropy = wl.get("entropy") == "gpu"
+    d2h = bool(wl.get("d2h"))
+    per_batch = int(os.environ.get("HJD_STREAM_BATCH", 16 if d2h else 32))
+    nslots = int(os.environ.get("HJD_STREAM_SLOTS", 4 if d2h else 6))
+    if d2h:
+        # pinned host ring, one buffer per frame that can be in flight
+        ring = [torch.empty((h, w), dtype=torch.int32).pin_memory() for _ in range(per_batch * nslots)]
+        outs = [ring[i % len(ring)] for i in range(nf)]
+    else:
+        outs = [torch.empty((h, w), dtype=torch.int32, device=dev) for _ in range(nf)]
     if gpu_entropy:
-        per_batch = int(os.environ.get("HJD_STREAM_BATCH", 32))
-        nslots = int(os.environ.get("HJD_STREAM_SLOTS", 6))
         st = hjd.GpuJpegStream(ctx, per_batch, per_batch * max(len(d) for d in pool) + (1 << 20),
                                per_batch * max_blocks, nslots=nslots, nthreads=nthreads)
         stat_key = "host_prep_ns"
@@ -271,6 +280,7 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
             "config": {"workload": wl["desc"], "frames_per_gpu_per_step": nf, "width": w, "height": h,
                        "sampling": "4:2:0" if s == 1 else "4:4:4", "host_threads_per_gpu": nthreads,
                        "entropy_decode": "gpu" if gpu_entropy else "host", "mean_jpeg_bytes": jpeg_bytes,
+                       "output": "pinned host memory (D2H-on)" if d2h else "BGRX in HBM (D2H-off)",
                        "parallelism": f"image-parallel x{world} (no collective)"},
             "end_to_end": {
                 ("host_prep_Mpx_per_thread_s" if gpu_entropy else "host_huffman_Mpx_per_thread_s"):

@@ -123,9 +123,17 @@ int hjd_gstream_destroy(hjd_gstream* s);
 /* Queue one JPEG (bytes valid until hjd_gstream_sync returns); pixels go to
  * d_out (device, row pitch out_pitch bytes, 16-byte aligned). */
 int hjd_gstream_submit(hjd_gstream* s, const uint8_t* data, size_t size, void* d_out, int32_t out_pitch);
+/* D2H sink (SURVEY.md s8(e) "D2H-on", s8(f) rank 4): same, but the pixels are
+ * copied back into host memory h_out (row pitch out_pitch bytes; pinned memory
+ * keeps the copy asynchronous) once the frame is decoded. */
+int hjd_gstream_submit_host(hjd_gstream* s, const uint8_t* data, size_t size, void* h_out, int32_t out_pitch);
 /* Flush and wait; returns the first error.  stats (may be NULL):
  * {images, pixels, host_prep_ns, h2d_bytes, batches}. */
 int hjd_gstream_sync(hjd_gstream* s, int64_t stats[5]);
+
+/* The 54-byte header of the reference's output BMP (src/decoder.cpp:372-394):
+ * 32 bpp, top-down; the file is this header followed by the W*H*4 BGRX bytes. */
+int hjd_bmp_header(int32_t width, int32_t height, uint8_t header[54]);
 
 /* Test hook (no GPU): runs the same parallel algorithm on the host, one frame,
  * and writes its coefficients.  Not a decode path. */

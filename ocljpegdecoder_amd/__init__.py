@@ -25,11 +25,12 @@ from .backend import (  # noqa: E402
     mcu_geometry,
 )
 
-from .jpeg import (GpuDecoder, GpuJpegStream, JpegInfo, JpegStream, decode_coefs, decode_coefs_batch, decode_jpeg,  # noqa: E402
-                   emulate_entropy, parse)
+from .jpeg import (GpuDecoder, GpuJpegStream, JpegInfo, JpegStream, bmp_bytes, bmp_header,  # noqa: E402
+                   decode_coefs, decode_coefs_batch, decode_jpeg, emulate_entropy, parse)
 
 __all__ = [
-    "GpuDecoder", "GpuJpegStream", "JpegInfo", "JpegStream", "decode_coefs", "decode_coefs_batch", "decode_jpeg", "emulate_entropy",
+    "GpuDecoder", "GpuJpegStream", "JpegInfo", "JpegStream", "bmp_bytes", "bmp_header", "decode_coefs",
+    "decode_coefs_batch", "decode_jpeg", "emulate_entropy",
     "parse",
     "Context", "FrameSpec", "Plan", "decode_frame", "device_count", "frame_blocks", "mcu_geometry",
     "YUV444", "YUV420", "OTHER", "IN_Q16_ZIGZAG", "IN_I32_NATURAL",

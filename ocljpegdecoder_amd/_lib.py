@@ -139,6 +139,8 @@ def _bind_host(lib):
                                               ctypes.c_int, ctypes.POINTER(vp)]),
         "hjd_gstream_destroy": (ctypes.c_int, [vp]),
         "hjd_gstream_submit": (ctypes.c_int, [vp, u8p, ctypes.c_size_t, vp, ctypes.c_int32]),
+        "hjd_gstream_submit_host": (ctypes.c_int, [vp, u8p, ctypes.c_size_t, vp, ctypes.c_int32]),
+        "hjd_bmp_header": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, u8p]),
         "hjd_gstream_sync": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int64)]),
         "hjd_debug_entropy_emulate": (ctypes.c_int, [u8p, ctypes.c_size_t, ctypes.c_int,
                                                      ctypes.POINTER(ctypes.c_int16), ctypes.c_int64, c_i32p]),

@@ -886,8 +886,14 @@ int launch_entropy(hjd_gdec* g, const EntBatchDev& b, hipStream_t s)
 
 // Upload the staged frames and run the entropy kernels (+ the pixel kernel
 // when d_outs is given) on stream s.
+struct HostCopy {
+    void* host;          // destination (pinned host memory recommended)
+    int32_t host_pitch;
+    int32_t width, height;
+};
+
 int gdec_issue(hjd_gdec* g, void* const* d_outs, const int32_t* pitches, int16_t* coefs_out, int64_t* block_offsets,
-               hipStream_t s)
+               hipStream_t s, const HostCopy* host = nullptr)
 {
     HJD_HIP(hipSetDevice(g->device));
     const int n = static_cast<int>(g->frames.size());
@@ -918,6 +924,14 @@ int gdec_issue(hjd_gdec* g, void* const* d_outs, const int32_t* pitches, int16_t
                 g->out_base[sidx], s, 0);
             if (rc) return rc;
             r0 += g->nrec[sidx];
+        }
+    }
+    if (host && d_outs) {   // D2H sink: pixels of host-output frames back to the caller's memory
+        for (int i = 0; i < n; ++i) {
+            if (!host[i].host) continue;
+            HJD_HIP(hipMemcpy2DAsync(host[i].host, static_cast<size_t>(host[i].host_pitch), d_outs[i],
+                                     static_cast<size_t>(pitches[i]), static_cast<size_t>(host[i].width) * 4,
+                                     static_cast<size_t>(host[i].height), hipMemcpyDeviceToHost, s));
         }
     }
     HJD_HIP(hipMemcpyAsync(g->h_status, g->d_status, 4 * static_cast<size_t>(n), hipMemcpyDeviceToHost, s));
@@ -1139,8 +1153,9 @@ struct GBatch {
     int prepared = 0;
     bool closed = false;
     bool issued = false;
-    std::vector<void*> outs;
+    std::vector<void*> outs;         // device destination, or null for a host-output frame
     std::vector<int32_t> pitches;
+    std::vector<void*> host_outs;    // host destination (D2H sink), or null
 };
 
 struct GJob {
@@ -1159,6 +1174,8 @@ struct hjd_gstream {
     int device = 0;
     std::vector<hjd_gdec*> slots;
     std::vector<hipStream_t> streams;
+    std::vector<uint8_t*> scratch;       // per slot: device pixels of host-output frames (D2H sink)
+    std::vector<size_t> scratch_bytes;
     std::vector<GBatch*> slot_batch;   // batch currently owning each slot (nullptr = free)
     int next_slot = 0;
     GBatch* open = nullptr;
@@ -1228,22 +1245,44 @@ void hjd_gstream::issue_locked(GBatch* b)
     // drop frames whose preparation failed (already recorded)
     std::vector<void*> outs;
     std::vector<int32_t> pitches;
+    std::vector<HostCopy> host;
     std::vector<Prepared> keep;
-    size_t used = 0;
+    size_t used = 0, scratch_need = 0;
     for (int i = 0; i < b->nframes; ++i) {
         Prepared& p = g->frames[i];
         if (p.rc != HJD_OK) continue;
         used = std::max(used, align_up(p.data_off + p.data_bits / 8 + kDataPad, 16));
         images++;
         pixels += static_cast<int64_t>(p.width) * p.height;
+        if (b->host_outs[i]) {
+            host.push_back(HostCopy{b->host_outs[i], b->pitches[i], p.width, p.height});
+            outs.push_back(reinterpret_cast<void*>(scratch_need));   // offset, rebased below
+            pitches.push_back(align_up(4 * static_cast<size_t>(p.width), 16));
+            scratch_need += align_up(static_cast<size_t>(pitches.back()) * p.height, 256);
+        } else {
+            host.push_back(HostCopy{nullptr, 0, p.width, p.height});
+            outs.push_back(b->outs[i]);
+            pitches.push_back(b->pitches[i]);
+        }
         keep.push_back(std::move(p));
-        outs.push_back(b->outs[i]);
-        pitches.push_back(b->pitches[i]);
     }
     g->frames.swap(keep);
     g->data_used = used;
-    if (!g->frames.empty()) {
-        const int rc = gdec_issue(g, outs.data(), pitches.data(), nullptr, nullptr, streams[b->slot]);
+    int rc = HJD_OK;
+    if (scratch_need > scratch_bytes[b->slot]) {   // grows rarely; the slot's previous batch is complete
+        if (scratch[b->slot]) (void)hipFree(scratch[b->slot]);
+        scratch[b->slot] = nullptr;
+        scratch_bytes[b->slot] = 0;
+        if (hipMalloc(reinterpret_cast<void**>(&scratch[b->slot]), scratch_need) != hipSuccess)
+            rc = set_error(HJD_E_NOMEM, "device scratch for host outputs (%zu bytes)", scratch_need);
+        else
+            scratch_bytes[b->slot] = scratch_need;
+    }
+    for (size_t i = 0; i < outs.size(); ++i)
+        if (host[i].host) outs[i] = scratch[b->slot] + reinterpret_cast<size_t>(outs[i]);
+    if (rc) record_error(rc, hjd_last_error());
+    if (!g->frames.empty() && rc == HJD_OK) {
+        rc = gdec_issue(g, outs.data(), pitches.data(), nullptr, nullptr, streams[b->slot], host.data());
         if (rc) record_error(rc, hjd_last_error());
         h2d_bytes += static_cast<int64_t>(g->H.used + g->data_used);
         batches++;
@@ -1293,6 +1332,8 @@ int hjd_gstream_create(hjd_ctx* ctx, int max_frames, int64_t max_scan_bytes, int
     st->device = hjd_ctx_device(ctx);
     st->slots.assign(nslots, nullptr);
     st->streams.assign(nslots, nullptr);
+    st->scratch.assign(nslots, nullptr);
+    st->scratch_bytes.assign(nslots, 0);
     st->slot_batch.assign(nslots, nullptr);
     for (int s = 0; s < nslots; ++s) {
         int rc = hjd_gdec_create(ctx, max_frames, max_scan_bytes, max_blocks, 0, &st->slots[s]);
@@ -1308,10 +1349,9 @@ int hjd_gstream_create(hjd_ctx* ctx, int max_frames, int64_t max_scan_bytes, int
     return HJD_OK;
 }
 
-int hjd_gstream_submit(hjd_gstream* st, const uint8_t* data, size_t size, void* d_out, int32_t out_pitch)
+static int gstream_submit(hjd_gstream* st, const uint8_t* data, size_t size, void* d_out, void* h_out,
+                          int32_t out_pitch)
 {
-    if (!st || !data || !d_out || out_pitch <= 0 || (out_pitch & 3) || (reinterpret_cast<uintptr_t>(d_out) & 15))
-        return set_error(HJD_E_INVALID, "invalid submit arguments (d_out must be 16-byte aligned)");
     hjd_internal::ScanHeader h;
     int rc = hjd_internal::parse_scan_header(data, size, &h);
     if (rc) return rc;
@@ -1339,6 +1379,7 @@ int hjd_gstream_submit(hjd_gstream* st, const uint8_t* data, size_t size, void* 
     if (b->nframes == 0) g->frames.assign(static_cast<size_t>(g->caps.max_frames), Prepared());
     GJob job{b, b->nframes, data, size, b->bytes, need};
     b->outs.push_back(d_out);
+    b->host_outs.push_back(h_out);
     b->pitches.push_back(out_pitch);
     b->nframes++;
     b->bytes += need;
@@ -1346,6 +1387,39 @@ int hjd_gstream_submit(hjd_gstream* st, const uint8_t* data, size_t size, void* 
     st->queue.push_back(job);
     lk.unlock();
     st->cv_jobs.notify_one();
+    return HJD_OK;
+}
+
+int hjd_gstream_submit(hjd_gstream* st, const uint8_t* data, size_t size, void* d_out, int32_t out_pitch)
+{
+    if (!st || !data || !d_out || out_pitch <= 0 || (out_pitch & 3) || (reinterpret_cast<uintptr_t>(d_out) & 15))
+        return set_error(HJD_E_INVALID, "invalid submit arguments (d_out must be 16-byte aligned)");
+    return gstream_submit(st, data, size, d_out, nullptr, out_pitch);
+}
+
+int hjd_gstream_submit_host(hjd_gstream* st, const uint8_t* data, size_t size, void* h_out, int32_t out_pitch)
+{
+    if (!st || !data || !h_out || out_pitch <= 0) return set_error(HJD_E_INVALID, "invalid submit arguments");
+    return gstream_submit(st, data, size, nullptr, h_out, out_pitch);
+}
+
+int hjd_bmp_header(int32_t width, int32_t height, uint8_t header[54])
+{
+    if (!header || width <= 0 || height <= 0) return set_error(HJD_E_INVALID, "invalid BMP geometry");
+    // src/decoder.cpp:372-394 (bmp_create): BITMAPFILEHEADER + BITMAPINFOHEADER,
+    // 32 bpp BI_RGB, negative height = top-down rows, pixels = the BGRX image.
+    auto put16 = [&](int o, uint32_t v) { header[o] = v & 0xFF; header[o + 1] = (v >> 8) & 0xFF; };
+    auto put32 = [&](int o, uint32_t v) { put16(o, v & 0xFFFF); put16(o + 2, v >> 16); };
+    memset(header, 0, 54);
+    const uint64_t size = 54 + static_cast<uint64_t>(width) * static_cast<uint64_t>(height) * 4;
+    put16(0, 0x4d42);
+    put32(2, static_cast<uint32_t>(size));
+    put32(10, 54);
+    put32(14, 40);
+    put32(18, static_cast<uint32_t>(width));
+    put32(22, static_cast<uint32_t>(-height));
+    put16(26, 1);
+    put16(28, 32);
     return HJD_OK;
 }
 
@@ -1401,6 +1475,7 @@ int hjd_gstream_destroy(hjd_gstream* st)
         delete st->slot_batch[s];
         if (st->slots[s]) hjd_gdec_destroy(st->slots[s]);
         if (st->streams[s]) (void)hipStreamDestroy(st->streams[s]);
+        if (st->scratch[s]) (void)hipFree(st->scratch[s]);
     }
     delete st;
     return HJD_OK;

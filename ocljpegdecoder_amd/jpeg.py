@@ -250,13 +250,28 @@ class GpuJpegStream:
         self._keep = []
 
     def submit(self, data: bytes, out, out_pitch: Optional[int] = None):
+        """out: contiguous device tensor, or a (pinned) host tensor / numpy
+        array -- then the pixels are copied back to host memory (D2H sink)."""
         buf = _buf(data) if not isinstance(data, ctypes.Array) else data
         self._keep.append(buf)
-        if not (out.is_cuda and out.is_contiguous()):
-            raise ValueError("out must be a contiguous device tensor")
+        if isinstance(out, np.ndarray):
+            if not out.flags.c_contiguous:
+                raise ValueError("out must be C-contiguous")
+            self._keep.append(out)
+            pitch = out_pitch or out.shape[-1] * out.itemsize
+            check(self.lib.hjd_gstream_submit_host(self.handle, ctypes.cast(buf, _u8p), len(buf), out.ctypes.data,
+                                                   int(pitch)), "hjd_gstream_submit_host")
+            return
+        if not out.is_contiguous():
+            raise ValueError("out must be contiguous")
         out_pitch = out_pitch or out.shape[-1] * out.element_size()
-        check(self.lib.hjd_gstream_submit(self.handle, ctypes.cast(buf, _u8p), len(buf), out.data_ptr(),
-                                          int(out_pitch)), "hjd_gstream_submit")
+        if out.is_cuda:
+            check(self.lib.hjd_gstream_submit(self.handle, ctypes.cast(buf, _u8p), len(buf), out.data_ptr(),
+                                              int(out_pitch)), "hjd_gstream_submit")
+        else:
+            self._keep.append(out)
+            check(self.lib.hjd_gstream_submit_host(self.handle, ctypes.cast(buf, _u8p), len(buf), out.data_ptr(),
+                                                   int(out_pitch)), "hjd_gstream_submit_host")
 
     def sync(self) -> dict:
         stats = (ctypes.c_int64 * 5)()
@@ -282,6 +297,21 @@ class GpuJpegStream:
             self.close()
         except Exception:
             pass
+
+
+def bmp_header(width: int, height: int) -> bytes:
+    """The reference's 54-byte BMP header (src/decoder.cpp:372-394): 32 bpp, top-down."""
+    lib = _lib.load()
+    h = (ctypes.c_uint8 * 54)()
+    check(lib.hjd_bmp_header(int(width), int(height), h), "hjd_bmp_header")
+    return bytes(h)
+
+
+def bmp_bytes(bgrx) -> bytes:
+    """A BMP file exactly as the reference writes it from the GPU path
+    (header + the H x W BGRX words)."""
+    a = np.ascontiguousarray(bgrx).view(np.uint32)
+    return bmp_header(a.shape[1], a.shape[0]) + a.astype("<u4").tobytes()
 
 
 def emulate_entropy(data: bytes, sub_bits: int = 0):

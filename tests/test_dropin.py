@@ -104,5 +104,7 @@ def test_reference_program_on_mi355x(name):
         shutil.rmtree(tmp, ignore_errors=True)
     w, h = rec["width"], rec["height"]
     assert len(bmp) == 54 + w * h * 4          # GPU path writes exactly H rows
+    import ocljpegdecoder_amd as hjd
+    assert bmp[:54] == hjd.bmp_header(w, h)    # our BMP sink writes the reference's header
     px = bmp[54:]
     assert hashlib.sha256(px).hexdigest() == rec["bgrx_sha256"]

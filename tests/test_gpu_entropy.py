@@ -207,3 +207,30 @@ def test_gstream_bad_file_reported(hjd, ctx):
     exp = O.decode_q16(coefs, info.qt, info.width, info.height, info.sampling)
     for o in outs:
         np.testing.assert_array_equal(o.cpu().numpy().view(np.uint32), exp)
+
+
+def test_gstream_host_outputs(hjd, ctx):
+    """D2H sink: pixels copied back into host memory (numpy and pinned torch),
+    mixed with device outputs in the same batches."""
+    import torch
+    datas = [_pil(int(w), int(h), 90, sub, seed=300 + i, **kw) for i, (w, h, sub, kw) in enumerate(
+        [(640, 480, 2, {}), (333, 177, 0, {}), (1024, 768, 2, {"restart_marker_blocks": 2}), (17, 9, 0, {})] * 3)]
+    infos = [hjd.parse(d) for d in datas]
+    outs = []
+    for i, info in enumerate(infos):
+        if i % 3 == 0:
+            outs.append(np.full((info.height, info.width), -1, dtype=np.int32))
+        elif i % 3 == 1:
+            outs.append(torch.full((info.height, info.width), -1, dtype=torch.int32).pin_memory())
+        else:
+            outs.append(torch.full((info.height, info.width), -1, dtype=torch.int32, device="cuda"))
+    cap_b = max(len(d) for d in datas) * 4 + (1 << 16)
+    with hjd.GpuJpegStream(ctx, 4, cap_b, 4 * max(i.nblocks for i in infos), nslots=2, nthreads=4) as st:
+        for d, o in zip(datas, outs):
+            st.submit(d, o)
+        st.sync()
+    for d, o, info in zip(datas, outs, infos):
+        coefs, _ = hjd.decode_coefs(d)
+        exp = O.decode_q16(coefs, info.qt, info.width, info.height, info.sampling)
+        got = o if isinstance(o, np.ndarray) else o.cpu().numpy()
+        np.testing.assert_array_equal(got.view(np.uint32), exp)

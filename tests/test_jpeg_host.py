@@ -122,3 +122,17 @@ def test_16bit_dqt_and_restart_rows(lib):
     assert list(info16.qt_precision) == [1, 1, 1]
     np.testing.assert_array_equal(np.array(info16.qt), np.array(info8.qt))
     np.testing.assert_array_equal(coefs16, coefs8)
+
+
+def test_bmp_header_matches_reference_layout(hjd):
+    """hjd_bmp_header == the reference's bmp_create() (src/decoder.cpp:372-394):
+    packed BITMAPFILEHEADER (14 B) + BITMAPINFOHEADER (40 B), 32 bpp, BI_RGB,
+    negative height (top-down)."""
+    import struct
+    for w, h in ((313, 234), (1, 1), (3840, 2160)):
+        size = 54 + w * h * 4
+        exp = struct.pack("<HIHHI", 0x4D42, size, 0, 0, 54) + struct.pack("<IiiHHIIiiII", 40, w, -h, 1, 32, 0, 0, 0, 0,
+                                                                           0, 0)
+        assert hjd.bmp_header(w, h) == exp
+    px = np.arange(12, dtype=np.uint32).reshape(3, 4)
+    assert hjd.bmp_bytes(px) == hjd.bmp_header(4, 3) + px.astype("<u4").tobytes()
