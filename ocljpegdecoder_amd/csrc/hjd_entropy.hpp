@@ -279,28 +279,6 @@ __host__ __device__ __forceinline__ uint32_t funnel(uint32_t w0, uint32_t w1, ui
     return static_cast<uint32_t>(((static_cast<uint64_t>(w0) << 32) | w1) >> (32 - off));
 }
 
-// The top w bits of x (0 when w == 0): one v_bfe_u32 on the device.
-__host__ __device__ __forceinline__ uint32_t top_bits(uint32_t x, uint32_t w)
-{
-#ifdef __HIP_DEVICE_COMPILE__
-    return __builtin_amdgcn_ubfe(x, 32u - w, w);
-#else
-    return w ? x >> (32 - w) : 0u;
-#endif
-}
-
-// Per-block decode info from its jinfo: DC/AC table slots and component masks.
-__host__ __device__ __forceinline__ void block_info(uint32_t ji, uint32_t& sdc, uint32_t& sac, int32_t& m0,
-                                                    int32_t& m1, int32_t& m2)
-{
-    const uint32_t comp = (ji >> 6) & 3;
-    sdc = ji & 7;
-    sac = (ji >> 3) & 7;
-    m0 = comp == 0 ? -1 : 0;
-    m1 = comp == 1 ? -1 : 0;
-    m2 = comp == 2 ? -1 : 0;
-}
-
 // Decode one run: from `entry` until the first unit boundary >= stop (write
 // mode: and until the block this run owns is complete).  Accumulates `st`
 // (must start as the identity).  Returns the exit state.  Per-component sums
@@ -343,9 +321,6 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
         int16_t* cur = nullptr;                        // write mode: its destination (null: not written)
         uint32_t quarter = 0;                          // write mode: quarter of the block being staged
         uint32_t ji = jinfo_of(c, j);
-        uint32_t sdc, sac;          // table slots of the current block
-        int32_t m0, m1, m2;         // all-ones for the current block's component
-        block_info(ji, sdc, sac, m0, m1, m2);
         result = 0;
         bool done = false;
         while (!done) {
@@ -367,7 +342,6 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
                     j = 0;
                     z = 0;
                     ji = jinfo_of(c, 0);
-                    block_info(ji, sdc, sac, m0, m1, m2);
                     owned = false;
                     cur = nullptr;
                     flags |= kReset;
@@ -385,14 +359,16 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
                     continue;
                 }
             }
-            // ---- one Huffman symbol + its extra bits, branch-light: every lane
-            // runs the same instructions whatever the symbol kind (DC, AC, EOB,
-            // ZRL); only long codes, block ends and the rare events branch ----
+            // ---- one Huffman symbol + its extra bits ----
+            const uint32_t comp = (ji >> 6) & 3;
             const bool dc = z == 0;
-            const HuffLut& t = c.tabs[dc ? sdc : sac];
+            const HuffLut& t = c.tabs[dc ? (ji & 7) : ((ji >> 3) & 7)];
             const uint32_t e = t.lut[peek >> (32 - kLutBits)];
-            uint32_t len = e >> 8, sym = e & 0xFF;
-            if (e == 0) {
+            uint32_t len, sym;
+            if (e != 0) {
+                len = e >> 8;
+                sym = e & 0xFF;
+            } else {
                 // Codes longer than the LUT (T.81 F.2.2.3): the length is the first
                 // l with code_l <= MAXCODE[l]; the six compares use independent
                 // loads and selects instead of a dependent loop.
@@ -411,27 +387,25 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
                 }
             }
             const uint32_t s = sym & 15;
-            const uint32_t r = dc ? 0u : sym >> 4;
-            const uint32_t bits = top_bits(peek << len, s);              // 0 when s == 0
-            const uint32_t span = (1u << s) - 1;
-            const int32_t v = static_cast<int32_t>(bits) - (bits < ((span + 1) >> 1) ? static_cast<int32_t>(span) : 0);
+            const uint32_t r = dc ? 0 : sym >> 4;
+            if (dc && sym > 11) flags |= kError;
+            int32_t v = 0;
+            if (s) {
+                const uint32_t bits = (peek << len) >> (32 - s);
+                v = bits < (1u << (s - 1)) ? static_cast<int32_t>(bits) - static_cast<int32_t>((1u << s) - 1)
+                                           : static_cast<int32_t>(bits);
+            }
             pos += len + s;
-            const bool nzac = !dc && s != 0;
-            const uint32_t zr = z + r;
-            const bool bad = nzac && zr > 63;
-            flags |= (bad || (dc && sym > 11)) ? kError : 0u;
-            const uint32_t znew = dc ? 1u : (s == 0 ? (r == 15 ? z + 16 : 64u) : (bad ? 64u : zr + 1));
-            const int32_t dv = dc ? v : 0;
-            nblk += dc ? 1 : 0;
-            d0 += dv & m0;
-            d1 += dv & m1;
-            d2 += dv & m2;
-            if (kWrite) {
-                if (dc) {
+            if (dc) {
+                nblk += 1;
+                d0 += comp == 0 ? v : 0;
+                d1 += comp == 1 ? v : 0;
+                d2 += comp == 2 ? v : 0;
+                if (kWrite) {
                     owned = true;
-                    p0 += dv & m0;
-                    p1 += dv & m1;
-                    p2 += dv & m2;
+                    p0 += comp == 0 ? v : 0;
+                    p1 += comp == 1 ? v : 0;
+                    p2 += comp == 2 ? v : 0;
                     // MCU-major destination; on valid data blk % bpm == j.  Blocks past
                     // the frame's count are ignored (as the host decoder stops there).
                     const uint32_t dst = blk - j + (ji >> 8);
@@ -440,22 +414,33 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
                         if (dst < out->nblocks && blk % static_cast<uint32_t>(c.bpm) == j) {
                             cur = out->coefs + static_cast<uint64_t>(dst) * 64;
                             zero_quarter(out->stage);
-                            out->stage[0] = static_cast<int16_t>((p0 & m0) | (p1 & m1) | (p2 & m2));
+                            out->stage[0] = static_cast<int16_t>(comp == 0 ? p0 : (comp == 1 ? p1 : p2));
                             quarter = 0;
                         } else {
                             flags |= kError;   // a restart interval ended inside an MCU
                         }
                     }
-                } else if (nzac && !bad && cur) {
-                    const uint32_t qz = zr >> 4;
-                    if (qz != quarter) {
-                        flush_quarters(cur, out->stage, quarter, qz);
-                        quarter = qz;
+                }
+                z = 1;
+            } else if (s == 0) {
+                z = r == 15 ? z + 16 : 64;       // ZRL / EOB
+            } else {
+                z += r;
+                if (z > 63) {
+                    flags |= kError;
+                    z = 64;
+                } else {
+                    if (kWrite && cur) {
+                        const uint32_t qz = z >> 4;
+                        if (qz != quarter) {
+                            flush_quarters(cur, out->stage, quarter, qz);
+                            quarter = qz;
+                        }
+                        out->stage[z & 15] = static_cast<int16_t>(v);
                     }
-                    out->stage[zr & 15] = static_cast<int16_t>(v);
+                    ++z;
                 }
             }
-            z = znew;
             if (z >= 64) {
                 if (kWrite && owned) {
                     if (cur) flush_quarters(cur, out->stage, quarter, 4);   // the rest of the block
@@ -466,7 +451,6 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
                 z = 0;
                 j = j + 1 == static_cast<uint32_t>(c.bpm) ? 0 : j + 1;
                 ji = jinfo_of(c, j);
-                block_info(ji, sdc, sac, m0, m1, m2);
             }
         }
         if (!done) result = pack_state(pos, j, z, seg);
