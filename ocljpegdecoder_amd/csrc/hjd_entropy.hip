@@ -1190,6 +1190,7 @@ struct hjd_gstream {
     std::atomic<int64_t> images{0}, pixels{0}, prep_ns{0}, h2d_bytes{0}, batches{0};
     int first_error = HJD_OK;
     std::string first_error_msg;
+    int local_cpus = 0;   // CPUs of the GPU's NUMA node the workers are bound to (0: unbound)
 
     void record_error(int rc, const std::string& msg)
     {
@@ -1335,16 +1336,29 @@ int hjd_gstream_create(hjd_ctx* ctx, int max_frames, int64_t max_scan_bytes, int
     st->scratch.assign(nslots, nullptr);
     st->scratch_bytes.assign(nslots, 0);
     st->slot_batch.assign(nslots, nullptr);
+    // NUMA locality: pinned staging is allocated, and the
+    // workers run, on the CPUs of the GPU's NUMA node (HJD_NUMA=0 disables).
+    const char* numa_env = getenv("HJD_NUMA");
+    const hjd_internal::CpuSet local = (numa_env && numa_env[0] == '0') ? hjd_internal::CpuSet{}
+                                                                       : hjd_internal::device_local_cpus(st->device);
+    const std::vector<int> prev = hjd_internal::bind_current_thread(local);
     for (int s = 0; s < nslots; ++s) {
         int rc = hjd_gdec_create(ctx, max_frames, max_scan_bytes, max_blocks, 0, &st->slots[s]);
         if (rc == HJD_OK && hipStreamCreateWithFlags(&st->streams[s], hipStreamNonBlocking) != hipSuccess)
             rc = set_error(HJD_E_HIP, "hipStreamCreate");
         if (rc) {
+            hjd_internal::restore_current_thread(prev);
             hjd_gstream_destroy(st);
             return rc;
         }
     }
-    for (int t = 0; t < nthreads; ++t) st->workers.emplace_back([st] { st->worker(); });
+    hjd_internal::restore_current_thread(prev);
+    st->local_cpus = static_cast<int>(local.cpus.size());
+    for (int t = 0; t < nthreads; ++t)
+        st->workers.emplace_back([st, local] {
+            hjd_internal::bind_current_thread(local);
+            st->worker();
+        });
     *out = st;
     return HJD_OK;
 }

@@ -2,6 +2,8 @@
 #pragma once
 #include <stdint.h>
 
+#include <vector>
+
 struct hjd_ctx;
 
 namespace hjd_internal {
@@ -45,5 +47,20 @@ int parse_scan_header(const uint8_t* data, size_t size, ScanHeader* h);
 
 // hjd_ctx accessors for the other translation units
 int ctx_num_cu(const struct ::hjd_ctx* ctx);
+
+}  // namespace hjd_internal
+
+namespace hjd_internal {
+
+// NUMA locality of a device's host-side workers: the CPUs
+// of the NUMA node the GPU's PCIe device hangs off (sysfs), or an empty set
+// when unknown.  bind_current_thread() applies such a set (no-op if empty)
+// and returns the previous mask so a caller can restore it.
+struct CpuSet {
+    std::vector<int> cpus;
+};
+CpuSet device_local_cpus(int device);
+std::vector<int> bind_current_thread(const CpuSet& s);
+void restore_current_thread(const std::vector<int>& prev);
 
 }  // namespace hjd_internal

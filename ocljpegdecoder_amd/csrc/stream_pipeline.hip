@@ -209,7 +209,15 @@ int hjd_stream_create(hjd_ctx* ctx, int64_t max_blocks, int nslots, int nthreads
         if ((e = hipEventCreateWithFlags(&st->kernel_done[s], hipEventDisableTiming)) != hipSuccess)
             return bail("event", e);
     }
-    for (int t = 0; t < nthreads; ++t) st->workers.emplace_back([st] { st->worker(); });
+    // NUMA-local workers; HJD_NUMA=0 disables
+    const char* numa_env = getenv("HJD_NUMA");
+    const hjd_internal::CpuSet local = (numa_env && numa_env[0] == '0') ? hjd_internal::CpuSet{}
+                                                                       : hjd_internal::device_local_cpus(st->device);
+    for (int t = 0; t < nthreads; ++t)
+        st->workers.emplace_back([st, local] {
+            hjd_internal::bind_current_thread(local);
+            st->worker();
+        });
     *out = st;
     return HJD_OK;
 }
