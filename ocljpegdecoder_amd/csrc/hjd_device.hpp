@@ -180,6 +180,16 @@ __device__ __forceinline__ uint32_t pk_clamp_u8(uint32_t a)
     return __builtin_bit_cast(uint32_t, x);
 }
 
+// v_sat_pk_u8_i16: two int16 lanes saturated to [0,255] and packed into bytes
+// 0 (low lane) and 1 (high lane) -- the clamp255 of src/macro.h:121-126 for two
+// pixels in one instruction (replaces a packed max + min).
+__device__ __forceinline__ uint32_t sat_pk_u8(uint32_t a)
+{
+    uint32_t r;
+    asm("v_sat_pk_u8_i16 %0, %1" : "=v"(r) : "v"(a));
+    return r;
+}
+
 // v_perm_b32: result byte i = sel byte i of {S1 bytes 0-3 -> 0..3, S0 bytes -> 4..7, 0x0c -> 0}
 __device__ __forceinline__ uint32_t perm(uint32_t s0, uint32_t s1, uint32_t sel)
 {
@@ -211,7 +221,7 @@ template <bool kCheckSpecial>
 __device__ __forceinline__ void pixels2(uint32_t ypair, const ChromaPair& c, const ChromaTerms* c0,
                                         const ChromaTerms* c1, uint32_t& px0, uint32_t& px1)
 {
-    const uint32_t R = pk_clamp_u8(pk_add16(ypair, c.r));
+    const uint32_t R = sat_pk_u8(pk_add16(ypair, c.r));   // bytes r0 r1
     uint32_t graw = pk_add16(ypair, c.g);
     if constexpr (kCheckSpecial) {
         const int y0 = static_cast<short>(ypair), y1 = static_cast<int>(ypair) >> 16;
@@ -219,11 +229,11 @@ __device__ __forceinline__ void pixels2(uint32_t ypair, const ChromaPair& c, con
         const short d1 = (c1->special && static_cast<unsigned>(y1 - 188) < 14u) ? 1 : 0;
         graw = __builtin_bit_cast(uint32_t, __builtin_bit_cast(s16x2, graw) - (s16x2){d0, d1});
     }
-    const uint32_t G = pk_clamp_u8(graw);
-    const uint32_t B = pk_clamp_u8(pk_add16(ypair, c.b));
-    const uint32_t T = perm(G, B, 0x06020400u);   // B.b0 G.b0 B.b2 G.b2
-    px0 = perm(R, T, 0x0c040100u);                // b0 g0 r0 0
-    px1 = perm(R, T, 0x0c060302u);                // b1 g1 r1 0
+    const uint32_t G = sat_pk_u8(graw);                   // bytes g0 g1
+    const uint32_t B = sat_pk_u8(pk_add16(ypair, c.b));   // bytes b0 b1
+    const uint32_t T = perm(G, B, 0x05010400u);           // b0 g0 b1 g1
+    px0 = perm(R, T, 0x0c040100u);                        // b0 g0 r0 0
+    px1 = perm(R, T, 0x0c050302u);                        // b1 g1 r1 0
 }
 
 // Scalar form (one pixel) on top of the same code, for the colour test hooks.
