@@ -283,12 +283,11 @@ __device__ __forceinline__ void load_tables(HuffLut* lds, const HuffLut* g, int 
 __device__ __forceinline__ SubStats shfl_down_stats(const SubStats& s, int d)
 {
     SubStats r;
-    r.nblk = __shfl_down(s.nblk, d);
+    r.nblk = static_cast<uint32_t>(__shfl_down(static_cast<int>(s.nblk), d));
+    r.flags = static_cast<uint32_t>(__shfl_down(static_cast<int>(s.flags), d));
     r.dc[0] = __shfl_down(s.dc[0], d);
     r.dc[1] = __shfl_down(s.dc[1], d);
     r.dc[2] = __shfl_down(s.dc[2], d);
-    r.flags = __shfl_down(s.flags, d);
-    r.pad[0] = r.pad[1] = r.pad[2] = 0;
     return r;
 }
 
@@ -532,7 +531,7 @@ __global__ __launch_bounds__(kGroupSubs) void ent_write_kernel(EntBatchDev b)
     RunOut o;
     o.coefs = b.coefs + F.coef_off * 64;
     o.stage = stage + tid * kStageStride;
-    o.blk = static_cast<uint32_t>(excl.nblk);
+    o.blk = excl.nblk;
     o.nblocks = F.nblocks;
     o.pred[0] = excl.dc[0];
     o.pred[1] = excl.dc[1];
@@ -540,7 +539,7 @@ __global__ __launch_bounds__(kGroupSubs) void ent_write_kernel(EntBatchDev b)
     SubStats st = stats_identity();
     run<true>(c, b.entries[F.sub_base + ku], (ku + 1) * S, st, &o);
     uint32_t bad = (st.flags & kError) ? kStatusCorrupt : 0;
-    if (ku == F.nsub - 1 && static_cast<uint32_t>(excl.nblk + st.nblk) < F.nblocks) bad |= kStatusCount;
+    if (ku == F.nsub - 1 && excl.nblk + st.nblk < F.nblocks) bad |= kStatusCount;
     if (bad) atomicOr(&b.status[f], bad);
 }
 
@@ -624,7 +623,7 @@ void emulate(const EntBatchDev& b)
             RunOut o;
             o.coefs = b.coefs + F.coef_off * 64;
             o.stage = stage;
-            o.blk = static_cast<uint32_t>(pre.nblk);
+            o.blk = pre.nblk;
             o.nblocks = F.nblocks;
             o.pred[0] = pre.dc[0];
             o.pred[1] = pre.dc[1];
@@ -632,7 +631,7 @@ void emulate(const EntBatchDev& b)
             SubStats s = stats_identity();
             run<true>(c, b.entries[F.sub_base + i], (i + 1) * S, s, &o);
             if (s.flags & kError) b.status[f] |= kStatusCorrupt;
-            if (i == F.nsub - 1 && static_cast<uint32_t>(pre.nblk + s.nblk) < F.nblocks) b.status[f] |= kStatusCount;
+            if (i == F.nsub - 1 && pre.nblk + s.nblk < F.nblocks) b.status[f] |= kStatusCount;
             pre = stats_combine(pre, b.stats[F.sub_base + i]);
         }
     }

@@ -76,12 +76,11 @@ static_assert(sizeof(EntFrame) == 64, "EntFrame layout");
 // Per-subsequence statistics of a run; combined with an ordered, segmented
 // operator to get each subsequence's block index and DC predictors.
 struct SubStats {
-    int32_t nblk;      // DC units decoded (= blocks started)
-    int32_t dc[3];     // sum of DC differences per component since the last reset in this run
-    uint32_t flags;    // kReset | kError
-    uint32_t pad[3];
+    uint32_t nblk : 30;   // DC units decoded (= blocks started)
+    uint32_t flags : 2;   // kReset | kError
+    int32_t dc[3];        // sum of DC differences per component since the last reset in this run
 };
-static_assert(sizeof(SubStats) == 32, "SubStats layout");
+static_assert(sizeof(SubStats) == 16, "SubStats layout");
 
 constexpr uint32_t kReset = 1;      // a restart (or the frame start) happened inside the run
 constexpr uint32_t kError = 2;      // invalid symbol / overrun (fatal only for the verified chain)
@@ -95,9 +94,8 @@ __host__ __device__ __forceinline__ SubStats stats_identity()
 {
     SubStats s;
     s.nblk = 0;
-    s.dc[0] = s.dc[1] = s.dc[2] = 0;
     s.flags = 0;
-    s.pad[0] = s.pad[1] = s.pad[2] = 0;
+    s.dc[0] = s.dc[1] = s.dc[2] = 0;
     return s;
 }
 
@@ -109,7 +107,6 @@ __host__ __device__ __forceinline__ SubStats stats_combine(const SubStats& a, co
     const bool rb = (b.flags & kReset) != 0;
     for (int c = 0; c < 3; ++c) r.dc[c] = rb ? b.dc[c] : a.dc[c] + b.dc[c];
     r.flags = a.flags | b.flags;
-    r.pad[0] = r.pad[1] = r.pad[2] = 0;
     return r;
 }
 
@@ -291,7 +288,7 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
     uint32_t z = st_z(entry);
     uint32_t j = st_j(entry);
     uint32_t seg = st_seg(entry);
-    int32_t nblk = st.nblk, d0 = st.dc[0], d1 = st.dc[1], d2 = st.dc[2];
+    int32_t nblk = static_cast<int32_t>(st.nblk), d0 = st.dc[0], d1 = st.dc[1], d2 = st.dc[2];
     uint32_t flags = st.flags;
     int32_t p0 = 0, p1 = 0, p2 = 0;
     uint32_t blk = 0;
@@ -455,7 +452,7 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
         }
         if (!done) result = pack_state(pos, j, z, seg);
     }
-    st.nblk = nblk;
+    st.nblk = static_cast<uint32_t>(nblk);
     st.dc[0] = d0;
     st.dc[1] = d1;
     st.dc[2] = d2;
