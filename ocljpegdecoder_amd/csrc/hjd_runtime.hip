@@ -82,7 +82,6 @@ struct hjd_plan {
 };
 
 static int geometry(int width, int height, int sampling, int& mcu_w, int& mcu_h, int& bpm, int& mpx);
-static int default_grid_cu(int num_cu, int64_t work_waves);
 static int decode_grid(int sampling, int fmt, int64_t tasks);
 
 int hjd_internal::ctx_num_cu(const hjd_ctx* ctx) { return ctx->num_cu; }
@@ -331,14 +330,6 @@ int hjd_plan_set_variant(hjd_plan* plan, int variant)
 int64_t hjd_plan_tasks(const hjd_plan* plan) { return plan ? plan->tasks : -1; }
 int64_t hjd_plan_pixels(const hjd_plan* plan) { return plan ? plan->pixels : -1; }
 int64_t hjd_plan_coef_bytes(const hjd_plan* plan) { return plan ? plan->coef_bytes : -1; }
-
-static int default_grid_cu(int num_cu, int64_t work_waves)
-{
-    // 4 resident 256-thread groups per CU (16 waves/CU; LDS 40 KiB per group).
-    const int64_t cap = static_cast<int64_t>(num_cu) * 4;
-    const int64_t need = (work_waves + hjd::kWavesPerGroup - 1) / hjd::kWavesPerGroup;
-    return static_cast<int>(std::max<int64_t>(1, std::min(cap, need)));
-}
 
 // Grid of the fused kernel: short contiguous task chunks per wave and many
 // more workgroups than fit at once (measured on MI355X, profiles/
