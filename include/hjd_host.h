@@ -93,7 +93,9 @@ int hjd_gdec_destroy(hjd_gdec* g);
 /* Decode n JPEGs to BGRX in device memory (d_outs[i], row pitch pitches[i];
  * 16-byte aligned).  Asynchronous on `stream` (hipStream_t, NULL = default);
  * the input bytes may be reused as soon as the call returns.  A later call on
- * the same object waits for this call's uploads first. */
+ * the same object waits (on the host) for this call's uploads and is ordered
+ * (on the device) after its kernels, whatever stream it uses; hjd_gdec_sync
+ * reports the statuses of the most recent call. */
 int hjd_gdec_decode(hjd_gdec* g, const uint8_t* const* datas, const size_t* sizes, int n, void* const* d_outs,
                     const int32_t* pitches, void* stream);
 

@@ -906,6 +906,9 @@ int gdec_issue(hjd_gdec* g, void* const* d_outs, const int32_t* pitches, int16_t
     b.linked = g->d_linked;
     b.agg = g->d_agg;
     b.status = g->d_status;
+    // the device buffers are reused: order this call after the previous one
+    // (which may have been issued on another stream)
+    if (g->pending) HJD_HIP(hipStreamWaitEvent(s, g->done, 0));
     HJD_HIP(hipMemcpyAsync(g->d_blob, g->h_stage, g->H.used, hipMemcpyHostToDevice, s));
     HJD_HIP(hipMemcpyAsync(g->d_blob + g->caps.data, g->h_stage + g->caps.data, g->data_used, hipMemcpyHostToDevice, s));
     HJD_HIP(hipEventRecord(g->staged, s));

@@ -234,3 +234,23 @@ def test_gstream_host_outputs(hjd, ctx):
         exp = O.decode_q16(coefs, info.qt, info.width, info.height, info.sampling)
         got = o if isinstance(o, np.ndarray) else o.cpu().numpy()
         np.testing.assert_array_equal(got.view(np.uint32), exp)
+
+
+def test_calls_on_different_streams_are_ordered(hjd, ctx):
+    """Back-to-back calls on two streams reuse the decoder's device buffers;
+    the second must not overwrite them under the first."""
+    import torch
+    datas = [_pil(1280, 720, 90, 2, seed=s) for s in range(3)]
+    infos = [hjd.parse(d) for d in datas]
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = [[torch.full((i.height, i.width), -1, dtype=torch.int32, device="cuda") for i in infos] for _ in range(4)]
+    with hjd.GpuDecoder(ctx, 3, sum(map(len, datas)), sum(i.nblocks for i in infos)) as gd:
+        for k in range(4):
+            gd.decode(datas, outs[k], s1 if k % 2 == 0 else s2)
+        gd.sync()
+    torch.cuda.synchronize()
+    for d, info, *os_ in zip(datas, infos, *outs):
+        coefs, _ = hjd.decode_coefs(d)
+        exp = O.decode_q16(coefs, info.qt, info.width, info.height, info.sampling)
+        for o in os_:
+            np.testing.assert_array_equal(o.cpu().numpy().view(np.uint32), exp)
