@@ -123,7 +123,8 @@ int hjd_gstream_create(hjd_ctx* ctx, int max_frames, int64_t max_scan_bytes, int
                        int nthreads, hjd_gstream** out);
 int hjd_gstream_destroy(hjd_gstream* s);
 /* Queue one JPEG (bytes valid until hjd_gstream_sync returns); pixels go to
- * d_out (device, row pitch out_pitch bytes, 16-byte aligned). */
+ * d_out (device, row pitch out_pitch bytes, 16-byte aligned).  submit and sync
+ * may be called from several threads (they are serialised internally). */
 int hjd_gstream_submit(hjd_gstream* s, const uint8_t* data, size_t size, void* d_out, int32_t out_pitch);
 /* D2H sink (SURVEY.md s8(e) "D2H-on", s8(f) rank 4): same, but the pixels are
  * copied back into host memory h_out (row pitch out_pitch bytes; pinned memory

@@ -1183,6 +1183,7 @@ struct hjd_gstream {
     GBatch* open = nullptr;
 
     std::mutex mu;
+    std::mutex api_mu;          // serialises submit/sync callers (batch opening drops `mu` while it waits)
     std::condition_variable cv_jobs, cv_state;
     std::deque<GJob> queue;
     bool stop = false;
@@ -1373,6 +1374,7 @@ static int gstream_submit(hjd_gstream* st, const uint8_t* data, size_t size, voi
     if (rc) return rc;
     if (out_pitch < 4 * h.width) return set_error(HJD_E_INVALID, "output pitch too small");
     const size_t need = align_up(size + kDataPad, 16);
+    std::lock_guard<std::mutex> api(st->api_mu);
     std::unique_lock<std::mutex> lk(st->mu);
     hjd_gdec* g0 = st->slots[0];
     if (need > g0->data_cap() || h.nblocks > g0->caps.max_blocks)
@@ -1442,6 +1444,7 @@ int hjd_bmp_header(int32_t width, int32_t height, uint8_t header[54])
 int hjd_gstream_sync(hjd_gstream* st, int64_t stats[5])
 {
     if (!st) return set_error(HJD_E_INVALID, "gstream is NULL");
+    std::lock_guard<std::mutex> api(st->api_mu);
     {
         std::unique_lock<std::mutex> lk(st->mu);
         if (st->open) {

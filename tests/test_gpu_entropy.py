@@ -254,3 +254,29 @@ def test_calls_on_different_streams_are_ordered(hjd, ctx):
         exp = O.decode_q16(coefs, info.qt, info.width, info.height, info.sampling)
         for o in os_:
             np.testing.assert_array_equal(o.cpu().numpy().view(np.uint32), exp)
+
+
+def test_gstream_concurrent_submitters(hjd, ctx):
+    """Several host threads submitting to one GPU-entropy stream."""
+    import threading
+
+    import torch
+    datas = [_pil(320 + 16 * i, 200, 90, 2 if i % 2 else 0, seed=400 + i) for i in range(8)]
+    infos = [hjd.parse(d) for d in datas]
+    jobs = [(datas[i % 8], infos[i % 8]) for i in range(48)]
+    outs = [torch.full((inf.height, inf.width), -1, dtype=torch.int32, device="cuda") for _, inf in jobs]
+    cap_b = max(map(len, datas)) * 3 + (1 << 16)
+    with hjd.GpuJpegStream(ctx, 3, cap_b, 3 * max(i.nblocks for i in infos), nslots=2, nthreads=4) as st:
+        def worker(k):
+            for i in range(k, len(jobs), 4):
+                st.submit(jobs[i][0], outs[i])
+        ts = [threading.Thread(target=worker, args=(k,)) for k in range(4)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        st.sync()
+    for (d, info), o in zip(jobs, outs):
+        coefs, _ = hjd.decode_coefs(d)
+        exp = O.decode_q16(coefs, info.qt, info.width, info.height, info.sampling)
+        np.testing.assert_array_equal(o.cpu().numpy().view(np.uint32), exp)
