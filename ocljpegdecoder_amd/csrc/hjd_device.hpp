@@ -34,7 +34,11 @@ __host__ __device__ __forceinline__ int mul24(int a, int b)
 __host__ __device__ __forceinline__ int mul181(int x) { return x * 181; }
 
 // min/max pairs lower to one v_med3_i32
-__host__ __device__ __forceinline__ int clamp_sample(int v) { return v < -256 ? -256 : (v > 255 ? 255 : v); }
+template <int kLevel = 0>
+__host__ __device__ __forceinline__ int clamp_sample(int v)
+{
+    return v < -256 + kLevel ? -256 + kLevel : (v > 255 + kLevel ? 255 + kLevel : v);
+}
 __device__ __forceinline__ int clamp_u8(int v) { return min(max(v, 0), 255); }
 
 // One 8-point pass on natural-order values v[0..7] (in place).
@@ -45,14 +49,18 @@ __device__ __forceinline__ int clamp_u8(int v) { return min(max(v, 0), 255); }
 //               src/idct8x8.cl:116).
 // The reference's DC-only short-cuts (:40-45, :86-92) give exactly the values
 // of the full butterfly, so the kernel always runs the full butterfly.
-template <bool kCol>
+// kLevel (column pass only): added to every output before the clamp, folded
+// into the DC rounding constant ((r + kLevel*2^14) >> 14 == (r >> 14) + kLevel),
+// so the luma level shift of the colour stage costs nothing.
+template <bool kCol, int kLevel = 0>
 __host__ __device__ __forceinline__ void idct8(int (&v)[8])
 {
     constexpr int kIn = kCol ? 8 : 11;
     constexpr int kRnd = kCol ? 4 : 0;
     constexpr int kSh = kCol ? 3 : 0;
 
-    int e0 = (v[0] << kIn) + (kCol ? 8192 : 128);
+    static_assert(kCol || kLevel == 0, "level shift is a column-pass option");
+    int e0 = (v[0] << kIn) + (kCol ? 8192 + (kLevel << 14) : 128);
     int e1 = v[4] << kIn;
 
     // odd part
@@ -81,10 +89,10 @@ __host__ __device__ __forceinline__ void idct8(int (&v)[8])
     int r0 = f7 + a1, r1 = f3 + g2, r2 = f0 + g4, r3 = f8 + a6;
     int r4 = f8 - a6, r5 = f0 - g4, r6 = f3 - g2, r7 = f7 - a1;
     if constexpr (kCol) {
-        v[0] = clamp_sample(r0 >> 14); v[1] = clamp_sample(r1 >> 14);
-        v[2] = clamp_sample(r2 >> 14); v[3] = clamp_sample(r3 >> 14);
-        v[4] = clamp_sample(r4 >> 14); v[5] = clamp_sample(r5 >> 14);
-        v[6] = clamp_sample(r6 >> 14); v[7] = clamp_sample(r7 >> 14);
+        v[0] = clamp_sample<kLevel>(r0 >> 14); v[1] = clamp_sample<kLevel>(r1 >> 14);
+        v[2] = clamp_sample<kLevel>(r2 >> 14); v[3] = clamp_sample<kLevel>(r3 >> 14);
+        v[4] = clamp_sample<kLevel>(r4 >> 14); v[5] = clamp_sample<kLevel>(r5 >> 14);
+        v[6] = clamp_sample<kLevel>(r6 >> 14); v[7] = clamp_sample<kLevel>(r7 >> 14);
     } else {
         v[0] = r0 >> 8; v[1] = r1 >> 8; v[2] = r2 >> 8; v[3] = r3 >> 8;
         v[4] = r4 >> 8; v[5] = r5 >> 8; v[6] = r6 >> 8; v[7] = r7 >> 8;
@@ -97,72 +105,93 @@ __host__ __device__ __forceinline__ void idct8(int (&v)[8])
 //   B = (int)(Y + 1.772*U + 128) in C double, each clamped to [0,255],
 //   packed 0x00RRGGBB (bytes B,G,R,0).
 //
-// Exact-integer restatement used by the kernel (proved by an exhaustive
-// device test over all 2^27 (Y,U,V) in [-256,255]^3, tests/test_gpu_parity.py):
-//   * clamp(trunc(x)) == clamp(floor(x)) for every real x;
-//   * Y+128 is an integer, so floor(x) = Y + 128 + floor(chroma term);
-//   * 1.402 = 701/500 and 1.772 = 443/250: for V,U != 0 the chroma term sits
-//     >= 1/500 from an integer, far above fp32/fp64 rounding, so
-//     floor(float(V)*1.402f) is exact (and exactly 0 for V == 0);
-//   * G's term is -(17207U + 35707V)/50000; it is computed as an exact integer
-//     floor division.  When the division is exact, the reference's double
-//     rounding can land one below the integer: over the whole domain this
-//     happens only for (U,V) = (-200,200) with Y in [188,201], where the
-//     reference gives one less (enumerated in tests/test_oracle.py).
+// Exact-integer restatement used by the kernel (proved over all 2^27
+// (Y,U,V) in [-256,255]^3 against the reference's hash by
+// tests/test_oracle.py::test_integer_csc_formulation_is_exact, and the device
+// code itself by the exhaustive device test in tests/test_gpu_parity.py):
+//   * clamp(trunc(x)) == clamp(floor(x)) for every real x, and Y+128 is an
+//     integer, so each channel is clamp(Y + 128 + floor(chroma term));
+//   * the +128 level shift is folded into the luma IDCT (its DC rounding
+//     constant, idct8<true, 128>): the colour stage receives Ys = Y + 128;
+//   * every chroma term is produced in the HIGH int16 of a 32-bit word, so
+//     one v_perm per channel assembles the int16 pair of two pixels:
+//       floor(1.402 v)               = hi16(v * 91881)
+//       floor(1.772 u)               = hi16(u * 116130 + 52)
+//       floor(-(17207u+35707v)/50000) = hi16(mulhi_i32(128*(-17207u-35707v), 43980466))
+//     (43980466 = ceil(2^48 / 6.4e6)).  The first two are 24-bit multiplies
+//     (R's reads the packed sample through SDWA, no extraction), the third
+//     is exact except where the division is exact with a negative quotient:
+//     (U,V) = (-200,200) and (-100,100), the only grid points whose mulhi
+//     has low half 0xffff (every other point's is <= 0xfffe).  There the
+//     value is one below the floor; the reference itself is one below the
+//     floor at (-200,200) for Y in [188,201] (its double rounding).  So the
+//     flag marks a pixel whose G term needs +1 unless it is that corner at
+//     those Y.  Callers take the corrected path only when some lane of the
+//     wave has a flagged pixel.
 // Chroma terms are computed once per chroma sample and shared by the 4 (4:2:0)
 // pixels that replicate it.
 // ---------------------------------------------------------------------------
+constexpr int kLumaLevel = 128;    // Ys = Y + 128, folded into the luma IDCT
+constexpr int kRK = 91881;         // floor(1.402 v) = (v * kRK) >> 16
+constexpr int kBK = 116130, kBBias = 52;   // floor(1.772 u) = (u * kBK + kBBias) >> 16
+constexpr int kGScale = 128;
+constexpr int kGKu = -17207 * kGScale, kGKv = -35707 * kGScale;   // 24-bit signed
+constexpr int kGMagic = 43980466;  // ceil(2^48 / (50000 * kGScale))
+constexpr int kGCornerQ = -75;     // G term at (U,V) = (-200,200) before correction
+constexpr int kGCornerYs0 = 188 + kLumaLevel;   // Y in [188,201]: the reference's rounding corner
+
+// The three chroma terms of one sample, each in the high int16 of its word.
 struct ChromaTerms {
-    int rq, gq, bq;
-    int special;
+    uint32_t r, g, b;
 };
 
-// Exact fixed-point floors (S = 20; K and the bias searched and proved over
-// v,u in [-256,255] by tests/test_oracle.py::test_fixed_point_colour_terms):
-//   floor(1.402 v) + 128 = (v*1470091 + (128<<20) + 1048) >> 20
-//   floor(1.772 u) + 128 = (u*1858077 + (128<<20) + 2097) >> 20
-// The +2^20/(2*den) bias keeps every case >= 1/1000 (R) or 1/500 (B) away
-// from an integer, which also covers the exact multiples (u = +-250).
-constexpr int kRK = 1470091, kRBias = (128 << 20) + 1048;
-constexpr int kBK = 1858077, kBBias = (128 << 20) + 2097;
-
-__host__ __device__ __forceinline__ int r_term(int v) { return (mul24(v, kRK) + kRBias) >> 20; }
-__host__ __device__ __forceinline__ int b_term(int u) { return (mul24(u, kBK) + kBBias) >> 20; }
-
-// floor(-(17207u + 35707v) / 50000) + 128, exactly, with one multiply-high:
-// m' = -(17207u + 35707v) + 300*50000 lies in [1.5e6, 2.9e7] < 2^25, and
-// floor(m'/50000) == mulhi(m', 2814749768) >> 15 for every m' < 2^25
-// (2814749768 = ceil(2^47/50000); exhaustively checked in
-// tests/test_oracle.py::test_fixed_point_colour_terms).  The offset's 300 is
-// removed together with the +128 level shift (-172).  m' also identifies the
-// double-rounding corner: (U,V) = (-200,200) is the only grid point with
-// m' = 11,300,000.
-constexpr int kGOffset = 15000000;
-constexpr unsigned kGMagic = 2814749768u;
-constexpr int kGSpecial = 11300000;
-
-__host__ __device__ __forceinline__ int g_mprime(int u, int v) { return mul24(u, -17207) + mul24(v, -35707) + kGOffset; }
-
-__host__ __device__ __forceinline__ int g_term_from_m(int mp)
+__host__ __device__ __forceinline__ int g_mulhi(int mc)
 {
 #if defined(__HIP_DEVICE_COMPILE__)
-    const unsigned hi = __umulhi(static_cast<unsigned>(mp), kGMagic);
+    return __mulhi(mc, kGMagic);
 #else
-    const unsigned hi = static_cast<unsigned>((static_cast<unsigned long long>(static_cast<unsigned>(mp)) * kGMagic) >> 32);
+    return static_cast<int>((static_cast<long long>(mc) * kGMagic) >> 32);
 #endif
-    return static_cast<int>(hi >> 15) - 172;
 }
 
-__device__ __forceinline__ ChromaTerms chroma_terms(int u, int v)
+// 24-bit multiply of one sign-extended int16 half of a packed sample word by
+// an SGPR constant: v_mul_i32_i24 with an SDWA source select, so the sample is
+// never unpacked into its own register.
+template <int kHalf>
+__device__ __forceinline__ int mul24_half(uint32_t w, int k)
 {
+    int r;
+    if constexpr (kHalf == 0)
+        asm("v_mul_i32_i24_sdwa %0, sext(%1), %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:DWORD"
+            : "=v"(r) : "v"(w), "s"(k));
+    else
+        asm("v_mul_i32_i24_sdwa %0, sext(%1), %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD"
+            : "=v"(r) : "v"(w), "s"(k));
+    return r;
+}
+
+template <int kHalf>
+__device__ __forceinline__ int half_of(uint32_t w)
+{
+    return kHalf == 0 ? static_cast<short>(w) : static_cast<int>(w) >> 16;
+}
+
+// Chroma terms of the (U,V) sample held in int16 half kHalf of the packed
+// words uw, vw.  V goes through SDWA multiplies only; U is unpacked once for
+// the two 24-bit multiply-adds (B, and G's sum).
+template <int kHalf>
+__device__ __forceinline__ ChromaTerms chroma_terms(uint32_t uw, uint32_t vw)
+{
+    const int u = half_of<kHalf>(uw);
     ChromaTerms t;
-    t.rq = r_term(v);
-    t.bq = b_term(u);
-    const int mp = g_mprime(u, v);
-    t.gq = g_term_from_m(mp);
-    t.special = mp == kGSpecial;
+    t.r = static_cast<uint32_t>(mul24_half<kHalf>(vw, kRK));
+    t.b = static_cast<uint32_t>(mul24(u, kBK) + kBBias);
+    t.g = static_cast<uint32_t>(g_mulhi(mul24(u, kGKu) + mul24_half<kHalf>(vw, kGKv)));
     return t;
 }
+
+// G flag: the mulhi's low half is 0xffff only at the exact negative quotients
+__device__ __forceinline__ bool g_flagged(const ChromaTerms& t) { return static_cast<uint16_t>(t.g) == 0xffffu; }
 
 // ---- packed (2 x int16 per VGPR) pixel math ---------------------------------
 typedef short s16x2 __attribute__((ext_vector_type(2)));
@@ -172,17 +201,9 @@ __device__ __forceinline__ uint32_t pk_add16(uint32_t a, uint32_t b)
     return __builtin_bit_cast(uint32_t, __builtin_bit_cast(s16x2, a) + __builtin_bit_cast(s16x2, b));
 }
 
-__device__ __forceinline__ uint32_t pk_clamp_u8(uint32_t a)
-{
-    s16x2 x = __builtin_bit_cast(s16x2, a);
-    x = __builtin_elementwise_max(x, (s16x2){0, 0});
-    x = __builtin_elementwise_min(x, (s16x2){255, 255});
-    return __builtin_bit_cast(uint32_t, x);
-}
-
 // v_sat_pk_u8_i16: two int16 lanes saturated to [0,255] and packed into bytes
 // 0 (low lane) and 1 (high lane) -- the clamp255 of src/macro.h:121-126 for two
-// pixels in one instruction (replaces a packed max + min).
+// pixels in one instruction.
 __device__ __forceinline__ uint32_t sat_pk_u8(uint32_t a)
 {
     uint32_t r;
@@ -196,50 +217,59 @@ __device__ __forceinline__ uint32_t perm(uint32_t s0, uint32_t s1, uint32_t sel)
     return __builtin_amdgcn_perm(s0, s1, sel);
 }
 constexpr uint32_t kSelLoLo = 0x05040100u;   // (s1.lo16) | (s0.lo16 << 16)
+constexpr uint32_t kSelHiHi = 0x07060302u;   // (s1.hi16) | (s0.hi16 << 16)
 
 // The chroma terms of two pixels as int16 pairs (low half = first pixel).
 struct ChromaPair {
     uint32_t r, g, b;
-    int special;      // either pixel's chroma is the (U,V) = (-200,200) corner
+    int flagged;      // either pixel's G term needs the corrected path
 };
 
 __device__ __forceinline__ ChromaPair pair_of(const ChromaTerms& c0, const ChromaTerms& c1)
 {
     ChromaPair p;
-    p.r = perm(c1.rq, c0.rq, kSelLoLo);
-    p.g = perm(c1.gq, c0.gq, kSelLoLo);
-    p.b = perm(c1.bq, c0.bq, kSelLoLo);
-    p.special = c0.special | c1.special;
+    p.r = perm(c1.r, c0.r, kSelHiHi);
+    p.g = perm(c1.g, c0.g, kSelHiHi);
+    p.b = perm(c1.b, c0.b, kSelHiHi);
+    p.flagged = g_flagged(c0) | g_flagged(c1);
     return p;
 }
 
-// Two BGRX pixels from an int16 pair of Y samples (low half first) and their
-// chroma pair.  kCheckSpecial adds the reference's double-rounding corner
-// (G one lower for (U,V) = (-200,200), Y in [188,201]); callers take that path
-// only when some lane of the wave needs it.
-template <bool kCheckSpecial>
-__device__ __forceinline__ void pixels2(uint32_t ypair, const ChromaPair& c, const ChromaTerms* c0,
+// G-term correction of one flagged pixel (see the block comment above).
+__device__ __forceinline__ short g_fix(const ChromaTerms& c, int ys)
+{
+    if (!g_flagged(c)) return 0;
+    const bool corner = static_cast<int>(c.g) >> 16 == kGCornerQ && static_cast<unsigned>(ys - kGCornerYs0) < 14u;
+    return corner ? 0 : 1;
+}
+
+// Two BGRX pixels from an int16 pair of level-shifted luma samples Ys = Y+128
+// (low half first) and their chroma pair.  kCheck applies g_fix; callers take
+// that path only when some lane of the wave has a flagged pixel.
+template <bool kCheck>
+__device__ __forceinline__ void pixels2(uint32_t yspair, const ChromaPair& c, const ChromaTerms* c0,
                                         const ChromaTerms* c1, uint32_t& px0, uint32_t& px1)
 {
-    const uint32_t R = sat_pk_u8(pk_add16(ypair, c.r));   // bytes r0 r1
-    uint32_t graw = pk_add16(ypair, c.g);
-    if constexpr (kCheckSpecial) {
-        const int y0 = static_cast<short>(ypair), y1 = static_cast<int>(ypair) >> 16;
-        const short d0 = (c0->special && static_cast<unsigned>(y0 - 188) < 14u) ? 1 : 0;
-        const short d1 = (c1->special && static_cast<unsigned>(y1 - 188) < 14u) ? 1 : 0;
-        graw = __builtin_bit_cast(uint32_t, __builtin_bit_cast(s16x2, graw) - (s16x2){d0, d1});
+    const uint32_t R = sat_pk_u8(pk_add16(yspair, c.r));   // bytes r0 r1
+    uint32_t graw = pk_add16(yspair, c.g);
+    if constexpr (kCheck) {
+        const short d0 = g_fix(*c0, static_cast<short>(yspair));
+        const short d1 = g_fix(*c1, static_cast<int>(yspair) >> 16);
+        graw = __builtin_bit_cast(uint32_t, __builtin_bit_cast(s16x2, graw) + (s16x2){d0, d1});
     }
     const uint32_t G = sat_pk_u8(graw);                   // bytes g0 g1
-    const uint32_t B = sat_pk_u8(pk_add16(ypair, c.b));   // bytes b0 b1
+    const uint32_t B = sat_pk_u8(pk_add16(yspair, c.b));   // bytes b0 b1
     const uint32_t T = perm(G, B, 0x05010400u);           // b0 g0 b1 g1
     px0 = perm(R, T, 0x0c040100u);                        // b0 g0 r0 0
     px1 = perm(R, T, 0x0c050302u);                        // b1 g1 r1 0
 }
 
-// Scalar form (one pixel) on top of the same code, for the colour test hooks.
-__device__ __forceinline__ uint32_t pixel_bgrx(int y, const ChromaTerms& t)
+// Scalar form (one pixel, raw Y/U/V) on top of the same code, for the colour test hooks.
+__device__ __forceinline__ uint32_t pixel_bgrx(int y, int u, int v)
 {
-    const uint32_t yp = perm(static_cast<uint32_t>(y), static_cast<uint32_t>(y), kSelLoLo);
+    const ChromaTerms t = chroma_terms<0>(static_cast<uint32_t>(u), static_cast<uint32_t>(v));
+    const uint32_t ys = static_cast<uint32_t>(y + kLumaLevel);
+    const uint32_t yp = perm(ys, ys, kSelLoLo);
     uint32_t p0, p1;
     pixels2<true>(yp, pair_of(t, t), &t, &t, p0, p1);
     return p0;

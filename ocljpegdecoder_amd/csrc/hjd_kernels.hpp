@@ -143,14 +143,28 @@ constexpr int kVarWgInterleave = 2;
 // tools/build_native.py --ablation); their outputs are deliberately wrong.
 constexpr int kAblNoStore = 4, kAblNoColour = 8, kAblNoIdct = 16;
 
-// 4 horizontally adjacent BGRX pixels.  kFull: the whole strip row lies inside
-// the frame and rows are 16-byte aligned -> one global_store_dwordx4 (nt by
-// default: the output is streamed and never re-read by the kernel).
+// 4 horizontally adjacent BGRX pixels at row + loff.  `row` is wave-uniform
+// (SGPRs) and loff a 32-bit per-lane byte offset, so the store uses the
+// scalar-base addressing form (no 64-bit address arithmetic per row).  kFull:
+// the whole strip row lies inside the frame and rows are 16-byte aligned ->
+// one global_store_dwordx4 (nt by default: the output is streamed and never
+// re-read by the kernel); otherwise per-pixel guarded dword stores (x = the
+// first pixel's column).
 template <bool kFull, int kVariant = 0>
-__device__ __forceinline__ void store4(uint8_t* __restrict__ row, int x, int width, uint32_t p0, uint32_t p1,
-                                       uint32_t p2, uint32_t p3)
+__device__ __forceinline__ void store4(uint8_t* __restrict__ row, uint32_t loff, int x, int width, uint32_t p0,
+                                       uint32_t p1, uint32_t p2, uint32_t p3)
 {
-    uint32_t* dst = reinterpret_cast<uint32_t*>(row) + x;
+    // Pin the row base in SGPRs as a global (addrspace 1) pointer and the lane
+    // offset as a 32-bit VGPR in this block: otherwise LLVM hoists
+    // base + zext(loff) into a 64-bit VGPR value (whose zero high half the
+    // per-block instruction selector cannot see) and adds each row's offset
+    // to it with VALU ops instead of using the scalar-base store form.
+    typedef __attribute__((address_space(1))) uint8_t gbyte;
+    typedef __attribute__((address_space(1))) uint32_t gword;
+    gbyte* grow = (gbyte*)row;
+    asm("" : "+s"(grow));
+    asm("" : "+v"(loff));
+    gword* dst = (gword*)(grow + loff);
     if constexpr ((kVariant & kAblNoStore) != 0) {
         asm volatile("" ::"v"(p0), "v"(p1), "v"(p2), "v"(p3));
         return;
@@ -158,10 +172,11 @@ __device__ __forceinline__ void store4(uint8_t* __restrict__ row, int x, int wid
     if constexpr (kFull) {
         typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
         const u32x4 v = {p0, p1, p2, p3};
+        typedef __attribute__((address_space(1))) u32x4 gvec;
         if constexpr (kVariant & kVarPlainStores)
-            *reinterpret_cast<u32x4*>(dst) = v;
+            *(gvec*)dst = v;
         else
-            __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst));
+            __builtin_nontemporal_store(v, (gvec*)dst);
     } else {
         if (x + 0 < width) dst[0] = p0;
         if (x + 1 < width) dst[1] = p1;
@@ -170,22 +185,26 @@ __device__ __forceinline__ void store4(uint8_t* __restrict__ row, int x, int wid
     }
 }
 
-// Colour stage of one task (samples are int16, row-major, in the block slots).
+// Colour stage of one task (samples are int16, row-major, in the block slots;
+// luma level-shifted by +128 by its IDCT, chroma raw).
 // Each lane owns 4 px x 2 rows.  4:2:0: one chroma row serves both pixel rows
 // (nearest 2x2 replication, src/decoder.cpp:474-483), chroma terms are computed
 // once per chroma sample; 4 iterations cover the 128x16 strip and every wave
 // store instruction writes two 512-byte row segments.  4:4:4: the same lane
 // shape over the 128x8 strip, chroma per pixel (src/decoder.cpp:457-471).
-// Pixel math is packed: two pixels per int16x2 VGPR (pixels2).
+// Pixel math is packed: two pixels per int16x2 VGPR (pixels2).  Row addresses:
+// row 4*it + h of the strip is wave-uniform; lanes 32-63 sit two rows lower,
+// which is folded into their 32-bit lane offset.
 template <bool kCheck, int kVariant, bool kFull>
-__device__ __forceinline__ void emit_row4(uint8_t* __restrict__ row, int xa, int width, uint32_t y01, uint32_t y23,
-                                          const ChromaPair& p01, const ChromaPair& p23, const ChromaTerms* c0,
-                                          const ChromaTerms* c1, const ChromaTerms* c2, const ChromaTerms* c3)
+__device__ __forceinline__ void emit_row4(uint8_t* __restrict__ row, uint32_t loff, int xa, int width, uint32_t y01,
+                                          uint32_t y23, const ChromaPair& p01, const ChromaPair& p23,
+                                          const ChromaTerms* c0, const ChromaTerms* c1, const ChromaTerms* c2,
+                                          const ChromaTerms* c3)
 {
     uint32_t q0, q1, q2, q3;
     pixels2<kCheck>(y01, p01, c0, c1, q0, q1);
     pixels2<kCheck>(y23, p23, c2, c3, q2, q3);
-    store4<kFull, kVariant>(row, xa, width, q0, q1, q2, q3);
+    store4<kFull, kVariant>(row, loff, xa, width, q0, q1, q2, q3);
 }
 
 template <int kSampling, bool kFull, int kVariant>
@@ -195,6 +214,9 @@ __device__ __forceinline__ void colour_stage(const char* __restrict__ slots, int
     const int cg = lane & 31;     // 4-pixel column group within the 128-px strip
     const int x0 = cg * 4;
     const int xa = x_base + x0;
+    const int ylane = 2 * (lane >> 5);   // this half-wave's row offset
+    const uint32_t loff = static_cast<uint32_t>(x0 * 4) + static_cast<uint32_t>(ylane) * static_cast<uint32_t>(pitch);
+    uint8_t* const strip = out + static_cast<int64_t>(y_base) * pitch + static_cast<int64_t>(x_base) * 4;
     if constexpr (kSampling == 1) {
         const int m = cg >> 2;        // MCU within strip
         const int xm = x0 & 15;       // x within MCU: 0,4,8,12
@@ -206,24 +228,25 @@ __device__ __forceinline__ void colour_stage(const char* __restrict__ slots, int
             const int2 ya = *reinterpret_cast<const int2*>(yblk + (y0 & 7) * 16);
             const int2 yb = *reinterpret_cast<const int2*>(yblk + ((y0 + 1) & 7) * 16);
             const int coff = p * 16 + (xm >> 1) * 2;
-            const int cu = *reinterpret_cast<const int*>(slots + (m * 6 + 4) * kSlotBytes + coff);
-            const int cv = *reinterpret_cast<const int*>(slots + (m * 6 + 5) * kSlotBytes + coff);
-            const ChromaTerms c0 = chroma_terms(static_cast<short>(cu), static_cast<short>(cv));
-            const ChromaTerms c1 = chroma_terms(cu >> 16, cv >> 16);
+            const uint32_t cu = *reinterpret_cast<const uint32_t*>(slots + (m * 6 + 4) * kSlotBytes + coff);
+            const uint32_t cv = *reinterpret_cast<const uint32_t*>(slots + (m * 6 + 5) * kSlotBytes + coff);
+            const ChromaTerms c0 = chroma_terms<0>(cu, cv);
+            const ChromaTerms c1 = chroma_terms<1>(cu, cv);
             const ChromaPair p0 = pair_of(c0, c0), p1 = pair_of(c1, c1);
             const int ya0 = y_base + y0;
-            uint8_t* row0 = out + static_cast<int64_t>(ya0) * pitch;
-            if (__builtin_amdgcn_ballot_w64((p0.special | p1.special) != 0)) {   // wave-uniform, rare
+            uint8_t* row0 = strip + static_cast<int64_t>(4 * it) * pitch;   // wave-uniform
+            if (__builtin_amdgcn_ballot_w64((p0.flagged | p1.flagged) != 0)) {   // wave-uniform, rare
                 if (kFull || ya0 < height)
-                    emit_row4<true, kVariant, kFull>(row0, xa, width, ya.x, ya.y, p0, p1, &c0, &c0, &c1, &c1);
+                    emit_row4<true, kVariant, kFull>(row0, loff, xa, width, ya.x, ya.y, p0, p1, &c0, &c0, &c1, &c1);
                 if (kFull || ya0 + 1 < height)
-                    emit_row4<true, kVariant, kFull>(row0 + pitch, xa, width, yb.x, yb.y, p0, p1, &c0, &c0, &c1, &c1);
+                    emit_row4<true, kVariant, kFull>(row0 + pitch, loff, xa, width, yb.x, yb.y, p0, p1, &c0, &c0, &c1,
+                                                     &c1);
             } else {
                 if (kFull || ya0 < height)
-                    emit_row4<false, kVariant, kFull>(row0, xa, width, ya.x, ya.y, p0, p1, &c0, &c0, &c1, &c1);
+                    emit_row4<false, kVariant, kFull>(row0, loff, xa, width, ya.x, ya.y, p0, p1, &c0, &c0, &c1, &c1);
                 if (kFull || ya0 + 1 < height)
-                    emit_row4<false, kVariant, kFull>(row0 + pitch, xa, width, yb.x, yb.y, p0, p1, &c0, &c0, &c1,
-                                                      &c1);
+                    emit_row4<false, kVariant, kFull>(row0 + pitch, loff, xa, width, yb.x, yb.y, p0, p1, &c0, &c0,
+                                                      &c1, &c1);
             }
         }
     } else {
@@ -237,20 +260,22 @@ __device__ __forceinline__ void colour_stage(const char* __restrict__ slots, int
                 const int y = 2 * p + h;
                 const char* base = slots + m * 3 * kSlotBytes + y * 16 + xm * 2;
                 const int2 sy = *reinterpret_cast<const int2*>(base);
-                const int2 su = *reinterpret_cast<const int2*>(base + kSlotBytes);
-                const int2 sv = *reinterpret_cast<const int2*>(base + 2 * kSlotBytes);
-                const ChromaTerms c0 = chroma_terms(static_cast<short>(su.x), static_cast<short>(sv.x));
-                const ChromaTerms c1 = chroma_terms(su.x >> 16, sv.x >> 16);
-                const ChromaTerms c2 = chroma_terms(static_cast<short>(su.y), static_cast<short>(sv.y));
-                const ChromaTerms c3 = chroma_terms(su.y >> 16, sv.y >> 16);
+                const uint2 su = *reinterpret_cast<const uint2*>(base + kSlotBytes);
+                const uint2 sv = *reinterpret_cast<const uint2*>(base + 2 * kSlotBytes);
+                const ChromaTerms c0 = chroma_terms<0>(su.x, sv.x);
+                const ChromaTerms c1 = chroma_terms<1>(su.x, sv.x);
+                const ChromaTerms c2 = chroma_terms<0>(su.y, sv.y);
+                const ChromaTerms c3 = chroma_terms<1>(su.y, sv.y);
                 const ChromaPair p01 = pair_of(c0, c1), p23 = pair_of(c2, c3);
                 const int ya = y_base + y;
-                uint8_t* row = out + static_cast<int64_t>(ya) * pitch;
+                uint8_t* row = strip + static_cast<int64_t>(4 * it + h) * pitch;   // wave-uniform
                 if (kFull || ya < height) {
-                    if (__builtin_amdgcn_ballot_w64((p01.special | p23.special) != 0))
-                        emit_row4<true, kVariant, kFull>(row, xa, width, sy.x, sy.y, p01, p23, &c0, &c1, &c2, &c3);
+                    if (__builtin_amdgcn_ballot_w64((p01.flagged | p23.flagged) != 0))
+                        emit_row4<true, kVariant, kFull>(row, loff, xa, width, sy.x, sy.y, p01, p23, &c0, &c1, &c2,
+                                                         &c3);
                     else
-                        emit_row4<false, kVariant, kFull>(row, xa, width, sy.x, sy.y, p01, p23, &c0, &c1, &c2, &c3);
+                        emit_row4<false, kVariant, kFull>(row, loff, xa, width, sy.x, sy.y, p01, p23, &c0, &c1, &c2,
+                                                          &c3);
                 }
             }
         }
@@ -264,9 +289,8 @@ __device__ __forceinline__ constexpr int round_component(int i)
     return kSampling == 1 ? (i < 4 ? 0 : i - 3) : (i % 3);
 }
 
-// IDCT of the task's 48 blocks (6 rounds).  kFmt 0: int16 zigzag staged in the
-// LDS slots; kFmt 1: int32 natural rows read straight from global memory.
-// Samples end up as int16 row-major in the block slots.
+// One round's row-pass inputs.  kFmt 0: int16 zigzag staged in the LDS slots
+// (dequant fused); kFmt 1: int32 natural rows read straight from global memory.
 template <int kSampling, int kFmt>
 __device__ __forceinline__ void load_round(const char* __restrict__ slots, int lane, int i, const int (&zoff)[8],
                                            const uint32_t (&q)[3][4], const int* __restrict__ src32, int nblk,
@@ -298,7 +322,7 @@ __device__ __forceinline__ void load_round(const char* __restrict__ slots, int l
 
 // IDCT of the task's 48 blocks (6 rounds).  kFmt 0: int16 zigzag staged in the
 // LDS slots; kFmt 1: int32 natural rows read straight from global memory.
-// Samples end up as int16 row-major in the block slots.  The next round's
+// Samples end up as int16 row-major in the block slots (luma as Y + 128).  The next round's
 // coefficient gathers are issued before this round's column math, so their
 // LDS latency overlaps it.
 template <int kSampling, int kFmt>
@@ -326,7 +350,10 @@ __device__ __forceinline__ void idct_stage(char* __restrict__ slots, char* __res
             for (int k = 0; k < 8; ++k) c8[k] = *reinterpret_cast<const int*>(col + k * kRowStride);
         }
         if (i + 1 < 6) load_round<kSampling, kFmt>(slots, lane, i + 1, zoff, q, src32, nblk, v);
-        idct8<true>(c8);
+        if (round_component<kSampling>(i) == 0)
+            idct8<true, kLumaLevel>(c8);   // luma leaves the IDCT level-shifted (Ys = Y + 128)
+        else
+            idct8<true>(c8);
         {
             char* blk = slots + b * kSlotBytes + r * 2;   // column r
 #pragma unroll
@@ -502,7 +529,7 @@ __global__ void csc_kernel(const int* __restrict__ y, const int* __restrict__ u,
 {
     for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
          i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-        out[i] = kMode == 0 ? pixel_bgrx(y[i], chroma_terms(u[i], v[i])) : pixel_bgrx_f64(y[i], u[i], v[i]);
+        out[i] = kMode == 0 ? pixel_bgrx(y[i], u[i], v[i]) : pixel_bgrx_f64(y[i], u[i], v[i]);
     }
 }
 
@@ -515,7 +542,7 @@ __global__ void csc_exhaustive_kernel(uint32_t* __restrict__ out)
         const int Y = static_cast<int>(i >> 18) - 256;
         const int U = static_cast<int>((i >> 9) & 511) - 256;
         const int V = static_cast<int>(i & 511) - 256;
-        out[i] = kMode == 0 ? pixel_bgrx(Y, chroma_terms(U, V)) : pixel_bgrx_f64(Y, U, V);
+        out[i] = kMode == 0 ? pixel_bgrx(Y, U, V) : pixel_bgrx_f64(Y, U, V);
     }
 }
 

@@ -94,38 +94,55 @@ def test_oracle_csc_exhaustive_hash():
     assert h.hexdigest() == O.manifest()["csc_exhaustive_sha256"]
 
 
-RK, RBIAS = 1470091, (128 << 20) + 1048
-BK, BBIAS = 1858077, (128 << 20) + 2097
-GOFF, GMAGIC, GSPECIAL = 15000000, 2814749768, 11300000
+# Constants of the device formulation (csrc/hjd_device.hpp colour block).
+LEVEL = 128                      # luma leaves the IDCT as Ys = Y + 128
+RK = 91881                       # floor(1.402 v) = (v * RK) >> 16
+BK, BBIAS = 116130, 52           # floor(1.772 u) = (u * BK + BBIAS) >> 16
+GSCALE = 128
+GKU, GKV = -17207 * GSCALE, -35707 * GSCALE
+GMAGIC = 43980466                # ceil(2^48 / (50000 * GSCALE))
+GCORNER_Q = -75
 
 
 def integer_csc(y, u, v):
-    """numpy model of the kernel's exact-integer colour formulation
-    (csrc/hjd_device.hpp r_term / b_term / g_mprime / g_term_from_m / pixels2)."""
+    """numpy model of the kernel's exact-integer colour formulation, op for op
+    (csrc/hjd_device.hpp chroma_terms / pair_of / g_fix / pixels2): every
+    chroma term is the high int16 of a 32-bit word."""
     y = y.astype(np.int64); u = u.astype(np.int64); v = v.astype(np.int64)
-    rq = (v * RK + RBIAS) >> 20                       # floor(1.402 v) + 128
-    bq = (u * BK + BBIAS) >> 20                       # floor(1.772 u) + 128
-    mp = -17207 * u - 35707 * v + GOFF
-    gq = ((mp.astype(np.uint64) * np.uint64(GMAGIC)) >> np.uint64(47)).astype(np.int64) - 172
-    special = (mp == GSPECIAL) & (y >= 188) & (y <= 201)
-    r = np.clip(y + rq, 0, 255)
-    g = np.clip(y + gq - special, 0, 255)
-    b = np.clip(y + bq, 0, 255)
+    ys = y + LEVEL
+    r = (v * RK) >> 16
+    b = (u * BK + BBIAS) >> 16
+    hi = ((u * GKU + v * GKV) * GMAGIC) >> 32       # v_mul_hi_i32
+    g = hi >> 16
+    flagged = (hi & 0xFFFF) == 0xFFFF
+    corner = (g == GCORNER_Q) & (ys >= 188 + LEVEL) & (ys <= 201 + LEVEL)
+    g = g + (flagged & ~corner)
+    r = np.clip(ys + r, 0, 255)
+    g = np.clip(ys + g, 0, 255)
+    b = np.clip(ys + b, 0, 255)
     return ((r << 16) | (g << 8) | b).astype(np.uint32)
 
 
 def test_fixed_point_colour_terms():
     """The constants of the device formulation, exhaustively on their domains."""
     x = np.arange(-256, 256, dtype=np.int64)
-    assert ((x * RK + RBIAS) >> 20 == np.floor_divide(701 * x, 500) + 128).all()
-    assert ((x * BK + BBIAS) >> 20 == np.floor_divide(443 * x, 250) + 128).all()
-    assert RK < 2 ** 23 and BK < 2 ** 23 and 256 * max(RK, BK) + RBIAS + 4096 < 2 ** 31   # 24-bit multiply, no overflow
-    m = np.arange(0, 1 << 25, dtype=np.uint64)
-    assert ((m * np.uint64(GMAGIC)) >> np.uint64(47) == m // 50000).all()
+    assert ((x * RK) >> 16 == np.floor_divide(701 * x, 500)).all()
+    assert ((x * BK + BBIAS) >> 16 == np.floor_divide(443 * x, 250)).all()
+    assert max(RK, BK, -GKU, -GKV) < 2 ** 23        # 24-bit signed multiplies
+    assert GMAGIC < 2 ** 31 and GMAGIC == -(-(1 << 48) // (50000 * GSCALE))
     u, v = np.meshgrid(x, x, indexing="ij")
-    mp = -17207 * u - 35707 * v + GOFF
-    assert mp.min() >= 0 and mp.max() < 2 ** 25
-    assert np.argwhere(mp == GSPECIAL).tolist() == [[56, 456]]   # (U,V) = (-200, 200) only
+    mc = u * GKU + v * GKV
+    assert np.abs(mc).max() < 2 ** 31                # fits the int32 mulhi operand
+    hi = (mc * GMAGIC) >> 32
+    q = hi >> 16
+    exact = np.floor_divide(-(17207 * u + 35707 * v), 50000)
+    flagged = (hi & 0xFFFF) == 0xFFFF
+    # the mulhi is the floor everywhere except at the flagged points, where it
+    # is one below; the flag marks exactly (U,V) = (-200,200) and (-100,100)
+    assert (q[~flagged] == exact[~flagged]).all()
+    assert (q[flagged] == exact[flagged] - 1).all()
+    assert sorted(map(tuple, (np.argwhere(flagged) - 256).tolist())) == [(-200, 200), (-100, 100)]
+    assert (hi & 0xFFFF)[~flagged].max() <= 0xFFFE
 
 
 def test_integer_csc_formulation_is_exact():
