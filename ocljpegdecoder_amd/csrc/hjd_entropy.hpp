@@ -111,8 +111,15 @@ __host__ __device__ __forceinline__ SubStats stats_combine(const SubStats& a, co
 }
 
 // ---- decoder state --------------------------------------------------------
-// bits 0-31 pos, 32-38 z, 39-41 j, 42-63 segment index (a hint, not compared)
-constexpr uint64_t kStateMask = (1ull << 42) - 1;
+// bits 0-31 pos, 32-38 z, 39-41 j, 42-63 restart-interval (segment) index.
+// States compare in full: a run is a deterministic function of all 64 bits,
+// which is what makes "two chains that agree at a boundary agree from there
+// on" hold.  The segment index is not redundant: a run from a wrong entry can
+// decode through a restart pad as data and stop past the segment end without
+// taking the restart, leaving (pos, z, j) that may coincide with the true
+// state's but a stale segment index (and DC predictors that were never
+// reset).  The one pair of equivalent states that differ only in the index,
+// a segment start seen from either side, costs at most one extra re-run.
 
 __host__ __device__ __forceinline__ uint64_t pack_state(uint32_t pos, uint32_t j, uint32_t z, uint32_t seg)
 {
@@ -123,7 +130,7 @@ __host__ __device__ __forceinline__ uint32_t st_pos(uint64_t s) { return static_
 __host__ __device__ __forceinline__ uint32_t st_z(uint64_t s) { return static_cast<uint32_t>(s >> 32) & 127; }
 __host__ __device__ __forceinline__ uint32_t st_j(uint64_t s) { return static_cast<uint32_t>(s >> 39) & 7; }
 __host__ __device__ __forceinline__ uint32_t st_seg(uint64_t s) { return static_cast<uint32_t>(s >> 42); }
-__host__ __device__ __forceinline__ bool same_state(uint64_t a, uint64_t b) { return ((a ^ b) & kStateMask) == 0; }
+__host__ __device__ __forceinline__ bool same_state(uint64_t a, uint64_t b) { return a == b; }
 
 __host__ __device__ __forceinline__ uint32_t bswap32(uint32_t x)
 {

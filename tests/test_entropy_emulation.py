@@ -15,14 +15,17 @@ import pytest
 import oracle_py as O
 
 
-def _pil(w, h, q, sub, seed, noise=20.0, **kw):
+def _pil(w, h, q, sub, seed, noise=20.0, gray=False, **kw):
     from PIL import Image
     rng = np.random.default_rng(seed)
     x = np.linspace(0, 255, w)[None, :, None]
     y = np.linspace(0, 255, h)[:, None, None]
     img = np.clip(x * [1, 0, 0.5] + y * [0, 1, 0.5] + rng.normal(0, noise, (h, w, 3)), 0, 255).astype(np.uint8)
+    im = Image.fromarray(img)
+    if gray:
+        im = im.convert("L")
     b = io.BytesIO()
-    Image.fromarray(img).save(b, format="JPEG", quality=q, subsampling=sub, **kw)
+    im.save(b, format="JPEG", quality=q, subsampling=sub, **kw)
     return b.getvalue()
 
 
@@ -59,6 +62,12 @@ CASES = [
     ("640x480 optimized", dict(w=640, h=480, q=75, sub=2, optimize=True)),
     ("1x1", dict(w=1, h=1, q=90, sub=2)),
     ("17x9 DRI 1", dict(w=17, h=9, q=90, sub=0, restart_marker_blocks=1)),
+    # extensions: 4:2:2 and one-component scans
+    ("640x480 q90 4:2:2", dict(w=640, h=480, q=90, sub=1)),
+    ("333x77 4:2:2 DRI 2", dict(w=333, h=77, q=85, sub=1, restart_marker_blocks=2)),
+    ("640x480 q90 gray", dict(w=640, h=480, q=90, sub=0, gray=True)),
+    ("333x77 gray DRI 7", dict(w=333, h=77, q=70, sub=0, gray=True, restart_marker_blocks=7)),
+    ("9x17 gray", dict(w=9, h=17, q=95, sub=0, gray=True)),
 ]
 
 
@@ -75,7 +84,11 @@ def test_synthetic(hjd, name, kw, sub_bits):
 
 def test_random_sweep(hjd):
     """Seeded random files x subsequence sizes, including pure-noise content
-    (the worst case for self-synchronisation)."""
+    (the worst case for self-synchronisation), all four samplings.  This sweep
+    found the stale-segment-index convergence bug (csrc/hjd_entropy.hpp
+    same_state): a 158x82 4:2:2 file with a 2-MCU restart interval at S=32,
+    where a wrong chain crossed a restart pad as data and met the true
+    (pos, z, j) with the previous segment's index."""
     from PIL import Image
     rng = np.random.default_rng(2024)
     done = 0
@@ -90,9 +103,11 @@ def test_random_sweep(hjd):
         img = (rng.integers(0, 256, (h, w, 3), dtype=np.uint8) if rng.integers(0, 3) == 0 else
                np.clip(rng.normal(128, rng.uniform(0, 60), (h, w, 3)), 0, 255).astype(np.uint8))
         b = io.BytesIO()
+        im = Image.fromarray(img)
+        if rng.integers(0, 6) == 0:
+            im = im.convert("L")
         try:
-            Image.fromarray(img).save(b, format="JPEG", quality=int(rng.integers(20, 101)),
-                                      subsampling=int(rng.choice([0, 2])), **kw)
+            im.save(b, format="JPEG", quality=int(rng.integers(20, 101)), subsampling=int(rng.choice([0, 1, 2])), **kw)
         except OSError:
             continue
         data = b.getvalue()
