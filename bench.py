@@ -45,6 +45,10 @@ WORKLOADS = {
                   desc="BASELINE configs[2]: batch of 1024 synthetic 3840x2160 4:2:0 frames, persistent kernel"),
     "4k444": dict(width=3840, height=2160, sampling=0, frames=1024,
                   desc="BASELINE configs[3]: batch of 1024 synthetic 3840x2160 4:4:4 frames, persistent kernel"),
+    "4k422": dict(width=3840, height=2160, sampling=3, frames=1024,
+                  desc="extension (SURVEY s8(f) rank 4): batch of 1024 synthetic 3840x2160 4:2:2 frames"),
+    "4kgray": dict(width=3840, height=2160, sampling=4, frames=1024,
+                   desc="extension (SURVEY s8(f) rank 4): batch of 1024 synthetic 3840x2160 grayscale frames"),
     "fhd420": dict(width=1920, height=1080, sampling=1, frames=1,
                    desc="BASELINE configs[1]: single 1920x1080 4:2:0 frame, one launch (cache/launch bound)"),
     "stream4k420": dict(width=3840, height=2160, sampling=1, frames=1024, entropy="gpu",
@@ -82,7 +86,10 @@ ZIGZAG = [0, 1, 8, 16, 9, 2, 3, 10, 17, 24, 32, 25, 18, 11, 4, 5,
           58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63]
 
 
-def synth_frame_gpu(torch, nblk, bpm, qt, seed, device):
+SAMPLING_NAMES = {0: "4:4:4", 1: "4:2:0", 3: "4:2:2", 4: "gray"}
+
+
+def synth_frame_gpu(torch, nblk, sampling, qt, seed, device):
     """Synthetic quantised zigzag coefficients for one frame, on the device:
     smooth+noise 8x8 sample blocks in [-128,127] -> float FDCT -> quantise
     (q=90-like tables).  Bounded samples keep the data in the reference's legal
@@ -100,7 +107,8 @@ def synth_frame_gpu(torch, nblk, bpm, qt, seed, device):
     F = torch.einsum("ux,nxy,vy->nuv", m, pix, m).reshape(nblk, 64)
     qnat = torch.zeros((3, 64), device=device)
     qnat[:, torch.tensor(ZIGZAG, device=device)] = torch.from_numpy(qt).float().to(device)
-    comp = torch.tensor([0] * (bpm - 2) + [1, 2], device=device).repeat(nblk // bpm)
+    import ocljpegdecoder_amd as hjd
+    comp = torch.from_numpy(hjd.block_components(sampling, nblk)).to(device)
     coef_nat = torch.round(F / qnat[comp])
     return coef_nat[:, torch.tensor(ZIGZAG, device=device)].to(torch.int16).contiguous()
 
@@ -127,10 +135,10 @@ def cpu_baseline(coef_pool_host, qt, wl, frames_done_gpu_rate):
     dt = time.perf_counter() - t0
     assert rc == 0
     res = {"value": round(nframes * w * h / dt / 1e6, 2), "unit": "Mpixels/s", "cores": nthreads, "kind": "port",
-           "sample": f"{nframes} frames {w}x{h} {'4:2:0' if s == 1 else '4:4:4'} (pool of {pool.shape[0]}), "
+           "sample": f"{nframes} frames {w}x{h} {SAMPLING_NAMES[s]} (pool of {pool.shape[0]}), "
                      f"int16 zigzag -> BGRX in RAM, {nthreads} threads, {dt:.2f} s wall",
            "cpu_model": _cpu_model(), "nproc": os.cpu_count()}
-    if O.ref_available():
+    if O.ref_available() and s in (0, 1):   # the reference rejects other samplings
         try:
             lib_ref = O.ref()
             lib_ref.ref_decode_mcu_data.argtypes = [O.i32p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
@@ -278,7 +286,7 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
             "data": "synthetic JPEG files (Pillow q90, gradient + sigma-20 noise), pool of 16 per rank, "
                     f"{nf} frames per step per GPU",
             "config": {"workload": wl["desc"], "frames_per_gpu_per_step": nf, "width": w, "height": h,
-                       "sampling": "4:2:0" if s == 1 else "4:4:4", "host_threads_per_gpu": nthreads,
+                       "sampling": SAMPLING_NAMES[s], "host_threads_per_gpu": nthreads,
                        "entropy_decode": "gpu" if gpu_entropy else "host", "mean_jpeg_bytes": jpeg_bytes,
                        "output": "pinned host memory (D2H-on)" if d2h else "BGRX in HBM (D2H-off)",
                        "parallelism": f"image-parallel x{world} (no collective)"},
@@ -344,7 +352,7 @@ def main():
     npool = min(POOL, nf)
     coefs = torch.empty((nf, nblk, 64), dtype=torch.int16, device=dev)
     for i in range(npool):
-        coefs[i] = synth_frame_gpu(torch, nblk, bpm, qt, seed=1000 * rank + i, device=dev)
+        coefs[i] = synth_frame_gpu(torch, nblk, s, qt, seed=1000 * rank + i, device=dev)
     for i in range(npool, nf):
         coefs[i].copy_(coefs[i % npool])
     out = torch.empty((nf, h, w), dtype=torch.int32, device=dev)
@@ -421,7 +429,7 @@ def main():
             "data": "synthetic (device-generated FDCT+quantised smooth+noise blocks, pool of "
                     f"{npool} distinct frames replicated to {nf}); inputs resident in HBM",
             "config": {"workload": wl["desc"], "frames_per_gpu": nf, "width": w, "height": h,
-                       "sampling": "4:2:0" if s == 1 else "4:4:4", "input": "int16 quantised zigzag + qtables",
+                       "sampling": SAMPLING_NAMES[s], "input": "int16 quantised zigzag + qtables",
                        "output": "BGRX 4 B/px in HBM", "parallelism": f"image-parallel x{world} (no collective)",
                        "tasks_per_launch": plan.tasks},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",

@@ -35,9 +35,14 @@ enum hjd_status {
     HJD_E_STATE = -5      /* call out of sequence (e.g. run before upload) */
 };
 
-/* Chroma sampling; numerically equal to the reference's ColorSpace enum
- * (src/macro.h:114-119: YUV444 = 0, YUV411 = 1 (really H2V2 4:2:0), Other = 2). */
-enum hjd_sampling { HJD_YUV444 = 0, HJD_YUV420 = 1, HJD_OTHER = 2 };
+/* Chroma sampling.  0..2 are numerically equal to the reference's ColorSpace
+ * enum (src/macro.h:114-119: YUV444 = 0, YUV411 = 1 (really H2V2 4:2:0),
+ * Other = 2).  HJD_YUV422 (Y H2V1, chroma H1V1) and HJD_GRAY (one component)
+ * are extensions the reference rejects (src/decoder.cpp:58-69; SURVEY.md
+ * s8(f) rank 4): the same IDCT and the same colour arithmetic with nearest
+ * (horizontal) chroma replication, and R = G = B = clamp(Y + 128) for gray
+ * (the reference's formula with U = V = 0). */
+enum hjd_sampling { HJD_YUV444 = 0, HJD_YUV420 = 1, HJD_OTHER = 2, HJD_YUV422 = 3, HJD_GRAY = 4 };
 
 /* Coefficient input format. */
 enum hjd_input_format {
@@ -54,7 +59,9 @@ enum hjd_input_format {
 /*
  * One frame of a batch.  Blocks are MCU-major in raster MCU order; per MCU the
  * Y blocks in HxV raster order, then Cb, then Cr (src/decoder.cpp:286-344).
- * MCU grid: ceil(W/8)xceil(H/8) (4:4:4) or ceil(W/16)xceil(H/16) (4:2:0).
+ * MCU grid: ceil(W/8)xceil(H/8) (4:4:4, 3 blocks; gray, 1 block),
+ * ceil(W/16)xceil(H/16) (4:2:0, 6 blocks) or ceil(W/16)xceil(H/8) (4:2:2,
+ * 4 blocks).
  */
 typedef struct hjd_frame {
     uint64_t coef_offset; /* first block's offset in the coef buffer, in BLOCKS */
@@ -62,7 +69,7 @@ typedef struct hjd_frame {
     int32_t width;        /* visible pixels (output is cropped to W x H) */
     int32_t height;
     int32_t out_pitch;    /* bytes per output row, >= 4*width, multiple of 4 */
-    int32_t sampling;     /* HJD_YUV444 or HJD_YUV420 */
+    int32_t sampling;     /* HJD_YUV444, HJD_YUV420, HJD_YUV422 or HJD_GRAY */
     int32_t qt_index[3];  /* per component (Y, Cb, Cr): index into the qtable set */
     int32_t reserved;     /* must be 0 */
 } hjd_frame;

@@ -32,7 +32,7 @@ extern "C" {
 typedef struct hjd_jpeg_info {
     int32_t width;
     int32_t height;
-    int32_t sampling;          /* HJD_YUV444 or HJD_YUV420 */
+    int32_t sampling;          /* HJD_YUV444, HJD_YUV420, HJD_YUV422 or HJD_GRAY */
     int32_t restart_interval;  /* MCUs per restart interval, 0 = none */
     int32_t mcu_w;             /* MCU grid */
     int32_t mcu_h;

@@ -14,8 +14,11 @@ from .backend import (  # noqa: E402
     IN_I32_NATURAL,
     IN_Q16_ZIGZAG,
     OTHER,
+    GRAY,
     YUV420,
+    YUV422,
     YUV444,
+    block_components,
     Context,
     FrameSpec,
     Plan,
@@ -33,5 +36,5 @@ __all__ = [
     "decode_coefs_batch", "decode_jpeg", "emulate_entropy",
     "parse",
     "Context", "FrameSpec", "Plan", "decode_frame", "device_count", "frame_blocks", "mcu_geometry",
-    "YUV444", "YUV420", "OTHER", "IN_Q16_ZIGZAG", "IN_I32_NATURAL",
+    "YUV444", "YUV420", "YUV422", "GRAY", "OTHER", "block_components", "IN_Q16_ZIGZAG", "IN_I32_NATURAL",
 ]

@@ -17,16 +17,28 @@ from ._lib import HjdFrame, check
 YUV444 = 0
 YUV420 = 1  # == the reference's ColorSpace::YUV411 (src/macro.h:114-119), H2V2
 OTHER = 2
+YUV422 = 3  # extension (Y H2V1), include/hjd.h
+GRAY = 4    # extension (one component), include/hjd.h
+
+# sampling -> (MCU px width, MCU px height, blocks per MCU, luma blocks per MCU)
+_GEOM = {YUV444: (8, 8, 3, 1), YUV420: (16, 16, 6, 4), YUV422: (16, 8, 4, 2), GRAY: (8, 8, 1, 1)}
 
 IN_Q16_ZIGZAG = 0
 IN_I32_NATURAL = 1
 
 
 def mcu_geometry(width: int, height: int, sampling: int):
-    """(mcu_w, mcu_h, blocks_per_mcu, mcu_px) -- src/decoder.cpp:161-192."""
-    mpx = 16 if sampling == YUV420 else 8
-    bpm = 6 if sampling == YUV420 else 3
-    return (width - 1) // mpx + 1, (height - 1) // mpx + 1, bpm, mpx
+    """(mcu_w, mcu_h, blocks_per_mcu, (mcu_px_w, mcu_px_h)) -- src/decoder.cpp:161-192."""
+    if sampling not in _GEOM:
+        raise ValueError(f"unsupported sampling {sampling}")
+    pw, ph, bpm, _ = _GEOM[sampling]
+    return (width - 1) // pw + 1, (height - 1) // ph + 1, bpm, (pw, ph)
+
+
+def block_components(sampling: int, nblocks: int) -> np.ndarray:
+    """Component (0 Y, 1 Cb, 2 Cr) of each block of an MCU-major block list."""
+    _, _, bpm, nluma = _GEOM[sampling]
+    return np.array(([0] * nluma + [1, 2][: bpm - nluma]) * (nblocks // bpm), dtype=np.int64)
 
 
 def frame_blocks(width: int, height: int, sampling: int) -> int:

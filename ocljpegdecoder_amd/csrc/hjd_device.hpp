@@ -231,7 +231,7 @@ __device__ __forceinline__ ChromaPair pair_of(const ChromaTerms& c0, const Chrom
     p.r = perm(c1.r, c0.r, kSelHiHi);
     p.g = perm(c1.g, c0.g, kSelHiHi);
     p.b = perm(c1.b, c0.b, kSelHiHi);
-    p.flagged = g_flagged(c0) | g_flagged(c1);
+    p.flagged = static_cast<int>(g_flagged(c0)) | static_cast<int>(g_flagged(c1));
     return p;
 }
 

@@ -125,6 +125,13 @@ int destuff(const uint8_t* p, const uint8_t* end, uint8_t* out, size_t cap, std:
     return HJD_OK;
 }
 
+// Pixel-kernel launch class of a sampling (parse_scan_header admits only known ones).
+inline int sampling_class(int sampling)
+{
+    hjd_internal::SamplingGeom g;
+    return hjd_internal::sampling_geom(sampling, &g) ? g.index : 0;
+}
+
 // Host-side result of preparing one JPEG.
 struct Prepared {
     int rc = HJD_OK;
@@ -684,10 +691,12 @@ struct hjd_gdec {
     // when d_outs is given); returns the device view (pointers into `blob`).
     int assemble(uint8_t* blob, int16_t* coefs, int64_t* block_offsets, void* const* d_outs, const int32_t* pitches,
                  EntBatchDev& d);
-    // pixel-kernel launch groups (0: 4:4:4, 1: 4:2:0)
-    int nrec[2] = {0, 0};
-    int64_t tasks[2] = {0, 0};
-    uint8_t* out_base[2] = {nullptr, nullptr};
+    // pixel-kernel launch groups, one per sampling (hjd_internal::SamplingGeom::index)
+    static constexpr int kClasses = 4;
+    static constexpr int kClassSampling[kClasses] = {HJD_YUV444, HJD_YUV420, HJD_YUV422, HJD_GRAY};
+    int nrec[kClasses] = {};
+    int64_t tasks[kClasses] = {};
+    uint8_t* out_base[kClasses] = {};
 };
 
 int hjd_gdec::wait_staging()
@@ -792,10 +801,12 @@ int hjd_gdec::assemble(uint8_t* blob, int16_t* coefs, int64_t* block_offsets, vo
     if (coef_off > static_cast<uint64_t>(caps.max_blocks) || sub_base > caps.max_subs || wg_base > caps.max_wgs)
         return set_error(HJD_E_INVALID, "batch exceeds the decoder's capacity");
 
-    nrec[0] = nrec[1] = 0;
-    tasks[0] = tasks[1] = 0;
-    out_base[0] = out_base[1] = nullptr;
-    if (d_outs) {   // pixel-kernel records: 4:4:4 frames first, then 4:2:0 (one launch each)
+    for (int k = 0; k < kClasses; ++k) {
+        nrec[k] = 0;
+        tasks[k] = 0;
+        out_base[k] = nullptr;
+    }
+    if (d_outs) {   // pixel-kernel records grouped by sampling class (one launch each)
         FrameRecord* recs = reinterpret_cast<FrameRecord*>(h_stage + o.recs);
         int32_t* qtn = reinterpret_cast<int32_t*>(h_stage + o.qt);
         for (int i = 0; i < n; ++i) {
@@ -803,12 +814,13 @@ int hjd_gdec::assemble(uint8_t* blob, int16_t* coefs, int64_t* block_offsets, vo
             if (!d_outs[i] || !pitches || pitches[i] < 4 * p.width || (pitches[i] & 3) ||
                 (reinterpret_cast<uintptr_t>(d_outs[i]) & 15))
                 return set_error(HJD_E_INVALID, "frame %d: bad output buffer or pitch (16-byte aligned, >= 4*width)", i);
-            ++nrec[p.sampling == HJD_YUV420 ? 1 : 0];
+            ++nrec[sampling_class(p.sampling)];
         }
-        int r[2] = {0, nrec[0]};
+        int r[kClasses];
+        for (int k = 0, acc = 0; k < kClasses; acc += nrec[k], ++k) r[k] = acc;
         for (int i = 0; i < n; ++i) {
             const Prepared& p = frames[i];
-            const int sidx = p.sampling == HJD_YUV420 ? 1 : 0;
+            const int sidx = sampling_class(p.sampling);
             if (!out_base[sidx]) out_base[sidx] = static_cast<uint8_t*>(d_outs[i]);
             const int qti[3] = {3 * i, 3 * i + 1, 3 * i + 2};
             FrameRecord rec;
@@ -917,10 +929,10 @@ int gdec_issue(hjd_gdec* g, void* const* d_outs, const int32_t* pitches, int16_t
     if (rc) return rc;
     if (d_outs) {
         int r0 = 0;
-        for (int sidx = 0; sidx < 2; ++sidx) {
+        for (int sidx = 0; sidx < hjd_gdec::kClasses; ++sidx) {
             if (!g->nrec[sidx]) continue;
             rc = hjd_internal::launch_decode(
-                g->device, g->num_cu, sidx == 1 ? HJD_YUV420 : HJD_YUV444, HJD_IN_Q16_ZIGZAG, 0, coefs,
+                g->device, g->num_cu, hjd_gdec::kClassSampling[sidx], HJD_IN_Q16_ZIGZAG, 0, coefs,
                 reinterpret_cast<const int32_t*>(g->d_blob + g->H.qt),
                 reinterpret_cast<const FrameRecord*>(g->d_blob + g->H.recs) + r0, g->nrec[sidx], g->tasks[sidx],
                 g->out_base[sidx], s, 0);

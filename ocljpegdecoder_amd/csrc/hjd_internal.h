@@ -12,6 +12,25 @@ namespace hjd_internal {
 // return `code`.  Defined in hjd_runtime.hip.
 int set_error(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 
+// Per-sampling geometry shared by the parser, the plans and the kernels.  A
+// pixel-kernel task is always 48 coefficient blocks (hjd::kTaskBlocks).
+struct SamplingGeom {
+    int index;          // kernel template index: 0 4:4:4, 1 4:2:0, 2 4:2:2, 3 gray
+    int mcu_px_w, mcu_px_h;
+    int bpm;            // blocks per MCU
+    int mcus_per_task;  // 48 / bpm
+};
+inline bool sampling_geom(int sampling, SamplingGeom* g)
+{
+    switch (sampling) {
+    case 0: *g = {0, 8, 8, 3, 16}; return true;    // HJD_YUV444
+    case 1: *g = {1, 16, 16, 6, 8}; return true;   // HJD_YUV420
+    case 3: *g = {2, 16, 8, 4, 12}; return true;   // HJD_YUV422
+    case 4: *g = {3, 8, 8, 1, 48}; return true;    // HJD_GRAY
+    default: return false;
+    }
+}
+
 // Device frame record of the fused kernel (layout of hjd::FrameDev).
 struct FrameRecord {
     int64_t coef_base, out_base, task_begin;

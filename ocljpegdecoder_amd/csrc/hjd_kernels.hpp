@@ -2,7 +2,8 @@
 //
 // Work decomposition:
 //   task  = one "strip" of 48 consecutive coefficient blocks of one frame:
-//           8 MCUs (4:2:0, 128x16 px) or 16 MCUs (4:4:4, 128x8 px) of one MCU row.
+//           8 MCUs (4:2:0, 128x16 px), 16 MCUs (4:4:4, 128x8 px), 12 MCUs
+//           (4:2:2, 192x8 px) or 48 MCUs (gray, 384x8 px) of one MCU row.
 //   wave  = one task at a time; 4 independent waves per 256-thread workgroup,
 //           each with a private 9 KiB LDS slice (no workgroup barriers);
 //           persistent grid-stride loop over all tasks of all frames.
@@ -107,6 +108,18 @@ __device__ __forceinline__ void cursor_seek(FrameCursor& c, const FrameDev* __re
     cursor_load(c, fr, nframes, total, lo);
 }
 
+// Compile-time geometry of the kernel's sampling index (hjd_internal::
+// sampling_geom): 0 4:4:4, 1 4:2:0, 2 4:2:2 (extension), 3 gray (extension).
+template <int kSampling>
+struct KGeom {
+    static constexpr int kBpm = kSampling == 0 ? 3 : kSampling == 1 ? 6 : kSampling == 2 ? 4 : 1;
+    static constexpr int kMcuW = kSampling == 0 || kSampling == 3 ? 8 : 16;   // MCU pixels
+    static constexpr int kMcuH = kSampling == 1 ? 16 : 8;
+    static constexpr int kMcus = kTaskBlocks / kBpm;                          // MCUs per task
+    static constexpr int kStripW = kMcus * kMcuW;                            // strip pixels
+    static_assert(kMcus * kBpm == kTaskBlocks, "a task is 48 whole MCUs' blocks");
+};
+
 // Where a task's strip sits in its frame.
 struct TaskGeom {
     int64_t blk0;   // first coefficient block (global)
@@ -118,17 +131,15 @@ struct TaskGeom {
 template <int kSampling>
 __device__ __forceinline__ TaskGeom task_geom(const FrameCursor& c, int64_t task)
 {
-    constexpr int kMcuPerTask = kSampling == 1 ? 8 : 16;
-    constexpr int kBpm = kSampling == 1 ? 6 : 3;
-    constexpr int kMcuPx = kSampling == 1 ? 16 : 8;
+    using G = KGeom<kSampling>;
     const int local = static_cast<int>(task - c.begin);
     const int my = local / c.strips;
-    const int mx0 = (local - my * c.strips) * kMcuPerTask;
+    const int mx0 = (local - my * c.strips) * G::kMcus;
     TaskGeom g;
-    g.nblk = min(kMcuPerTask, c.mcu_w - mx0) * kBpm;
-    g.blk0 = c.coef_base + (static_cast<int64_t>(my) * c.mcu_w + mx0) * kBpm;
-    g.y_base = my * kMcuPx;
-    g.x_base = mx0 * kMcuPx;
+    g.nblk = min(G::kMcus, c.mcu_w - mx0) * G::kBpm;
+    g.blk0 = c.coef_base + (static_cast<int64_t>(my) * c.mcu_w + mx0) * G::kBpm;
+    g.y_base = my * G::kMcuH;
+    g.x_base = mx0 * G::kMcuW;
     return g;
 }
 
@@ -249,7 +260,7 @@ __device__ __forceinline__ void colour_stage(const char* __restrict__ slots, int
                                                       &c1, &c1);
             }
         }
-    } else {
+    } else if constexpr (kSampling == 0) {
         const int m = cg >> 1;        // MCU within strip (16 x 8 px)
         const int xm = x0 & 7;        // 0 or 4
 #pragma unroll
@@ -279,14 +290,90 @@ __device__ __forceinline__ void colour_stage(const char* __restrict__ slots, int
                 }
             }
         }
+    } else if constexpr (kSampling == 2) {
+        // 4:2:2 (extension): 192x8 strip of 12 MCUs (Y0 Y1 Cb Cr, 16x8 px);
+        // units of 4 px x 1 row, 48 per row, 6 per lane; each chroma sample
+        // serves 2 horizontally adjacent pixels (nearest replication, as the
+        // reference's 4:2:0 path does in both directions, src/decoder.cpp:474-483).
+        (void)loff;
+#pragma unroll 2
+        for (int it = 0; it < 6; ++it) {
+            const int u = it * 64 + lane;
+            const int y = u / 48;
+            const int cu4 = u - y * 48;       // unit within the row
+            const int m = cu4 >> 2;
+            const int xm = (cu4 & 3) * 4;     // x within MCU: 0,4,8,12
+            const int2 sy = *reinterpret_cast<const int2*>(slots + (4 * m + (xm >> 3)) * kSlotBytes + y * 16 +
+                                                           (xm & 7) * 2);
+            const int coff = y * 16 + xm;     // chroma samples xm/2, xm/2+1
+            const uint32_t cu = *reinterpret_cast<const uint32_t*>(slots + (4 * m + 2) * kSlotBytes + coff);
+            const uint32_t cv = *reinterpret_cast<const uint32_t*>(slots + (4 * m + 3) * kSlotBytes + coff);
+            const ChromaTerms c0 = chroma_terms<0>(cu, cv);
+            const ChromaTerms c1 = chroma_terms<1>(cu, cv);
+            const ChromaPair p0 = pair_of(c0, c0), p1 = pair_of(c1, c1);
+            const uint32_t lo = static_cast<uint32_t>(y) * static_cast<uint32_t>(pitch) +
+                                static_cast<uint32_t>(cu4 * 16);
+            const int xu = x_base + cu4 * 4;
+            const bool flagged = __builtin_amdgcn_ballot_w64((p0.flagged | p1.flagged) != 0) != 0;
+            if (kFull || y_base + y < height) {
+                if (flagged)
+                    emit_row4<true, kVariant, kFull>(strip, lo, xu, width, sy.x, sy.y, p0, p1, &c0, &c0, &c1, &c1);
+                else
+                    emit_row4<false, kVariant, kFull>(strip, lo, xu, width, sy.x, sy.y, p0, p1, &c0, &c0, &c1, &c1);
+            }
+        }
+    } else {
+        // gray (extension): 384x8 strip of 48 one-block MCUs; units of 4 px x
+        // 1 row, 96 per row, 12 per lane; R = G = B = clamp(Y + 128), the
+        // reference's conversion with U = V = 0 (src/decoder.cpp:367-370).
+        (void)loff;
+#pragma unroll
+        for (int it = 0; it < 12; ++it) {
+            const int u = it * 64 + lane;
+            const int y = u / 96;
+            const int cu4 = u - y * 96;
+            const int2 sy = *reinterpret_cast<const int2*>(slots + (cu4 >> 1) * kSlotBytes + y * 16 + (cu4 & 1) * 8);
+            const uint32_t g01 = sat_pk_u8(static_cast<uint32_t>(sy.x));   // bytes g0 g1
+            const uint32_t g23 = sat_pk_u8(static_cast<uint32_t>(sy.y));
+            const uint32_t lo = static_cast<uint32_t>(y) * static_cast<uint32_t>(pitch) +
+                                static_cast<uint32_t>(cu4 * 16);
+            if (kFull || y_base + y < height)
+                store4<kFull, kVariant>(strip, lo, x_base + cu4 * 4, width, perm(g01, g01, 0x0c000000u),
+                                        perm(g01, g01, 0x0c010101u), perm(g23, g23, 0x0c000000u),
+                                        perm(g23, g23, 0x0c010101u));
+        }
     }
 }
 
-// Component (0 = Y, 1 = Cb, 2 = Cr) of round i's block for lane group g.
+// Task-local block (= LDS slot) transformed by lane group g in round i.  The
+// mapping keeps each round's component uniform across the wave (dequant table
+// and luma level shift): 4:4:4 / 4:2:0 / gray blocks are MCU-interleaved with
+// a period dividing 6, so 6g + i works; 4:2:2 MCUs are (Y0, Y1, Cb, Cr), so
+// rounds 0-2 take the 24 luma blocks, rounds 3-5 the 12 Cb then 12 Cr blocks.
+template <int kSampling>
+__device__ __forceinline__ int round_block(int i, int g)
+{
+    if constexpr (kSampling == 2) {
+        if (i < 3) {
+            const int idx = i * 8 + g;          // luma block idx of the strip
+            return 4 * (idx >> 1) + (idx & 1);
+        }
+        const int idx = (i - 3) * 8 + g;        // 0-11 Cb, 12-23 Cr
+        return idx < 12 ? 4 * idx + 2 : 4 * (idx - 12) + 3;
+    } else {
+        return 6 * g + i;
+    }
+}
+
+// Component (0 = Y, 1 = Cb, 2 = Cr) of round i's blocks; -1 where it differs
+// between lane groups (4:2:2 round 4: groups 0-3 Cb, 4-7 Cr).
 template <int kSampling>
 __device__ __forceinline__ constexpr int round_component(int i)
 {
-    return kSampling == 1 ? (i < 4 ? 0 : i - 3) : (i % 3);
+    return kSampling == 1 ? (i < 4 ? 0 : i - 3)
+         : kSampling == 0 ? (i % 3)
+         : kSampling == 3 ? 0
+         : (i < 3 ? 0 : i == 3 ? 1 : i == 5 ? 2 : -1);
 }
 
 // One round's row-pass inputs.  kFmt 0: int16 zigzag staged in the LDS slots
@@ -297,14 +384,15 @@ __device__ __forceinline__ void load_round(const char* __restrict__ slots, int l
                                            int (&v)[8])
 {
     const int g = lane >> 3, r = lane & 7;
-    const int b = 6 * g + i;
+    const int b = round_block<kSampling>(i, g);
     const int comp = round_component<kSampling>(i);
     if constexpr (kFmt == 0) {
         const char* blk = slots + b * kSlotBytes;
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
             const int coef = *reinterpret_cast<const short*>(blk + zoff[c]);
-            const uint32_t qq = q[comp][c >> 1];   // two 16-bit factors per VGPR
+            // two 16-bit factors per VGPR; a mixed round selects per lane
+            const uint32_t qq = comp >= 0 ? q[comp < 0 ? 0 : comp][c >> 1] : (g < 4 ? q[1][c >> 1] : q[2][c >> 1]);
             const int qc = (c & 1) ? static_cast<int>(qq >> 16) : static_cast<int>(qq & 0xffffu);
             v[c] = mul24(coef, qc);   // dequant (src/decoder.cpp:340)
         }
@@ -335,7 +423,7 @@ __device__ __forceinline__ void idct_stage(char* __restrict__ slots, char* __res
     load_round<kSampling, kFmt>(slots, lane, 0, zoff, q, src32, nblk, v);
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
-        const int b = 6 * g + i;
+        const int b = round_block<kSampling>(i, g);
         idct8<false>(v);
         {
             int4* dst = reinterpret_cast<int4*>(rowbuf + g * kRowBufBlock + r * kRowStride);
@@ -468,11 +556,12 @@ __global__ __launch_bounds__(kGroupThreads, 4) void decode_kernel(const void* __
             idct_stage<kSampling, kFmt>(slots, rowbuf, lane, zoff, q,
                                         static_cast<const int*>(coefs) + tg.blk0 * 64, tg.nblk);
 
-        constexpr int kRows = kSampling == 1 ? 16 : 8;
+        constexpr int kRows = KGeom<kSampling>::kMcuH;
+        constexpr int kStripW = KGeom<kSampling>::kStripW;
         uint8_t* fout = out + cc.out_base;
         if constexpr ((kVariant & kAblNoColour) != 0) {
             (void)fout;
-        } else if (cc.vec_ok && tg.x_base + 128 <= cc.width && tg.y_base + kRows <= cc.height)
+        } else if (cc.vec_ok && tg.x_base + kStripW <= cc.width && tg.y_base + kRows <= cc.height)
             colour_stage<kSampling, true, kVariant>(slots, lane, fout, cc.pitch, cc.width, cc.height, tg.y_base, tg.x_base);
         else {
             colour_stage<kSampling, false, kVariant>(slots, lane, fout, cc.pitch, cc.width, cc.height, tg.y_base, tg.x_base);

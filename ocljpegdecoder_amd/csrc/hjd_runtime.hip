@@ -19,6 +19,8 @@
 #include "hjd_kernels.hpp"
 
 using hjd::FrameDev;
+using hjd_internal::SamplingGeom;
+using hjd_internal::sampling_geom;
 
 namespace {
 
@@ -81,7 +83,7 @@ struct hjd_plan {
     int variant = 0;            // kernel variant bits (hjd_plan_set_variant)
 };
 
-static int geometry(int width, int height, int sampling, int& mcu_w, int& mcu_h, int& bpm, int& mpx);
+static int geometry(int width, int height, int sampling, int& mcu_w, int& mcu_h, int& bpm, int& tasks_mcus);
 static int decode_grid(int sampling, int fmt, int64_t tasks);
 
 int hjd_internal::ctx_num_cu(const hjd_ctx* ctx) { return ctx->num_cu; }
@@ -89,13 +91,12 @@ int hjd_internal::ctx_num_cu(const hjd_ctx* ctx) { return ctx->num_cu; }
 int64_t hjd_internal::make_frame_record(int width, int height, int sampling, int64_t coef_base, int64_t out_base,
                                         int pitch, const int qt_index[3], FrameRecord* rec)
 {
-    int mw, mh, bpm, mpx;
-    int rc = geometry(width, height, sampling, mw, mh, bpm, mpx);
+    int mw, mh, bpm, tasks_mcus;
+    int rc = geometry(width, height, sampling, mw, mh, bpm, tasks_mcus);
     if (rc) return rc;
     static_assert(sizeof(FrameRecord) == sizeof(FrameDev), "record layout");
     FrameDev d;
     memset(&d, 0, sizeof(d));
-    const int tasks_mcus = sampling == HJD_YUV420 ? 8 : 16;
     d.coef_base = coef_base;
     d.out_base = out_base;
     d.task_begin = 0;
@@ -118,9 +119,12 @@ int hjd_internal::launch_decode(int device, int num_cu, int sampling, int input_
     HJD_HIP(hipSetDevice(device));
     const int fmt = input_format == HJD_IN_Q16_ZIGZAG ? 0 : 1;
     (void)num_cu;
+    SamplingGeom sg;
+    if (!sampling_geom(sampling, &sg)) return set_error(HJD_E_INVALID, "unsupported sampling %d", sampling);
     const int grid = grid_blocks > 0 ? grid_blocks : decode_grid(sampling, fmt, tasks);
 #ifdef HJD_ABLATION
     if (fmt == 0 && variant > 1) {
+        if (sg.index > 1) return hjd_internal::set_error(HJD_E_INVALID, "ablation variants are 4:4:4/4:2:0 only");
         using KA = void (*)(const void*, const int*, const FrameDev*, int, int64_t, uint8_t*);
         KA k = nullptr;
         const bool s420 = sampling == HJD_YUV420;
@@ -139,15 +143,14 @@ int hjd_internal::launch_decode(int device, int num_cu, int sampling, int input_
         return HJD_OK;
     }
 #endif
-    const int key = (sampling == HJD_YUV420 ? 8 : 0) | (fmt << 2) | (variant & 3);
+    // [sampling index][input format][variant bits 0-1]
+    const int key = (sg.index << 3) | (fmt << 2) | (variant & 3);
     using K = void (*)(const void*, const int*, const FrameDev*, int, int64_t, uint8_t*);
-    static const K kTable[16] = {
-        hjd::decode_kernel<0, 0, 0>, hjd::decode_kernel<0, 0, 1>, hjd::decode_kernel<0, 0, 2>,
-        hjd::decode_kernel<0, 0, 3>, hjd::decode_kernel<0, 1, 0>, hjd::decode_kernel<0, 1, 1>,
-        hjd::decode_kernel<0, 1, 2>, hjd::decode_kernel<0, 1, 3>, hjd::decode_kernel<1, 0, 0>,
-        hjd::decode_kernel<1, 0, 1>, hjd::decode_kernel<1, 0, 2>, hjd::decode_kernel<1, 0, 3>,
-        hjd::decode_kernel<1, 1, 0>, hjd::decode_kernel<1, 1, 1>, hjd::decode_kernel<1, 1, 2>,
-        hjd::decode_kernel<1, 1, 3>};
+#define HJD_K4(S, F) hjd::decode_kernel<S, F, 0>, hjd::decode_kernel<S, F, 1>, hjd::decode_kernel<S, F, 2>, \
+                     hjd::decode_kernel<S, F, 3>
+    static const K kTable[32] = {HJD_K4(0, 0), HJD_K4(0, 1), HJD_K4(1, 0), HJD_K4(1, 1),
+                                 HJD_K4(2, 0), HJD_K4(2, 1), HJD_K4(3, 0), HJD_K4(3, 1)};
+#undef HJD_K4
     hipLaunchKernelGGL(kTable[key], dim3(grid), dim3(hjd::kGroupThreads), 0, static_cast<hipStream_t>(stream),
                        d_coefs, d_qt_nat, reinterpret_cast<const FrameDev*>(d_frames), nframes, tasks,
                        static_cast<uint8_t*>(d_out));
@@ -202,23 +205,24 @@ int hjd_ctx_destroy(hjd_ctx* ctx)
 
 int hjd_ctx_device(const hjd_ctx* ctx) { return ctx ? ctx->device : -1; }
 
-static int geometry(int width, int height, int sampling, int& mcu_w, int& mcu_h, int& bpm, int& mpx)
+static int geometry(int width, int height, int sampling, int& mcu_w, int& mcu_h, int& bpm, int& tasks_mcus)
 {
     if (width <= 0 || height <= 0 || width > 65535 || height > 65535)
         return fail(HJD_E_INVALID, "invalid dimensions %dx%d", width, height);
-    if (sampling != HJD_YUV444 && sampling != HJD_YUV420)
-        return fail(HJD_E_INVALID, "unsupported sampling %d (only 4:4:4 and 4:2:0)", sampling);
-    mpx = sampling == HJD_YUV420 ? 16 : 8;
-    bpm = sampling == HJD_YUV420 ? 6 : 3;
-    mcu_w = (width - 1) / mpx + 1;   // src/decoder.cpp:189-190
-    mcu_h = (height - 1) / mpx + 1;
+    SamplingGeom g;
+    if (!sampling_geom(sampling, &g))
+        return fail(HJD_E_INVALID, "unsupported sampling %d (4:4:4, 4:2:0, 4:2:2 or gray)", sampling);
+    bpm = g.bpm;
+    tasks_mcus = g.mcus_per_task;
+    mcu_w = (width - 1) / g.mcu_px_w + 1;   // src/decoder.cpp:189-190
+    mcu_h = (height - 1) / g.mcu_px_h + 1;
     return HJD_OK;
 }
 
 int hjd_frame_blocks(int width, int height, int sampling, int64_t* nblocks)
 {
-    int mw, mh, bpm, mpx;
-    int rc = geometry(width, height, sampling, mw, mh, bpm, mpx);
+    int mw, mh, bpm, tasks_mcus;
+    int rc = geometry(width, height, sampling, mw, mh, bpm, tasks_mcus);
     if (rc) return rc;
     if (!nblocks) return fail(HJD_E_INVALID, "nblocks is NULL");
     *nblocks = static_cast<int64_t>(mw) * mh * bpm;
@@ -241,8 +245,8 @@ int hjd_plan_create(hjd_ctx* ctx, const hjd_frame* frames, int nframes, int inpu
     int sampling = nframes > 0 ? frames[0].sampling : HJD_YUV420;
     for (int i = 0; i < nframes; ++i) {
         const hjd_frame& f = frames[i];
-        int mw, mh, bpm, mpx;
-        int rc = geometry(f.width, f.height, f.sampling, mw, mh, bpm, mpx);
+        int mw, mh, bpm, tasks_mcus;
+        int rc = geometry(f.width, f.height, f.sampling, mw, mh, bpm, tasks_mcus);
         if (rc) return fail(rc, "frame %d: %s", i, g_last_error.c_str());
         if (f.sampling != sampling)
             return fail(HJD_E_INVALID, "frame %d: mixed sampling in one plan (use one plan per sampling)", i);
@@ -255,7 +259,6 @@ int hjd_plan_create(hjd_ctx* ctx, const hjd_frame* frames, int nframes, int inpu
                 if (f.qt_index[c] < 0 || f.qt_index[c] >= nq)
                     return fail(HJD_E_INVALID, "frame %d: qt_index[%d]=%d out of range", i, c, f.qt_index[c]);
         }
-        const int tasks_mcus = f.sampling == HJD_YUV420 ? 8 : 16;
         d.coef_base = static_cast<int64_t>(f.coef_offset);
         d.out_base = static_cast<int64_t>(f.out_offset);
         d.task_begin = tasks;
@@ -338,7 +341,7 @@ int64_t hjd_plan_coef_bytes(const hjd_plan* plan) { return plan ? plan->coef_byt
 // far better locality than with 4096 persistent waves spread over the whole
 // batch (4:2:0 +12 %, 4:4:4 +13 % over one persistent wave per slot).  The
 // heavier 4:4:4 tasks still profit from the one-task-ahead prefetch, so their
-// waves take ~8 tasks; 4:2:0 waves take one.
+// waves take ~8 tasks; 4:2:0 waves take one (4:2:2 and gray: 8, like 4:4:4).
 static int decode_grid(int sampling, int fmt, int64_t tasks)
 {
     const int64_t per_wave = (sampling == HJD_YUV420 && fmt == 0) ? 1 : 8;

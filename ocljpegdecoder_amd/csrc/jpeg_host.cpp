@@ -115,24 +115,33 @@ int parse(const uint8_t* d, size_t n, Frame& f)
             f.height = be16(s + 1);
             f.width = be16(s + 3);
             f.ncomp = s[5];
-            if (f.ncomp != 3) return set_error(HJD_E_INVALID, "unsupported number of components %d", f.ncomp);
+            if (f.ncomp != 3 && f.ncomp != 1)
+                return set_error(HJD_E_INVALID, "unsupported number of components %d", f.ncomp);
             if (sl < 6 + 3 * f.ncomp) return set_error(HJD_E_INVALID, "truncated SOF0");
             if (f.width <= 0 || f.height <= 0) return set_error(HJD_E_INVALID, "invalid dimensions");
-            for (int c = 0; c < 3; ++c) {
+            for (int c = 0; c < f.ncomp; ++c) {
                 f.comp[c].id = s[6 + 3 * c];
                 f.comp[c].h = s[7 + 3 * c] >> 4;
                 f.comp[c].v = s[7 + 3 * c] & 15;
                 f.comp[c].tq = s[8 + 3 * c];
                 if (f.comp[c].tq > 3) return set_error(HJD_E_INVALID, "bad quantisation table id");
             }
-            // src/decoder.cpp:58-69: only H2V2/H1V1/H1V1 and all-H1V1
+            // src/decoder.cpp:58-69 accepts H2V2/H1V1/H1V1 and all-H1V1; H2V1/H1V1/H1V1
+            // (4:2:2) and one component (gray) are this library's extensions
+            // (SURVEY.md s8(f) rank 4).  A one-component scan is non-interleaved:
+            // its MCU is one block whatever the sampling factors (T.81 A.2.2).
             const Component* c = f.comp;
-            if (c[0].h == 2 && c[0].v == 2 && c[1].h == 1 && c[1].v == 1 && c[2].h == 1 && c[2].v == 1)
+            const bool chroma11 = f.ncomp == 3 && c[1].h == 1 && c[1].v == 1 && c[2].h == 1 && c[2].v == 1;
+            if (f.ncomp == 1)
+                f.sampling = HJD_GRAY;
+            else if (chroma11 && c[0].h == 2 && c[0].v == 2)
                 f.sampling = HJD_YUV420;
-            else if (c[0].h == 1 && c[0].v == 1 && c[1].h == 1 && c[1].v == 1 && c[2].h == 1 && c[2].v == 1)
+            else if (chroma11 && c[0].h == 1 && c[0].v == 1)
                 f.sampling = HJD_YUV444;
+            else if (chroma11 && c[0].h == 2 && c[0].v == 1)
+                f.sampling = HJD_YUV422;
             else
-                return set_error(HJD_E_INVALID, "unsupported sampling (only 4:2:0 and 4:4:4)");
+                return set_error(HJD_E_INVALID, "unsupported sampling (4:2:0, 4:4:4, 4:2:2 or gray)");
             have_sof = true;
             break;
         }
@@ -160,12 +169,13 @@ int parse(const uint8_t* d, size_t n, Frame& f)
             break;
         case 0xDA: {   // SOS (src/parser.cpp:132-154)
             if (!have_sof) return set_error(HJD_E_INVALID, "SOS before SOF0");
-            if (sl < 1 || s[0] != 3 || sl < 1 + 2 * 3 + 3)
-                return set_error(HJD_E_INVALID, "unsupported scan (needs all 3 components interleaved)");
-            for (int i = 0; i < 3; ++i) {
+            const int ns = f.ncomp;
+            if (sl < 1 || s[0] != ns || sl < 1 + 2 * ns + 3)
+                return set_error(HJD_E_INVALID, "unsupported scan (needs all components interleaved)");
+            for (int i = 0; i < ns; ++i) {
                 const int cid = s[1 + 2 * i], tdta = s[2 + 2 * i];
                 int fc = -1;
-                for (int c = 0; c < 3; ++c)
+                for (int c = 0; c < ns; ++c)
                     if (f.comp[c].id == cid) fc = c;
                 if (fc < 0) return set_error(HJD_E_INVALID, "scan component %d not in frame", cid);
                 f.scan_order[i] = fc;
@@ -173,10 +183,10 @@ int parse(const uint8_t* d, size_t n, Frame& f)
                 f.comp[fc].ta = tdta & 15;
                 if (f.comp[fc].td > 3 || f.comp[fc].ta > 3) return set_error(HJD_E_INVALID, "bad Huffman table id");
             }
-            const uint8_t* tail = s + 1 + 2 * 3;
+            const uint8_t* tail = s + 1 + 2 * ns;
             if (tail[0] != 0 || tail[1] != 63 || tail[2] != 0)
                 return set_error(HJD_E_INVALID, "not a baseline scan (Ss/Se/Ah/Al)");
-            for (int c = 0; c < 3; ++c) {
+            for (int c = 0; c < ns; ++c) {
                 if (f.qt_prec[f.comp[c].tq] < 0) return set_error(HJD_E_INVALID, "missing quantisation table");
                 if (!f.dc[f.comp[c].td].defined) return set_error(HJD_E_INVALID, "missing DC Huffman table");
                 if (!f.ac[f.comp[c].ta].defined) return set_error(HJD_E_INVALID, "missing AC Huffman table");
@@ -198,14 +208,15 @@ void fill_info(const Frame& f, hjd_jpeg_info* info)
     info->height = f.height;
     info->sampling = f.sampling;
     info->restart_interval = f.restart_interval;
-    const int mpx = f.sampling == HJD_YUV420 ? 16 : 8;
-    const int bpm = f.sampling == HJD_YUV420 ? 6 : 3;
-    info->mcu_w = (f.width - 1) / mpx + 1;
-    info->mcu_h = (f.height - 1) / mpx + 1;
-    info->nblocks = static_cast<int64_t>(info->mcu_w) * info->mcu_h * bpm;
-    for (int c = 0; c < 3; ++c) {
-        memcpy(info->qt[c], f.qt[f.comp[c].tq], sizeof(info->qt[c]));
-        info->qt_precision[c] = f.qt_prec[f.comp[c].tq];
+    hjd_internal::SamplingGeom g;
+    hjd_internal::sampling_geom(f.sampling, &g);   // parse() admitted only known samplings
+    info->mcu_w = (f.width - 1) / g.mcu_px_w + 1;
+    info->mcu_h = (f.height - 1) / g.mcu_px_h + 1;
+    info->nblocks = static_cast<int64_t>(info->mcu_w) * info->mcu_h * g.bpm;
+    for (int c = 0; c < 3; ++c) {   // gray: the Y table for all three (only Y is used)
+        const int fc = c < f.ncomp ? c : 0;
+        memcpy(info->qt[c], f.qt[f.comp[fc].tq], sizeof(info->qt[c]));
+        info->qt_precision[c] = f.qt_prec[f.comp[fc].tq];
     }
     info->scan_offset = static_cast<int64_t>(f.scan_offset);
 }
@@ -314,12 +325,13 @@ int decode_scan(const uint8_t* d, size_t n, const Frame& f, const hjd_jpeg_info&
 {
     BitReader br{d + f.scan_offset, d + n};
     int pred[3] = {0, 0, 0};
-    const int nblk_c[3] = {f.comp[0].h * f.comp[0].v, 1, 1};
+    // blocks per MCU of each component (gray: one block, non-interleaved scan)
+    const int nblk_c[3] = {f.ncomp == 1 ? 1 : f.comp[0].h * f.comp[0].v, 1, 1};
     int blk_base[3];   // block offset of each frame component inside an MCU
     blk_base[0] = 0;
     blk_base[1] = nblk_c[0];
     blk_base[2] = nblk_c[0] + 1;
-    const int bpm = nblk_c[0] + 2;
+    const int bpm = f.ncomp == 1 ? 1 : nblk_c[0] + 2;
     const int64_t nmcu = static_cast<int64_t>(info.mcu_w) * info.mcu_h;
     int restarts = 0, since = 0;
     for (int64_t m = 0; m < nmcu; ++m) {
@@ -332,7 +344,7 @@ int decode_scan(const uint8_t* d, size_t n, const Frame& f, const hjd_jpeg_info&
         }
         ++since;
         int16_t* mcu = coefs + m * bpm * 64;
-        for (int si = 0; si < 3; ++si) {
+        for (int si = 0; si < f.ncomp; ++si) {
             const int c = f.scan_order[si];
             const HuffTable& dc = f.dc[f.comp[c].td];
             const HuffTable& ac = f.ac[f.comp[c].ta];
@@ -379,10 +391,10 @@ int hjd_internal::parse_scan_header(const uint8_t* data, size_t size, ScanHeader
     memcpy(h->qt, info.qt, sizeof(h->qt));
     // bitstream block order of one MCU (src/decoder.cpp:308-344): scan components
     // in SOS order, H*V blocks each; output slot = Y blocks, then Cb, then Cr.
-    const int nblk_c[3] = {f.comp[0].h * f.comp[0].v, 1, 1};
+    const int nblk_c[3] = {f.ncomp == 1 ? 1 : f.comp[0].h * f.comp[0].v, 1, 1};
     const int blk_base[3] = {0, nblk_c[0], nblk_c[0] + 1};
     int j = 0;
-    for (int si = 0; si < 3; ++si) {
+    for (int si = 0; si < f.ncomp; ++si) {
         const int c = f.scan_order[si];
         for (int b = 0; b < nblk_c[c]; ++b, ++j) {
             h->jcomp[j] = c;

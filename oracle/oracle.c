@@ -148,6 +148,31 @@ static void put_mcu(const int32_t (*m)[64], int sampling, int mx, int my, int wi
                 out[(int64_t)py * pitch + px] = oracle_yuv_to_bgrx(m[0][pos], m[1][pos], m[2][pos]);
             }
         }
+    } else if (sampling == ORACLE_YUV422) {
+        /* extension (the reference rejects H2V1): nearest horizontal chroma
+         * replication, the 4:2:0 rule of decoder.cpp:474-483 in x only */
+        for (y = 0; y < 8; y++) {
+            int py = my * 8 + y;
+            if (py >= height) break;
+            for (x = 0; x < 16; x++) {
+                int px = mx * 16 + x;
+                if (px >= width) break;
+                int Y = m[x >> 3][(y << 3) | (x & 7)];
+                int c = (y << 3) + (x >> 1);
+                out[(int64_t)py * pitch + px] = oracle_yuv_to_bgrx(Y, m[2][c], m[3][c]);
+            }
+        }
+    } else if (sampling == ORACLE_GRAY) {
+        /* extension: one component, the reference's conversion with U = V = 0 */
+        for (y = 0; y < 8; y++) {
+            int py = my * 8 + y;
+            if (py >= height) break;
+            for (x = 0; x < 8; x++) {
+                int px = mx * 8 + x;
+                if (px >= width) break;
+                out[(int64_t)py * pitch + px] = oracle_yuv_to_bgrx(m[0][y * 8 + x], 0, 0);
+            }
+        }
     } else {
         for (y = 0; y < 16; y++) {
             int py = my * 16 + y;
@@ -163,14 +188,19 @@ static void put_mcu(const int32_t (*m)[64], int sampling, int mx, int my, int wi
     }
 }
 
-static int frame_geometry(int width, int height, int sampling, int* mcw, int* mch, int* bpm, int* msz)
+static int frame_geometry(int width, int height, int sampling, int* mcw, int* mch, int* bpm, int* nluma)
 {
+    int mw, mh;
     if (width <= 0 || height <= 0) return -1;
-    if (sampling != ORACLE_YUV444 && sampling != ORACLE_YUV420) return -1;
-    *msz = sampling == ORACLE_YUV444 ? 8 : 16;
-    *bpm = sampling == ORACLE_YUV444 ? 3 : 6;
-    *mcw = (width - 1) / *msz + 1; /* decoder.cpp:189-190 */
-    *mch = (height - 1) / *msz + 1;
+    switch (sampling) {
+    case ORACLE_YUV444: mw = 8; mh = 8; *bpm = 3; *nluma = 1; break;
+    case ORACLE_YUV420: mw = 16; mh = 16; *bpm = 6; *nluma = 4; break;
+    case ORACLE_YUV422: mw = 16; mh = 8; *bpm = 4; *nluma = 2; break;
+    case ORACLE_GRAY: mw = 8; mh = 8; *bpm = 1; *nluma = 1; break;
+    default: return -1;
+    }
+    *mcw = (width - 1) / mw + 1; /* decoder.cpp:189-190 */
+    *mch = (height - 1) / mh + 1;
     return 0;
 }
 
@@ -178,10 +208,10 @@ int oracle_decode_frame_q16(const int16_t* coefs, const int32_t* qt_y, const int
                             const int32_t* qt_cr, int width, int height, int sampling,
                             uint32_t* out, int out_pitch_px)
 {
-    int mcw, mch, bpm, msz, mx, my, b;
-    if (frame_geometry(width, height, sampling, &mcw, &mch, &bpm, &msz)) return -1;
+    int mcw, mch, bpm, nluma, mx, my, b;
+    if (frame_geometry(width, height, sampling, &mcw, &mch, &bpm, &nluma)) return -1;
     const int32_t* qt[6];
-    for (b = 0; b < bpm; b++) qt[b] = b < bpm - 2 ? qt_y : (b == bpm - 2 ? qt_cb : qt_cr);
+    for (b = 0; b < bpm; b++) qt[b] = b < nluma ? qt_y : (b == nluma ? qt_cb : qt_cr);
     int32_t m[6][64];
     const int16_t* src = coefs;
     for (my = 0; my < mch; my++) {
@@ -199,8 +229,8 @@ int oracle_decode_frame_q16(const int16_t* coefs, const int32_t* qt_y, const int
 int oracle_decode_frame_i32(const int32_t* mcu_data, int width, int height, int sampling,
                             uint32_t* out, int out_pitch_px)
 {
-    int mcw, mch, bpm, msz, mx, my, b;
-    if (frame_geometry(width, height, sampling, &mcw, &mch, &bpm, &msz)) return -1;
+    int mcw, mch, bpm, nluma, mx, my, b;
+    if (frame_geometry(width, height, sampling, &mcw, &mch, &bpm, &nluma)) return -1;
     int32_t m[6][64];
     const int32_t* src = mcu_data;
     for (my = 0; my < mch; my++) {

@@ -39,8 +39,13 @@ uint32_t oracle_yuv_to_bgrx(int32_t y, int32_t u, int32_t v);
 /* bulk form of oracle_yuv_to_bgrx, for the exhaustive colour test */
 void oracle_yuv_to_bgrx_n(const int32_t* y, const int32_t* u, const int32_t* v, uint32_t* out, int64_t n);
 
-/* sampling codes shared with include/hjd.h */
-enum { ORACLE_YUV444 = 0, ORACLE_YUV420 = 1 };
+/* sampling codes shared with include/hjd.h.  ORACLE_YUV422 (Y H2V1) and
+ * ORACLE_GRAY are extensions the reference rejects (decoder.cpp:58-69): the
+ * same IDCT and colour arithmetic with nearest horizontal chroma replication,
+ * gray as the conversion with U = V = 0.  Parity for them is unpinned by the
+ * reference (it has no such path); tests pin the HIP path to this
+ * restatement. */
+enum { ORACLE_YUV444 = 0, ORACLE_YUV420 = 1, ORACLE_YUV422 = 3, ORACLE_GRAY = 4 };
 
 /*
  * Whole frame from int16 quantised zigzag coefficients, MCU-major

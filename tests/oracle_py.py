@@ -105,8 +105,7 @@ def dequant_natural(coefs: np.ndarray, qt: np.ndarray, sampling: int) -> np.ndar
     """int16 zigzag + per-component qtables -> int32 natural (jpg.mcu_data)."""
     from_zz = np.array(ZIGZAG)
     c = np.asarray(coefs, dtype=np.int32).reshape(-1, 64)
-    bpm = 6 if sampling == 1 else 3
-    comp = np.array(([0] * (bpm - 2) + [1, 2]) * (c.shape[0] // bpm))
+    comp = block_components(sampling, c.shape[0])
     q = np.asarray(qt, dtype=np.int32).reshape(3, 64)[comp]
     out = np.zeros_like(c)
     out[:, from_zz] = c * q
@@ -152,8 +151,7 @@ def synthetic_coefs(width, height, sampling, seed=0, quality_scale=1.0):
     pix = np.clip(pix, -128, 127)
     F = np.einsum("ux,nxy,vy->nuv", m, pix, m).reshape(nblk, 64)
     qt = std_qtables(quality_scale)
-    bpm = 6 if sampling == 1 else 3
-    comp = np.array(([0] * (bpm - 2) + [1, 2]) * (nblk // bpm))
+    comp = block_components(sampling, nblk)
     qnat = np.zeros((3, 64), np.int32)
     qnat[:, ZIGZAG] = qt
     coef_nat = np.rint(F / qnat[comp]).astype(np.int32)
@@ -175,7 +173,17 @@ def std_qtables(scale=1.0):
     return np.clip(np.rint(zz * scale), 1, 255).astype(np.int32)
 
 
+# sampling (include/hjd.h codes) -> (MCU px width, MCU px height, blocks per MCU,
+# luma blocks per MCU); 3 (4:2:2) and 4 (gray) are the extensions of oracle.h
+GEOM = {0: (8, 8, 3, 1), 1: (16, 16, 6, 4), 3: (16, 8, 4, 2), 4: (8, 8, 1, 1)}
+
+
 def frame_blocks(width, height, sampling):
-    mpx = 16 if sampling == 1 else 8
-    bpm = 6 if sampling == 1 else 3
-    return ((width - 1) // mpx + 1) * ((height - 1) // mpx + 1) * bpm
+    pw, ph, bpm, _ = GEOM[sampling]
+    return ((width - 1) // pw + 1) * ((height - 1) // ph + 1) * bpm
+
+
+def block_components(sampling, nblocks):
+    """Component (0 Y, 1 Cb, 2 Cr) of each block of an MCU-major block list."""
+    _, _, bpm, nluma = GEOM[sampling]
+    return np.array(([0] * nluma + [1, 2][: bpm - nluma]) * (nblocks // bpm))

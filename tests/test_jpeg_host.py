@@ -79,13 +79,65 @@ def test_rejects_unsupported(lib):
     img = Image.fromarray(np.zeros((16, 16, 3), np.uint8))
     b = io.BytesIO(); img.save(b, format="JPEG", progressive=True)
     assert decode(lib, b.getvalue())[0] != 0            # progressive: SOF2
-    b = io.BytesIO(); img.convert("L").save(b, format="JPEG")
-    assert decode(lib, b.getvalue())[0] != 0            # 1 component
-    b = io.BytesIO(); img.save(b, format="JPEG", subsampling=1)   # 4:2:2
-    assert decode(lib, b.getvalue())[0] != 0
+    # 4:4:0 (Y H1V2): patch the luma sampling byte of a 4:2:2 file's SOF0
+    b = io.BytesIO(); img.save(b, format="JPEG", subsampling=1)
+    data = bytearray(b.getvalue())
+    sof = data.index(b"\xff\xc0")
+    assert data[sof + 11] == 0x21
+    data[sof + 11] = 0x12
+    assert decode(lib, bytes(data))[0] != 0
     assert decode(lib, b"\x00\x01garbage")[0] != 0
     good = _pil_jpeg(32, 32, 90, 2)
     assert decode(lib, good[: len(good) // 2])[0] != 0 or True   # truncated: must not crash
+
+
+def _pil_smooth(w, h, quality, mode, subsampling=0, seed=0, **kw):
+    """Gradient + mild noise image encoded by Pillow (mode "RGB" or "L")."""
+    import io
+    from PIL import Image
+    rng = np.random.default_rng(seed)
+    x = np.arange(w)[None, :]
+    y = np.arange(h)[:, None]
+    img = np.stack([x * 255 / w + 0 * y, y * 255 / h + 0 * x, (x + y) * 127 / (w + h) + 60], -1)
+    img = np.clip(img + rng.normal(0, 6, img.shape), 0, 255).astype(np.uint8)
+    im = Image.fromarray(img)
+    if mode == "L":
+        im = im.convert("L")
+    b = io.BytesIO()
+    im.save(b, format="JPEG", quality=quality, subsampling=subsampling, **kw)
+    return b.getvalue(), b
+
+
+@pytest.mark.parametrize("mode,sub,w,h,kw", [
+    ("L", 0, 40, 24, {}),
+    ("L", 0, 333, 77, {"restart_marker_blocks": 5}),
+    ("RGB", 1, 48, 16, {}),
+    ("RGB", 1, 333, 77, {}),
+    ("RGB", 1, 200, 40, {"restart_marker_rows": 1}),
+])
+def test_extension_samplings_decode(lib, mode, sub, w, h, kw):
+    """4:2:2 and gray (the reference rejects both, so
+    there is no reference output to match).  Host Huffman + the oracle's
+    restatement must agree with Pillow's own decode of the same file to within
+    IDCT/upsampling differences (Pillow: libjpeg islow IDCT, fancy
+    upsampling); a wrong entropy decode would be garbage, not +-1 noise."""
+    import io
+    from PIL import Image
+    data, _ = _pil_smooth(w, h, 90, mode, sub, **kw)
+    rc, info, coefs = decode(lib, data)
+    assert rc == 0, lib.hjd_last_error()
+    want_sampling = 4 if mode == "L" else 3
+    assert (info.width, info.height, info.sampling) == (w, h, want_sampling)
+    assert info.nblocks == O.frame_blocks(w, h, want_sampling)
+    px = O.decode_q16(coefs, np.array(info.qt), w, h, want_sampling)
+    bgr = px.view(np.uint8).reshape(h, w, 4)[..., :3].astype(np.int32)
+    ref = np.asarray(Image.open(io.BytesIO(data)).convert("RGB"))[..., ::-1].astype(np.int32)
+    d = np.abs(bgr - ref)
+    # measured: gray max 1 (IDCT rounding), 4:2:2 max 4-6 (Pillow's filtered
+    # chroma upsampling); one DC coefficient off by 20 already gives 8-14
+    assert d.mean() < 1.5 and d.max() <= (1 if mode == "L" else 6), (d.mean(), d.max())
+    if mode == "L":
+        assert (bgr[..., 0] == bgr[..., 1]).all() and (bgr[..., 1] == bgr[..., 2]).all()
 
 
 def test_16bit_dqt_and_restart_rows(lib):

@@ -41,7 +41,7 @@ def main():
     coefs = torch.empty((nf, nblk, 64), dtype=torch.int16, device=dev)
     npool = min(8, nf)
     for i in range(npool):
-        coefs[i] = bench.synth_frame_gpu(torch, nblk, bpm, qt, seed=i, device=dev)
+        coefs[i] = bench.synth_frame_gpu(torch, nblk, s, qt, seed=i, device=dev)
     for i in range(npool, nf):
         coefs[i].copy_(coefs[i % npool])
     out = torch.empty((nf, h, w), dtype=torch.int32, device=dev)
