@@ -49,6 +49,9 @@ WORKLOADS = {
                   desc="extension (SURVEY s8(f) rank 4): batch of 1024 synthetic 3840x2160 4:2:2 frames"),
     "4kgray": dict(width=3840, height=2160, sampling=4, frames=1024,
                    desc="extension (SURVEY s8(f) rank 4): batch of 1024 synthetic 3840x2160 grayscale frames"),
+    "4k420_bgr24": dict(width=3840, height=2160, sampling=1, frames=1024, out_format=1,
+                        desc="extension (SURVEY s8(f) rank 4): configs[2] with 3-byte BGR24 output (24-bpp BMP "
+                             "rows) instead of BGRX"),
     "fhd420": dict(width=1920, height=1080, sampling=1, frames=1,
                    desc="BASELINE configs[1]: single 1920x1080 4:2:0 frame, one launch (cache/launch bound)"),
     "stream4k420": dict(width=3840, height=2160, sampling=1, frames=1024, entropy="gpu",
@@ -57,6 +60,10 @@ WORKLOADS = {
     "stream4k420_d2h": dict(width=3840, height=2160, sampling=1, frames=256, entropy="gpu", d2h=True,
                             desc="BASELINE configs[4] per GPU, D2H-on (SURVEY s8(e)): as stream4k420, and every "
                                  "frame's BGRX copied back to pinned host memory"),
+    "stream4k420_d2h_bgr24": dict(width=3840, height=2160, sampling=1, frames=256, entropy="gpu", d2h=True,
+                                  out_format=1,
+                                  desc="BASELINE configs[4] per GPU, D2H-on, BGR24 sink (SURVEY s8(f) rank 4): as "
+                                       "stream4k420_d2h with 3-byte pixels copied back"),
     "stream4k420_host": dict(width=3840, height=2160, sampling=1, frames=128, entropy="host",
                              desc="BASELINE configs[4] per GPU, host-Huffman variant: host Huffman workers || "
                                   "pinned H2D || fused kernel"),
@@ -225,15 +232,18 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
     d2h = bool(wl.get("d2h"))
     per_batch = int(os.environ.get("HJD_STREAM_BATCH", 16 if d2h else 32))
     nslots = int(os.environ.get("HJD_STREAM_SLOTS", 4 if d2h else 6))
+    ofmt = wl.get("out_format", hjd.OUT_BGRX)
+    pitch = hjd.default_pitch(w, ofmt)
+    shape, dtype = ((h, w), torch.int32) if ofmt == hjd.OUT_BGRX else ((h, pitch), torch.uint8)
     if d2h:
         # pinned host ring, one buffer per frame that can be in flight
-        ring = [torch.empty((h, w), dtype=torch.int32).pin_memory() for _ in range(per_batch * nslots)]
+        ring = [torch.empty(shape, dtype=dtype).pin_memory() for _ in range(per_batch * nslots)]
         outs = [ring[i % len(ring)] for i in range(nf)]
     else:
-        outs = [torch.empty((h, w), dtype=torch.int32, device=dev) for _ in range(nf)]
+        outs = [torch.empty(shape, dtype=dtype, device=dev) for _ in range(nf)]
     if gpu_entropy:
         st = hjd.GpuJpegStream(ctx, per_batch, per_batch * max(len(d) for d in pool) + (1 << 20),
-                               per_batch * max_blocks, nslots=nslots, nthreads=nthreads)
+                               per_batch * max_blocks, nslots=nslots, nthreads=nthreads, out_format=ofmt)
         stat_key = "host_prep_ns"
     else:
         st = hjd.JpegStream(ctx, max_blocks, nslots=nthreads + 4, nthreads=nthreads)
@@ -273,7 +283,11 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
         sys.path.insert(0, os.path.join(REPO, "tests"))
         import oracle_py as O
         exp = O.decode_q16(ref, info.qt, info.width, info.height, info.sampling)
-        ok = bool((outs[0].cpu().numpy().view(np.uint32) == exp).all())
+        got = outs[0].cpu().numpy()
+        if ofmt == hjd.OUT_BGRX:
+            ok = bool((got.view(np.uint32) == exp).all())
+        else:
+            ok = bool((got[:, :3 * w] == exp.view(np.uint8).reshape(h, w, 4)[..., :3].reshape(h, -1)).all())
     except Exception as e:  # oracle library not built
         log("stream spot check skipped:", e)
     if rank == 0:
@@ -288,7 +302,8 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
             "config": {"workload": wl["desc"], "frames_per_gpu_per_step": nf, "width": w, "height": h,
                        "sampling": SAMPLING_NAMES[s], "host_threads_per_gpu": nthreads,
                        "entropy_decode": "gpu" if gpu_entropy else "host", "mean_jpeg_bytes": jpeg_bytes,
-                       "output": "pinned host memory (D2H-on)" if d2h else "BGRX in HBM (D2H-off)",
+                       "output": ("pinned host memory (D2H-on)" if d2h else "in HBM (D2H-off)") +
+                                 (", BGR24" if ofmt == hjd.OUT_BGR24 else ", BGRX"),
                        "parallelism": f"image-parallel x{world} (no collective)"},
             "end_to_end": {
                 ("host_prep_Mpx_per_thread_s" if gpu_entropy else "host_huffman_Mpx_per_thread_s"):
@@ -355,9 +370,11 @@ def main():
         coefs[i] = synth_frame_gpu(torch, nblk, s, qt, seed=1000 * rank + i, device=dev)
     for i in range(npool, nf):
         coefs[i].copy_(coefs[i % npool])
-    out = torch.empty((nf, h, w), dtype=torch.int32, device=dev)
-    specs = [hjd.FrameSpec(w, h, s, coef_offset=i * nblk, out_offset=i * h * w * 4, qt_index=(0, 1, 2))
-             for i in range(nf)]
+    ofmt = wl.get("out_format", hjd.OUT_BGRX)
+    pitch = hjd.default_pitch(w, ofmt)
+    out = torch.empty((nf, h, pitch), dtype=torch.uint8, device=dev)
+    specs = [hjd.FrameSpec(w, h, s, coef_offset=i * nblk, out_offset=i * h * pitch, out_pitch=pitch,
+                           qt_index=(0, 1, 2), out_format=ofmt) for i in range(nf)]
     ctx = hjd.Context(dev.index)
     plan = hjd.Plan(ctx, specs, hjd.IN_Q16_ZIGZAG, qtables=qt)
     torch.cuda.synchronize()
@@ -386,7 +403,7 @@ def main():
     wall_max = shard.aggregate({"seconds": wall})["seconds"]   # max over ranks
 
     px_per_launch = plan.pixels
-    bytes_per_launch = plan.coef_bytes + 4 * plan.pixels
+    bytes_per_launch = plan.coef_bytes + hjd.OUT_BYTES[ofmt] * plan.pixels
     total_px = px_per_launch * args.steps * world
     value = total_px / wall_max / 1e6
     achieved = bytes_per_launch / (kernel_ms / 1e3) / 1e9
@@ -430,7 +447,8 @@ def main():
                     f"{npool} distinct frames replicated to {nf}); inputs resident in HBM",
             "config": {"workload": wl["desc"], "frames_per_gpu": nf, "width": w, "height": h,
                        "sampling": SAMPLING_NAMES[s], "input": "int16 quantised zigzag + qtables",
-                       "output": "BGRX 4 B/px in HBM", "parallelism": f"image-parallel x{world} (no collective)",
+                       "output": "BGRX 4 B/px in HBM" if ofmt == hjd.OUT_BGRX else "BGR24 3 B/px in HBM",
+                       "parallelism": f"image-parallel x{world} (no collective)",
                        "tasks_per_launch": plan.tasks},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4),

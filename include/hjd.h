@@ -44,6 +44,17 @@ enum hjd_status {
  * (the reference's formula with U = V = 0). */
 enum hjd_sampling { HJD_YUV444 = 0, HJD_YUV420 = 1, HJD_OTHER = 2, HJD_YUV422 = 3, HJD_GRAY = 4 };
 
+/* Output pixel format. */
+enum hjd_out_format {
+    /* 4 bytes per pixel: B, G, R, 0 (the reference's RGB32 buffer and its
+     * 32-bpp BMP rows, src/decoder.cpp:367-395). */
+    HJD_OUT_BGRX = 0,
+    /* 3 bytes per pixel: B, G, R (a 24-bpp BMP row; extension, SURVEY.md
+     * s8(f) rank 4).  Same values as BGRX without the pad byte; the kernel
+     * writes 25 % fewer bytes. */
+    HJD_OUT_BGR24 = 1
+};
+
 /* Coefficient input format. */
 enum hjd_input_format {
     /* int16 quantised coefficients in zigzag order, exactly as Huffman decoding
@@ -68,10 +79,10 @@ typedef struct hjd_frame {
     uint64_t out_offset;  /* byte offset of pixel (0,0) in the output buffer */
     int32_t width;        /* visible pixels (output is cropped to W x H) */
     int32_t height;
-    int32_t out_pitch;    /* bytes per output row, >= 4*width, multiple of 4 */
+    int32_t out_pitch;    /* bytes per output row, >= 4*width (BGR24: 3*width), multiple of 4 */
     int32_t sampling;     /* HJD_YUV444, HJD_YUV420, HJD_YUV422 or HJD_GRAY */
     int32_t qt_index[3];  /* per component (Y, Cb, Cr): index into the qtable set */
-    int32_t reserved;     /* must be 0 */
+    int32_t out_format;   /* HJD_OUT_BGRX (0) or HJD_OUT_BGR24; the same for all frames of a plan */
 } hjd_frame;
 
 typedef struct hjd_ctx hjd_ctx;

@@ -109,6 +109,11 @@ int hjd_gdec_decode_coefs(hjd_gdec* g, const uint8_t* const* datas, const size_t
  * Returns HJD_E_INVALID if any frame's entropy data was corrupt. */
 int hjd_gdec_sync(hjd_gdec* g, int32_t* status);
 
+/* Pixel format of the following hjd_gdec_decode calls: HJD_OUT_BGRX (default)
+ * or HJD_OUT_BGR24 (include/hjd.h; 3-byte pixels, d_outs 4-byte aligned,
+ * pitches >= 3*width, multiple of 4). */
+int hjd_gdec_set_output_format(hjd_gdec* g, int out_format);
+
 #define HJD_GDEC_SEQUENTIAL 1   /* verification fell back to the sequential path */
 #define HJD_GDEC_CORRUPT 2      /* invalid Huffman data on the decoded chain */
 #define HJD_GDEC_COUNT 4        /* fewer blocks than the frame needs */
@@ -133,10 +138,19 @@ int hjd_gstream_submit_host(hjd_gstream* s, const uint8_t* data, size_t size, vo
 /* Flush and wait; returns the first error.  stats (may be NULL):
  * {images, pixels, host_prep_ns, h2d_bytes, batches}. */
 int hjd_gstream_sync(hjd_gstream* s, int64_t stats[5]);
+/* Pixel format of the stream's outputs (device and host sinks alike):
+ * HJD_OUT_BGRX (default) or HJD_OUT_BGR24; with BGR24 the D2H sink moves
+ * 3 bytes per pixel.  Only between hjd_gstream_sync and the next submit
+ * (HJD_E_STATE otherwise). */
+int hjd_gstream_set_output_format(hjd_gstream* s, int out_format);
 
 /* The 54-byte header of the reference's output BMP (src/decoder.cpp:372-394):
  * 32 bpp, top-down; the file is this header followed by the W*H*4 BGRX bytes. */
 int hjd_bmp_header(int32_t width, int32_t height, uint8_t header[54]);
+/* The 24-bpp counterpart (SURVEY.md s8(f) rank 4 "RGB24 writer"): top-down,
+ * rows padded to 4 bytes; the file is this header followed by the rows of an
+ * HJD_OUT_BGR24 image at pitch (3*W+3)&~3. */
+int hjd_bmp_header_bgr24(int32_t width, int32_t height, uint8_t header[54]);
 
 /* Test hook (no GPU): runs the same parallel algorithm on the host, one frame,
  * and writes its coefficients.  Not a decode path. */

@@ -14,6 +14,9 @@ from .backend import (  # noqa: E402
     IN_I32_NATURAL,
     IN_Q16_ZIGZAG,
     OTHER,
+    OUT_BGR24,
+    OUT_BGRX,
+    OUT_BYTES,
     GRAY,
     YUV420,
     YUV422,
@@ -23,6 +26,7 @@ from .backend import (  # noqa: E402
     FrameSpec,
     Plan,
     decode_frame,
+    default_pitch,
     device_count,
     frame_blocks,
     mcu_geometry,
@@ -36,5 +40,5 @@ __all__ = [
     "decode_coefs_batch", "decode_jpeg", "emulate_entropy",
     "parse",
     "Context", "FrameSpec", "Plan", "decode_frame", "device_count", "frame_blocks", "mcu_geometry",
-    "YUV444", "YUV420", "YUV422", "GRAY", "OTHER", "block_components", "IN_Q16_ZIGZAG", "IN_I32_NATURAL",
+    "YUV444", "YUV420", "YUV422", "GRAY", "OTHER", "block_components", "OUT_BGRX", "OUT_BGR24", "OUT_BYTES", "default_pitch", "IN_Q16_ZIGZAG", "IN_I32_NATURAL",
 ]

@@ -25,7 +25,7 @@ class HjdFrame(ctypes.Structure):
         ("out_pitch", ctypes.c_int32),
         ("sampling", ctypes.c_int32),
         ("qt_index", ctypes.c_int32 * 3),
-        ("reserved", ctypes.c_int32),
+        ("out_format", ctypes.c_int32),
     ]
 
 
@@ -135,12 +135,15 @@ def _bind_host(lib):
         "hjd_gdec_decode_coefs": (ctypes.c_int, [vp, ctypes.POINTER(u8p), ctypes.POINTER(ctypes.c_size_t),
                                                  ctypes.c_int, vp, ctypes.POINTER(ctypes.c_int64), vp]),
         "hjd_gdec_sync": (ctypes.c_int, [vp, c_i32p]),
+        "hjd_gdec_set_output_format": (ctypes.c_int, [vp, ctypes.c_int]),
         "hjd_gstream_create": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
                                               ctypes.c_int, ctypes.POINTER(vp)]),
         "hjd_gstream_destroy": (ctypes.c_int, [vp]),
         "hjd_gstream_submit": (ctypes.c_int, [vp, u8p, ctypes.c_size_t, vp, ctypes.c_int32]),
         "hjd_gstream_submit_host": (ctypes.c_int, [vp, u8p, ctypes.c_size_t, vp, ctypes.c_int32]),
         "hjd_bmp_header": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, u8p]),
+        "hjd_bmp_header_bgr24": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, u8p]),
+        "hjd_gstream_set_output_format": (ctypes.c_int, [vp, ctypes.c_int]),
         "hjd_gstream_sync": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int64)]),
         "hjd_debug_entropy_emulate": (ctypes.c_int, [u8p, ctypes.c_size_t, ctypes.c_int,
                                                      ctypes.POINTER(ctypes.c_int16), ctypes.c_int64, c_i32p]),

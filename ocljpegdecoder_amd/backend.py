@@ -26,6 +26,15 @@ _GEOM = {YUV444: (8, 8, 3, 1), YUV420: (16, 16, 6, 4), YUV422: (16, 8, 4, 2), GR
 IN_Q16_ZIGZAG = 0
 IN_I32_NATURAL = 1
 
+OUT_BGRX = 0    # 4 B/px: B, G, R, 0 (the reference's RGB32 / 32-bpp BMP rows)
+OUT_BGR24 = 1   # 3 B/px: B, G, R (extension: 24-bpp BMP rows)
+OUT_BYTES = {OUT_BGRX: 4, OUT_BGR24: 3}
+
+
+def default_pitch(width: int, out_format: int = OUT_BGRX) -> int:
+    """Tightest legal row pitch: bytes of one row rounded up to 4."""
+    return (OUT_BYTES[out_format] * width + 3) & ~3
+
 
 def mcu_geometry(width: int, height: int, sampling: int):
     """(mcu_w, mcu_h, blocks_per_mcu, (mcu_px_w, mcu_px_h)) -- src/decoder.cpp:161-192."""
@@ -112,8 +121,13 @@ class FrameSpec:
     sampling: int
     coef_offset: int = 0          # in blocks
     out_offset: int = 0           # bytes
-    out_pitch: int = 0            # bytes (0 -> 4*width)
+    out_pitch: int = 0            # bytes (0 -> default_pitch(width, out_format))
     qt_index: Sequence[int] = field(default_factory=lambda: (0, 1, 1))
+    out_format: int = OUT_BGRX
+
+    @property
+    def pitch(self) -> int:
+        return self.out_pitch or default_pitch(self.width, self.out_format)
 
     def to_c(self) -> HjdFrame:
         f = HjdFrame()
@@ -121,11 +135,11 @@ class FrameSpec:
         f.out_offset = self.out_offset
         f.width = self.width
         f.height = self.height
-        f.out_pitch = self.out_pitch or 4 * self.width
+        f.out_pitch = self.pitch
         f.sampling = self.sampling
         for i in range(3):
             f.qt_index[i] = int(self.qt_index[i])
-        f.reserved = 0
+        f.out_format = self.out_format
         return f
 
 
@@ -155,7 +169,7 @@ class Plan:
         self.coef_elem_bytes = 2 if input_format == IN_Q16_ZIGZAG else 4
         self.coef_elems_needed = max([64 * (f.coef_offset + frame_blocks(f.width, f.height, f.sampling))
                                       for f in self.frames] or [0])
-        self.out_bytes_needed = max([f.out_offset + (f.height - 1) * (f.out_pitch or 4 * f.width) + 4 * f.width
+        self.out_bytes_needed = max([f.out_offset + (f.height - 1) * f.pitch + OUT_BYTES[f.out_format] * f.width
                                      for f in self.frames] or [0])
 
     def _check_tensor(self, t, what, elem_bytes, nbytes_needed):

@@ -697,6 +697,7 @@ struct hjd_gdec {
     int nrec[kClasses] = {};
     int64_t tasks[kClasses] = {};
     uint8_t* out_base[kClasses] = {};
+    int out_format = HJD_OUT_BGRX;      // pixel output format (hjd_gdec_set_output_format)
 };
 
 int hjd_gdec::wait_staging()
@@ -809,11 +810,15 @@ int hjd_gdec::assemble(uint8_t* blob, int16_t* coefs, int64_t* block_offsets, vo
     if (d_outs) {   // pixel-kernel records grouped by sampling class (one launch each)
         FrameRecord* recs = reinterpret_cast<FrameRecord*>(h_stage + o.recs);
         int32_t* qtn = reinterpret_cast<int32_t*>(h_stage + o.qt);
+        const int obytes = hjd_internal::out_format_bytes(out_format);
+        const uintptr_t amask = out_format == HJD_OUT_BGRX ? 15 : 3;
         for (int i = 0; i < n; ++i) {
             const Prepared& p = frames[i];
-            if (!d_outs[i] || !pitches || pitches[i] < 4 * p.width || (pitches[i] & 3) ||
-                (reinterpret_cast<uintptr_t>(d_outs[i]) & 15))
-                return set_error(HJD_E_INVALID, "frame %d: bad output buffer or pitch (16-byte aligned, >= 4*width)", i);
+            if (!d_outs[i] || !pitches || pitches[i] < obytes * p.width || (pitches[i] & 3) ||
+                (reinterpret_cast<uintptr_t>(d_outs[i]) & amask))
+                return set_error(HJD_E_INVALID,
+                                 "frame %d: bad output buffer or pitch (BGRX: 16-byte aligned, >= 4*width; "
+                                 "BGR24: 4-byte aligned, >= 3*width)", i);
             ++nrec[sampling_class(p.sampling)];
         }
         int r[kClasses];
@@ -826,7 +831,8 @@ int hjd_gdec::assemble(uint8_t* blob, int16_t* coefs, int64_t* block_offsets, vo
             FrameRecord rec;
             const int64_t t = hjd_internal::make_frame_record(
                 p.width, p.height, p.sampling, static_cast<int64_t>(ef[i].coef_off),
-                static_cast<int64_t>(static_cast<uint8_t*>(d_outs[i]) - out_base[sidx]), pitches[i], qti, &rec);
+                static_cast<int64_t>(static_cast<uint8_t*>(d_outs[i]) - out_base[sidx]), pitches[i], qti, &rec,
+                out_format);
             if (t < 0) return static_cast<int>(t);
             rec.task_begin = tasks[sidx];
             tasks[sidx] += t;
@@ -935,7 +941,7 @@ int gdec_issue(hjd_gdec* g, void* const* d_outs, const int32_t* pitches, int16_t
                 g->device, g->num_cu, hjd_gdec::kClassSampling[sidx], HJD_IN_Q16_ZIGZAG, 0, coefs,
                 reinterpret_cast<const int32_t*>(g->d_blob + g->H.qt),
                 reinterpret_cast<const FrameRecord*>(g->d_blob + g->H.recs) + r0, g->nrec[sidx], g->tasks[sidx],
-                g->out_base[sidx], s, 0);
+                g->out_base[sidx], s, 0, g->out_format);
             if (rc) return rc;
             r0 += g->nrec[sidx];
         }
@@ -944,7 +950,8 @@ int gdec_issue(hjd_gdec* g, void* const* d_outs, const int32_t* pitches, int16_t
         for (int i = 0; i < n; ++i) {
             if (!host[i].host) continue;
             HJD_HIP(hipMemcpy2DAsync(host[i].host, static_cast<size_t>(host[i].host_pitch), d_outs[i],
-                                     static_cast<size_t>(pitches[i]), static_cast<size_t>(host[i].width) * 4,
+                                     static_cast<size_t>(pitches[i]),
+                                     static_cast<size_t>(host[i].width) * hjd_internal::out_format_bytes(g->out_format),
                                      static_cast<size_t>(host[i].height), hipMemcpyDeviceToHost, s));
         }
     }
@@ -1027,6 +1034,14 @@ int hjd_gdec_decode_coefs(hjd_gdec* g, const uint8_t* const* datas, const size_t
     if (!d_coefs || (reinterpret_cast<uintptr_t>(d_coefs) & 15))
         return set_error(HJD_E_INVALID, "d_coefs must be a 16-byte aligned device pointer");
     return gdec_run(g, datas, sizes, n, nullptr, nullptr, d_coefs, block_offsets, static_cast<hipStream_t>(stream));
+}
+
+int hjd_gdec_set_output_format(hjd_gdec* g, int out_format)
+{
+    if (!g) return set_error(HJD_E_INVALID, "gdec is NULL");
+    if (!hjd_internal::out_format_bytes(out_format)) return set_error(HJD_E_INVALID, "unknown output format %d", out_format);
+    g->out_format = out_format;   // applies to the next decode; an issued one keeps its format
+    return HJD_OK;
 }
 
 int hjd_gdec_sync(hjd_gdec* g, int32_t* status)
@@ -1206,6 +1221,7 @@ struct hjd_gstream {
     int first_error = HJD_OK;
     std::string first_error_msg;
     int local_cpus = 0;   // CPUs of the GPU's NUMA node the workers are bound to (0: unbound)
+    int out_format = HJD_OUT_BGRX;
 
     void record_error(int rc, const std::string& msg)
     {
@@ -1273,7 +1289,7 @@ void hjd_gstream::issue_locked(GBatch* b)
         if (b->host_outs[i]) {
             host.push_back(HostCopy{b->host_outs[i], b->pitches[i], p.width, p.height});
             outs.push_back(reinterpret_cast<void*>(scratch_need));   // offset, rebased below
-            pitches.push_back(align_up(4 * static_cast<size_t>(p.width), 16));
+            pitches.push_back(align_up(static_cast<size_t>(hjd_internal::out_format_bytes(out_format)) * p.width, 16));
             scratch_need += align_up(static_cast<size_t>(pitches.back()) * p.height, 256);
         } else {
             host.push_back(HostCopy{nullptr, 0, p.width, p.height});
@@ -1384,7 +1400,8 @@ static int gstream_submit(hjd_gstream* st, const uint8_t* data, size_t size, voi
     hjd_internal::ScanHeader h;
     int rc = hjd_internal::parse_scan_header(data, size, &h);
     if (rc) return rc;
-    if (out_pitch < 4 * h.width) return set_error(HJD_E_INVALID, "output pitch too small");
+    if (out_pitch < hjd_internal::out_format_bytes(st->out_format) * h.width)
+        return set_error(HJD_E_INVALID, "output pitch too small");
     const size_t need = align_up(size + kDataPad, 16);
     std::lock_guard<std::mutex> api(st->api_mu);
     std::unique_lock<std::mutex> lk(st->mu);
@@ -1422,8 +1439,9 @@ static int gstream_submit(hjd_gstream* st, const uint8_t* data, size_t size, voi
 
 int hjd_gstream_submit(hjd_gstream* st, const uint8_t* data, size_t size, void* d_out, int32_t out_pitch)
 {
-    if (!st || !data || !d_out || out_pitch <= 0 || (out_pitch & 3) || (reinterpret_cast<uintptr_t>(d_out) & 15))
-        return set_error(HJD_E_INVALID, "invalid submit arguments (d_out must be 16-byte aligned)");
+    const uintptr_t amask = st && st->out_format == HJD_OUT_BGR24 ? 3 : 15;
+    if (!st || !data || !d_out || out_pitch <= 0 || (out_pitch & 3) || (reinterpret_cast<uintptr_t>(d_out) & amask))
+        return set_error(HJD_E_INVALID, "invalid submit arguments (d_out must be 16-byte (BGR24: 4-byte) aligned)");
     return gstream_submit(st, data, size, d_out, nullptr, out_pitch);
 }
 
@@ -1433,15 +1451,28 @@ int hjd_gstream_submit_host(hjd_gstream* st, const uint8_t* data, size_t size, v
     return gstream_submit(st, data, size, nullptr, h_out, out_pitch);
 }
 
-int hjd_bmp_header(int32_t width, int32_t height, uint8_t header[54])
+int hjd_gstream_set_output_format(hjd_gstream* st, int out_format)
 {
-    if (!header || width <= 0 || height <= 0) return set_error(HJD_E_INVALID, "invalid BMP geometry");
+    if (!st) return set_error(HJD_E_INVALID, "gstream is NULL");
+    if (!hjd_internal::out_format_bytes(out_format)) return set_error(HJD_E_INVALID, "unknown output format %d", out_format);
+    std::lock_guard<std::mutex> api(st->api_mu);
+    std::lock_guard<std::mutex> lk(st->mu);
+    if (st->open || st->batches_in_flight)
+        return set_error(HJD_E_STATE, "output format can only change between hjd_gstream_sync and the next submit");
+    st->out_format = out_format;
+    for (hjd_gdec* g : st->slots) g->out_format = out_format;
+    return HJD_OK;
+}
+
+static void bmp_header_bpp(int32_t width, int32_t height, int bpp, uint8_t header[54])
+{
     // src/decoder.cpp:372-394 (bmp_create): BITMAPFILEHEADER + BITMAPINFOHEADER,
-    // 32 bpp BI_RGB, negative height = top-down rows, pixels = the BGRX image.
+    // BI_RGB, negative height = top-down rows; rows padded to 4 bytes.
     auto put16 = [&](int o, uint32_t v) { header[o] = v & 0xFF; header[o + 1] = (v >> 8) & 0xFF; };
     auto put32 = [&](int o, uint32_t v) { put16(o, v & 0xFFFF); put16(o + 2, v >> 16); };
     memset(header, 0, 54);
-    const uint64_t size = 54 + static_cast<uint64_t>(width) * static_cast<uint64_t>(height) * 4;
+    const uint64_t row = (static_cast<uint64_t>(width) * (bpp / 8) + 3) & ~uint64_t(3);
+    const uint64_t size = 54 + row * static_cast<uint64_t>(height);
     put16(0, 0x4d42);
     put32(2, static_cast<uint32_t>(size));
     put32(10, 54);
@@ -1449,7 +1480,20 @@ int hjd_bmp_header(int32_t width, int32_t height, uint8_t header[54])
     put32(18, static_cast<uint32_t>(width));
     put32(22, static_cast<uint32_t>(-height));
     put16(26, 1);
-    put16(28, 32);
+    put16(28, static_cast<uint32_t>(bpp));
+}
+
+int hjd_bmp_header(int32_t width, int32_t height, uint8_t header[54])
+{
+    if (!header || width <= 0 || height <= 0) return set_error(HJD_E_INVALID, "invalid BMP geometry");
+    bmp_header_bpp(width, height, 32, header);   // the reference's 32-bpp BGRX file
+    return HJD_OK;
+}
+
+int hjd_bmp_header_bgr24(int32_t width, int32_t height, uint8_t header[54])
+{
+    if (!header || width <= 0 || height <= 0) return set_error(HJD_E_INVALID, "invalid BMP geometry");
+    bmp_header_bpp(width, height, 24, header);
     return HJD_OK;
 }
 

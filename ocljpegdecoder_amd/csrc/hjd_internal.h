@@ -40,15 +40,24 @@ struct FrameRecord {
 };
 
 // Fill a one-frame record (task_begin 0); returns the frame's task count, or
-// a negative status for an unsupported geometry.
+// a negative status for an unsupported geometry.  out_format: HJD_OUT_*.
 int64_t make_frame_record(int width, int height, int sampling, int64_t coef_base, int64_t out_base, int pitch,
-                          const int qt_index[3], FrameRecord* rec);
+                          const int qt_index[3], FrameRecord* rec, int out_format = 0);
 
 // Launch the fused kernel on device-resident frame records / natural-order
 // qtables (no host synchronisation, safe to call from any host thread).
 int launch_decode(int device, int num_cu, int sampling, int input_format, int variant, const void* d_coefs,
                   const int32_t* d_qt_nat, const FrameRecord* d_frames, int nframes, int64_t tasks, void* d_out,
-                  void* stream, int grid_blocks);
+                  void* stream, int grid_blocks, int out_format = 0);
+
+// Bytes per output pixel of an HJD_OUT_* format (0 if unknown).
+inline int out_format_bytes(int out_format) { return out_format == 0 ? 4 : out_format == 1 ? 3 : 0; }
+
+// Rows of this format can take the kernel's full-width vector stores.
+inline bool out_vector_ok(int out_format, int64_t pitch, int64_t out_base)
+{
+    return out_format == 1 ? ((pitch | out_base) & 3) == 0 : ((pitch | out_base) & 15) == 0;
+}
 
 // Parsed baseline-JPEG header as the GPU entropy path needs it (jpeg_host.cpp).
 struct ScanHeader {

@@ -153,14 +153,21 @@ constexpr int kVarWgInterleave = 2;
 // Ablation bits: compiled into the tuning-only library (HJD_ABLATION, see
 // tools/build_native.py --ablation); their outputs are deliberately wrong.
 constexpr int kAblNoStore = 4, kAblNoColour = 8, kAblNoIdct = 16;
+// Output format bit (include/hjd.h HJD_OUT_BGR24): 3-byte B,G,R pixels
+// instead of 4-byte BGRX words.
+constexpr int kOutBgr24 = 32;
+template <int kVariant>
+constexpr int kOutBytes = (kVariant & kOutBgr24) != 0 ? 3 : 4;
 
-// 4 horizontally adjacent BGRX pixels at row + loff.  `row` is wave-uniform
+// 4 horizontally adjacent pixels (BGRX words p0..p3) at row + loff.  `row` is wave-uniform
 // (SGPRs) and loff a 32-bit per-lane byte offset, so the store uses the
 // scalar-base addressing form (no 64-bit address arithmetic per row).  kFull:
 // the whole strip row lies inside the frame and rows are 16-byte aligned ->
 // one global_store_dwordx4 (nt by default: the output is streamed and never
 // re-read by the kernel); otherwise per-pixel guarded dword stores (x = the
-// first pixel's column).
+// first pixel's column).  BGR24: the four pixels are repacked into 12 bytes
+// (three v_perm) and stored as one dwordx3 (rows 4-byte aligned), or as
+// guarded bytes on edge strips.
 template <bool kFull, int kVariant = 0>
 __device__ __forceinline__ void store4(uint8_t* __restrict__ row, uint32_t loff, int x, int width, uint32_t p0,
                                        uint32_t p1, uint32_t p2, uint32_t p3)
@@ -180,7 +187,26 @@ __device__ __forceinline__ void store4(uint8_t* __restrict__ row, uint32_t loff,
         asm volatile("" ::"v"(p0), "v"(p1), "v"(p2), "v"(p3));
         return;
     }
-    if constexpr (kFull) {
+    if constexpr ((kVariant & kOutBgr24) != 0) {
+        if constexpr (kFull) {
+            typedef unsigned int u32x3 __attribute__((ext_vector_type(3), aligned(4)));
+            typedef __attribute__((address_space(1))) u32x3 gvec3;
+            const u32x3 v = {perm(p1, p0, 0x04020100u),    // b0 g0 r0 b1
+                             perm(p2, p1, 0x05040201u),    // g1 r1 b2 g2
+                             perm(p3, p2, 0x06050402u)};   // r2 b3 g3 r3
+            __builtin_nontemporal_store(v, (gvec3*)dst);
+        } else {
+            gbyte* d8 = (gbyte*)dst;
+            const uint32_t px[4] = {p0, p1, p2, p3};
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (x + k < width) {
+                    d8[3 * k] = static_cast<uint8_t>(px[k]);
+                    d8[3 * k + 1] = static_cast<uint8_t>(px[k] >> 8);
+                    d8[3 * k + 2] = static_cast<uint8_t>(px[k] >> 16);
+                }
+        }
+    } else if constexpr (kFull) {
         typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
         const u32x4 v = {p0, p1, p2, p3};
         typedef __attribute__((address_space(1))) u32x4 gvec;
@@ -225,9 +251,10 @@ __device__ __forceinline__ void colour_stage(const char* __restrict__ slots, int
     const int cg = lane & 31;     // 4-pixel column group within the 128-px strip
     const int x0 = cg * 4;
     const int xa = x_base + x0;
+    constexpr int kPx = kOutBytes<kVariant>;   // output bytes per pixel
     const int ylane = 2 * (lane >> 5);   // this half-wave's row offset
-    const uint32_t loff = static_cast<uint32_t>(x0 * 4) + static_cast<uint32_t>(ylane) * static_cast<uint32_t>(pitch);
-    uint8_t* const strip = out + static_cast<int64_t>(y_base) * pitch + static_cast<int64_t>(x_base) * 4;
+    const uint32_t loff = static_cast<uint32_t>(x0 * kPx) + static_cast<uint32_t>(ylane) * static_cast<uint32_t>(pitch);
+    uint8_t* const strip = out + static_cast<int64_t>(y_base) * pitch + static_cast<int64_t>(x_base) * kPx;
     if constexpr (kSampling == 1) {
         const int m = cg >> 2;        // MCU within strip
         const int xm = x0 & 15;       // x within MCU: 0,4,8,12
@@ -312,7 +339,7 @@ __device__ __forceinline__ void colour_stage(const char* __restrict__ slots, int
             const ChromaTerms c1 = chroma_terms<1>(cu, cv);
             const ChromaPair p0 = pair_of(c0, c0), p1 = pair_of(c1, c1);
             const uint32_t lo = static_cast<uint32_t>(y) * static_cast<uint32_t>(pitch) +
-                                static_cast<uint32_t>(cu4 * 16);
+                                static_cast<uint32_t>(cu4 * 4 * kPx);
             const int xu = x_base + cu4 * 4;
             const bool flagged = __builtin_amdgcn_ballot_w64((p0.flagged | p1.flagged) != 0) != 0;
             if (kFull || y_base + y < height) {
@@ -336,7 +363,7 @@ __device__ __forceinline__ void colour_stage(const char* __restrict__ slots, int
             const uint32_t g01 = sat_pk_u8(static_cast<uint32_t>(sy.x));   // bytes g0 g1
             const uint32_t g23 = sat_pk_u8(static_cast<uint32_t>(sy.y));
             const uint32_t lo = static_cast<uint32_t>(y) * static_cast<uint32_t>(pitch) +
-                                static_cast<uint32_t>(cu4 * 16);
+                                static_cast<uint32_t>(cu4 * 4 * kPx);
             if (kFull || y_base + y < height)
                 store4<kFull, kVariant>(strip, lo, x_base + cu4 * 4, width, perm(g01, g01, 0x0c000000u),
                                         perm(g01, g01, 0x0c010101u), perm(g23, g23, 0x0c000000u),

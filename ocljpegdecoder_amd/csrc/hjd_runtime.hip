@@ -81,6 +81,7 @@ struct hjd_plan {
     FrameDev* d_frames = nullptr;
     int* d_qt = nullptr;        // natural-order tables [nq][64]
     int variant = 0;            // kernel variant bits (hjd_plan_set_variant)
+    int out_format = HJD_OUT_BGRX;   // common output format of all frames
 };
 
 static int geometry(int width, int height, int sampling, int& mcu_w, int& mcu_h, int& bpm, int& tasks_mcus);
@@ -89,7 +90,7 @@ static int decode_grid(int sampling, int fmt, int64_t tasks);
 int hjd_internal::ctx_num_cu(const hjd_ctx* ctx) { return ctx->num_cu; }
 
 int64_t hjd_internal::make_frame_record(int width, int height, int sampling, int64_t coef_base, int64_t out_base,
-                                        int pitch, const int qt_index[3], FrameRecord* rec)
+                                        int pitch, const int qt_index[3], FrameRecord* rec, int out_format)
 {
     int mw, mh, bpm, tasks_mcus;
     int rc = geometry(width, height, sampling, mw, mh, bpm, tasks_mcus);
@@ -107,14 +108,14 @@ int64_t hjd_internal::make_frame_record(int width, int height, int sampling, int
     d.mcu_w = mw;
     d.strips = (mw + tasks_mcus - 1) / tasks_mcus;
     for (int c = 0; c < 3; ++c) d.qt[c] = qt_index ? qt_index[c] : 0;
-    d.vec_ok = ((pitch & 15) == 0 && (out_base & 15) == 0) ? 1 : 0;
+    d.vec_ok = out_vector_ok(out_format, pitch, out_base) ? 1 : 0;
     memcpy(rec, &d, sizeof(d));
     return static_cast<int64_t>(d.strips) * mh;
 }
 
 int hjd_internal::launch_decode(int device, int num_cu, int sampling, int input_format, int variant,
                                 const void* d_coefs, const int32_t* d_qt_nat, const FrameRecord* d_frames,
-                                int nframes, int64_t tasks, void* d_out, void* stream, int grid_blocks)
+                                int nframes, int64_t tasks, void* d_out, void* stream, int grid_blocks, int out_format)
 {
     HJD_HIP(hipSetDevice(device));
     const int fmt = input_format == HJD_IN_Q16_ZIGZAG ? 0 : 1;
@@ -122,11 +123,26 @@ int hjd_internal::launch_decode(int device, int num_cu, int sampling, int input_
     SamplingGeom sg;
     if (!sampling_geom(sampling, &sg)) return set_error(HJD_E_INVALID, "unsupported sampling %d", sampling);
     const int grid = grid_blocks > 0 ? grid_blocks : decode_grid(sampling, fmt, tasks);
+    if (out_format != HJD_OUT_BGRX && out_format != HJD_OUT_BGR24)
+        return set_error(HJD_E_INVALID, "unknown output format %d", out_format);
+    using K = void (*)(const void*, const int*, const FrameDev*, int, int64_t, uint8_t*);
+    if (out_format == HJD_OUT_BGR24) {   // [sampling index][input format], default variant
+        static const K kTable24[8] = {
+            hjd::decode_kernel<0, 0, hjd::kOutBgr24>, hjd::decode_kernel<0, 1, hjd::kOutBgr24>,
+            hjd::decode_kernel<1, 0, hjd::kOutBgr24>, hjd::decode_kernel<1, 1, hjd::kOutBgr24>,
+            hjd::decode_kernel<2, 0, hjd::kOutBgr24>, hjd::decode_kernel<2, 1, hjd::kOutBgr24>,
+            hjd::decode_kernel<3, 0, hjd::kOutBgr24>, hjd::decode_kernel<3, 1, hjd::kOutBgr24>};
+        if (variant != 0) return set_error(HJD_E_INVALID, "kernel variants are BGRX-only");
+        hipLaunchKernelGGL(kTable24[(sg.index << 1) | fmt], dim3(grid), dim3(hjd::kGroupThreads), 0,
+                           static_cast<hipStream_t>(stream), d_coefs, d_qt_nat,
+                           reinterpret_cast<const FrameDev*>(d_frames), nframes, tasks, static_cast<uint8_t*>(d_out));
+        HJD_HIP(hipGetLastError());
+        return HJD_OK;
+    }
 #ifdef HJD_ABLATION
     if (fmt == 0 && variant > 1) {
         if (sg.index > 1) return hjd_internal::set_error(HJD_E_INVALID, "ablation variants are 4:4:4/4:2:0 only");
-        using KA = void (*)(const void*, const int*, const FrameDev*, int, int64_t, uint8_t*);
-        KA k = nullptr;
+        K k = nullptr;
         const bool s420 = sampling == HJD_YUV420;
         switch (variant) {
         case 4: k = s420 ? hjd::decode_kernel<1, 0, 4> : hjd::decode_kernel<0, 0, 4>; break;
@@ -145,7 +161,6 @@ int hjd_internal::launch_decode(int device, int num_cu, int sampling, int input_
 #endif
     // [sampling index][input format][variant bits 0-1]
     const int key = (sg.index << 3) | (fmt << 2) | (variant & 3);
-    using K = void (*)(const void*, const int*, const FrameDev*, int, int64_t, uint8_t*);
 #define HJD_K4(S, F) hjd::decode_kernel<S, F, 0>, hjd::decode_kernel<S, F, 1>, hjd::decode_kernel<S, F, 2>, \
                      hjd::decode_kernel<S, F, 3>
     static const K kTable[32] = {HJD_K4(0, 0), HJD_K4(0, 1), HJD_K4(1, 0), HJD_K4(1, 1),
@@ -243,6 +258,9 @@ int hjd_plan_create(hjd_ctx* ctx, const hjd_frame* frames, int nframes, int inpu
     std::vector<FrameDev> fd(static_cast<size_t>(std::max(nframes, 1)));
     int64_t tasks = 0, pixels = 0, blocks = 0;
     int sampling = nframes > 0 ? frames[0].sampling : HJD_YUV420;
+    const int out_format = nframes > 0 ? frames[0].out_format : HJD_OUT_BGRX;
+    const int obytes = hjd_internal::out_format_bytes(out_format);
+    if (!obytes) return fail(HJD_E_INVALID, "unknown output format %d", out_format);
     for (int i = 0; i < nframes; ++i) {
         const hjd_frame& f = frames[i];
         int mw, mh, bpm, tasks_mcus;
@@ -250,9 +268,10 @@ int hjd_plan_create(hjd_ctx* ctx, const hjd_frame* frames, int nframes, int inpu
         if (rc) return fail(rc, "frame %d: %s", i, g_last_error.c_str());
         if (f.sampling != sampling)
             return fail(HJD_E_INVALID, "frame %d: mixed sampling in one plan (use one plan per sampling)", i);
-        if (f.out_pitch < 4 * f.width || (f.out_pitch & 3) || (f.out_offset & 3))
+        if (f.out_format != out_format)
+            return fail(HJD_E_INVALID, "frame %d: mixed output formats in one plan (use one plan per format)", i);
+        if (f.out_pitch < static_cast<int64_t>(obytes) * f.width || (f.out_pitch & 3) || (f.out_offset & 3))
             return fail(HJD_E_INVALID, "frame %d: bad output pitch/offset", i);
-        if (f.reserved != 0) return fail(HJD_E_INVALID, "frame %d: reserved field must be 0", i);
         FrameDev& d = fd[i];
         if (input_format == HJD_IN_Q16_ZIGZAG) {
             for (int c = 0; c < 3; ++c)
@@ -269,7 +288,7 @@ int hjd_plan_create(hjd_ctx* ctx, const hjd_frame* frames, int nframes, int inpu
         d.mcu_w = mw;
         d.strips = (mw + tasks_mcus - 1) / tasks_mcus;
         for (int c = 0; c < 3; ++c) d.qt[c] = input_format == HJD_IN_Q16_ZIGZAG ? f.qt_index[c] : 0;
-        d.vec_ok = ((f.out_pitch & 15) == 0 && (f.out_offset & 15) == 0) ? 1 : 0;
+        d.vec_ok = hjd_internal::out_vector_ok(out_format, f.out_pitch, static_cast<int64_t>(f.out_offset)) ? 1 : 0;
         tasks += static_cast<int64_t>(d.strips) * mh;
         pixels += static_cast<int64_t>(f.width) * f.height;
         blocks += static_cast<int64_t>(mw) * mh * bpm;
@@ -281,6 +300,7 @@ int hjd_plan_create(hjd_ctx* ctx, const hjd_frame* frames, int nframes, int inpu
     p->ctx = ctx;
     p->input_format = input_format;
     p->sampling = sampling;
+    p->out_format = out_format;
     p->nframes = nframes;
     p->tasks = tasks;
     p->pixels = pixels;
@@ -368,7 +388,7 @@ int hjd_plan_launch(hjd_plan* plan, const void* d_coefs, void* d_out, void* stre
     return hjd_internal::launch_decode(plan->ctx->device, plan->ctx->num_cu, plan->sampling, plan->input_format,
                                        plan->variant, d_coefs, plan->d_qt,
                                        reinterpret_cast<const hjd_internal::FrameRecord*>(plan->d_frames),
-                                       plan->nframes, plan->tasks, d_out, stream, grid_blocks);
+                                       plan->nframes, plan->tasks, d_out, stream, grid_blocks, plan->out_format);
 }
 
 int hjd_idct_blocks(hjd_ctx* ctx, const int32_t* d_in, int32_t* d_out, int64_t nblocks, void* stream)

@@ -86,17 +86,22 @@ def decode_coefs_batch(datas: Sequence[bytes], nthreads: int = 0) -> List[np.nda
     return outs
 
 
-def decode_jpeg(ctx, data: bytes, stream=None):
-    """JPEG bytes -> (H, W) int32 device tensor of BGRX words (host Huffman,
-    then the fused kernel on the device)."""
+def decode_jpeg(ctx, data: bytes, stream=None, out_format: int = 0):
+    """JPEG bytes -> device pixels (host Huffman, then the fused kernel on the
+    device): an (H, W) int32 tensor of BGRX words, or with out_format=OUT_BGR24
+    an (H, pitch) uint8 tensor of B,G,R bytes (pitch = (3W+3)&~3, the 24-bpp
+    BMP row)."""
     import torch
-    from .backend import IN_Q16_ZIGZAG, FrameSpec, Plan
+    from .backend import IN_Q16_ZIGZAG, OUT_BGR24, FrameSpec, Plan, default_pitch
     coefs, info = decode_coefs(data)
     dev = torch.device("cuda", ctx.device)
     d_coefs = torch.from_numpy(coefs).to(dev)
-    out = torch.empty((info.height, info.width), dtype=torch.int32, device=dev)
-    plan = Plan(ctx, [FrameSpec(info.width, info.height, info.sampling, qt_index=(0, 1, 2))], IN_Q16_ZIGZAG,
-                qtables=info.qt)
+    if out_format == OUT_BGR24:
+        out = torch.empty((info.height, default_pitch(info.width, OUT_BGR24)), dtype=torch.uint8, device=dev)
+    else:
+        out = torch.empty((info.height, info.width), dtype=torch.int32, device=dev)
+    plan = Plan(ctx, [FrameSpec(info.width, info.height, info.sampling, qt_index=(0, 1, 2), out_format=out_format)],
+                IN_Q16_ZIGZAG, qtables=info.qt)
     plan.launch(d_coefs, out, stream)
     return out
 
@@ -182,8 +187,13 @@ class GpuDecoder:
         self.handle = h
         self._n = 0
 
+    def set_output_format(self, out_format: int):
+        """OUT_BGRX (default) or OUT_BGR24 for the following decode() calls."""
+        check(self.lib.hjd_gdec_set_output_format(self.handle, int(out_format)), "hjd_gdec_set_output_format")
+
     def decode(self, datas: Sequence[bytes], outs, stream=None):
-        """outs: contiguous device tensors (H, W) int32 (or (H, pitch/4))."""
+        """outs: contiguous device tensors, one row per image row: (H, W) int32
+        (or (H, pitch/4)) for BGRX, (H, pitch) uint8 for BGR24."""
         _keep, arr_d, arr_s = _byte_arrays(datas)
         n = len(datas)
         if len(outs) != n:
@@ -240,7 +250,7 @@ class GpuJpegStream:
     each batch is Huffman-decoded and converted to BGRX on the GPU."""
 
     def __init__(self, ctx, max_frames: int, max_scan_bytes: int, max_blocks: int, nslots: int = 3,
-                 nthreads: int = 0):
+                 nthreads: int = 0, out_format: int = 0):
         self.lib = _lib.load()
         self.ctx = ctx
         h = ctypes.c_void_p()
@@ -248,6 +258,12 @@ class GpuJpegStream:
                                           int(nslots), int(nthreads), ctypes.byref(h)), "hjd_gstream_create")
         self.handle = h
         self._keep = []
+        if out_format:
+            self.set_output_format(out_format)
+
+    def set_output_format(self, out_format: int):
+        """OUT_BGRX or OUT_BGR24 (between sync() and the next submit)."""
+        check(self.lib.hjd_gstream_set_output_format(self.handle, int(out_format)), "hjd_gstream_set_output_format")
 
     def submit(self, data: bytes, out, out_pitch: Optional[int] = None):
         """out: contiguous device tensor, or a (pinned) host tensor / numpy
@@ -299,18 +315,31 @@ class GpuJpegStream:
             pass
 
 
-def bmp_header(width: int, height: int) -> bytes:
-    """The reference's 54-byte BMP header (src/decoder.cpp:372-394): 32 bpp, top-down."""
+def bmp_header(width: int, height: int, bpp: int = 32) -> bytes:
+    """The reference's 54-byte BMP header (src/decoder.cpp:372-394): 32 bpp,
+    top-down; bpp=24 gives the 24-bpp counterpart (rows padded to 4 bytes)."""
     lib = _lib.load()
     h = (ctypes.c_uint8 * 54)()
-    check(lib.hjd_bmp_header(int(width), int(height), h), "hjd_bmp_header")
+    if bpp == 32:
+        check(lib.hjd_bmp_header(int(width), int(height), h), "hjd_bmp_header")
+    elif bpp == 24:
+        check(lib.hjd_bmp_header_bgr24(int(width), int(height), h), "hjd_bmp_header_bgr24")
+    else:
+        raise ValueError("bpp must be 32 or 24")
     return bytes(h)
 
 
-def bmp_bytes(bgrx) -> bytes:
-    """A BMP file exactly as the reference writes it from the GPU path
-    (header + the H x W BGRX words)."""
-    a = np.ascontiguousarray(bgrx).view(np.uint32)
+def bmp_bytes(pixels, width: Optional[int] = None) -> bytes:
+    """A BMP file from decoded pixels, as the reference writes it from the GPU
+    path: an (H, W) array of BGRX words gives the reference's 32-bpp file; an
+    (H, pitch) uint8 array of BGR24 rows (pitch = (3W+3)&~3, as decode_jpeg
+    returns with OUT_BGR24) gives the 24-bpp file (width W required)."""
+    a = np.ascontiguousarray(pixels)
+    if a.dtype == np.uint8:
+        if width is None or a.shape[1] != (3 * width + 3) & ~3:
+            raise ValueError("BGR24 rows need width and pitch (3*width+3)&~3")
+        return bmp_header(width, a.shape[0], 24) + a.tobytes()
+    a = a.view(np.uint32)
     return bmp_header(a.shape[1], a.shape[0]) + a.astype("<u4").tobytes()
 
 

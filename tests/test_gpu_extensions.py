@@ -154,3 +154,89 @@ def test_stream_paths(hjd, ctx):
         gs.sync()
     for o, e in zip(outs, exps):
         np.testing.assert_array_equal(to_u32(o), e)
+
+
+# ---- BGR24 output (SURVEY.md s8(f) rank 4 "RGB24 writer") -------------------
+def _bgr24(bgrx):
+    """(H, W) BGRX words -> (H, 3W) bytes B, G, R."""
+    return np.ascontiguousarray(bgrx).view(np.uint8).reshape(bgrx.shape[0], bgrx.shape[1], 4)[..., :3].reshape(
+        bgrx.shape[0], -1)
+
+
+def _decode24(hjd, ctx, coefs, qt, w, h, s, pitch, guard=64, fmt=0):
+    import torch
+    buf = torch.full((guard * 2 + pitch * h,), 0xA5, dtype=torch.uint8, device="cuda")
+    spec = hjd.FrameSpec(w, h, s, out_offset=guard, out_pitch=pitch, qt_index=(0, 1, 2), out_format=hjd.OUT_BGR24)
+    plan = hjd.Plan(ctx, [spec], fmt, qtables=qt if fmt == 0 else None)
+    plan.launch(torch.from_numpy(np.ascontiguousarray(coefs)).cuda(), buf)
+    torch.cuda.synchronize()
+    full = buf.cpu().numpy()
+    rows = full[guard:guard + pitch * h].reshape(h, pitch)
+    # nothing outside the W x 3 bytes of each row (pads, guard bands) is written
+    mask = np.ones(full.shape, bool)
+    mask[guard:guard + pitch * h].reshape(h, pitch)[:, :3 * w] = False
+    assert (full[mask] == 0xA5).all()
+    return rows[:, :3 * w]
+
+
+@pytest.mark.parametrize("s", [0, 1, YUV422, GRAY])
+@pytest.mark.parametrize("w,h,pad", [(1, 1, 0), (17, 9, 0), (129, 33, 4), (385, 16, 0), (1920, 40, 0),
+                                     (2049, 31, 12)])
+def test_bgr24_vs_oracle(hjd, ctx, s, w, h, pad):
+    coefs, qt = O.synthetic_coefs(w, h, s, seed=w + 7 * h + s)
+    pitch = hjd.default_pitch(w, hjd.OUT_BGR24) + pad
+    got = _decode24(hjd, ctx, coefs, qt, w, h, s, pitch)
+    np.testing.assert_array_equal(got, _bgr24(O.decode_q16(coefs, qt, w, h, s)))
+
+
+def test_bgr24_i32_input_and_golden(hjd, ctx):
+    """BGR24 from the idct.h-compat input on the reference's golden files ==
+    the reference's BGRX without the pad byte."""
+    for name in O.golden_cases():
+        c = O.load_case(name)
+        w, h, s = int(c["width"]), int(c["height"]), int(c["sampling"])
+        nat = O.dequant_natural(c["coefs_q16"], c["qt"], s)
+        got = _decode24(hjd, ctx, nat, None, w, h, s, hjd.default_pitch(w, hjd.OUT_BGR24), fmt=1)
+        np.testing.assert_array_equal(got, _bgr24(c["bgrx"]), err_msg=name)
+
+
+def test_bgr24_jpeg_paths_and_d2h_sink(hjd, ctx):
+    """decode_jpeg, GpuDecoder and the GPU-entropy stream's device and host
+    (D2H) sinks in BGR24, on golden and extension files; the 24-bpp BMP of the
+    result opens in Pillow with the same pixels."""
+    import io
+    import os
+    import torch
+    from PIL import Image
+    datas = [open(os.path.join(O.GOLDEN, n + ".jpg"), "rb").read() for n in O.golden_cases()] + _jpegs()
+    exps, infos = zip(*[_expected(hjd, d) for d in datas])
+    pitches = [hjd.default_pitch(i.width, hjd.OUT_BGR24) for i in infos]
+    for d, e, i, p in zip(datas, exps, infos, pitches):
+        out = hjd.decode_jpeg(ctx, d, out_format=hjd.OUT_BGR24)
+        assert tuple(out.shape) == (i.height, p)
+        rows = out.cpu().numpy()
+        np.testing.assert_array_equal(rows[:, :3 * i.width], _bgr24(e))
+    im = Image.open(io.BytesIO(hjd.bmp_bytes(rows, width=infos[-1].width)))
+    np.testing.assert_array_equal(np.asarray(im.convert("RGB"))[..., ::-1].reshape(rows.shape[0], -1),
+                                  _bgr24(exps[-1]))
+    outs = [torch.full((i.height, p), 0xA5, dtype=torch.uint8, device="cuda") for i, p in zip(infos, pitches)]
+    with hjd.GpuDecoder(ctx, len(datas), sum(map(len, datas)), sum(i.nblocks for i in infos), 1024) as gd:
+        gd.set_output_format(hjd.OUT_BGR24)
+        gd.decode(datas, outs)
+        gd.sync()
+    for o, e, i in zip(outs, exps, infos):
+        np.testing.assert_array_equal(o.cpu().numpy()[:, :3 * i.width], _bgr24(e))
+    dev_outs = [torch.full((i.height, p), 0xA5, dtype=torch.uint8, device="cuda") for i, p in zip(infos, pitches)]
+    host_outs = [torch.full((i.height, p), 0xA5, dtype=torch.uint8).pin_memory() for i, p in zip(infos, pitches)]
+    with hjd.GpuJpegStream(ctx, max_frames=4, max_scan_bytes=sum(map(len, datas)),
+                           max_blocks=sum(i.nblocks for i in infos), out_format=hjd.OUT_BGR24) as gs:
+        for k, d in enumerate(datas):
+            gs.submit(d, dev_outs[k] if k % 2 else host_outs[k])
+        gs.sync()
+        with pytest.raises(Exception):
+            gs.submit(datas[0], dev_outs[0])
+            gs.set_output_format(hjd.OUT_BGRX)   # refused while a batch is open
+        gs.sync()
+    for k, (e, i) in enumerate(zip(exps, infos)):
+        got = (dev_outs[k].cpu() if k % 2 else host_outs[k]).numpy()
+        np.testing.assert_array_equal(got[:, :3 * i.width], _bgr24(e), err_msg=f"frame {k}")

@@ -188,3 +188,24 @@ def test_bmp_header_matches_reference_layout(hjd):
         assert hjd.bmp_header(w, h) == exp
     px = np.arange(12, dtype=np.uint32).reshape(3, 4)
     assert hjd.bmp_bytes(px) == hjd.bmp_header(4, 3) + px.astype("<u4").tobytes()
+
+
+def test_bmp_files_open_in_pillow(hjd):
+    """Both sinks' BMP files (the reference's 32-bpp BGRX layout and the
+    24-bpp BGR24 extension, rows padded to 4 bytes) decode in an independent
+    BMP reader to the intended RGB pixels."""
+    import io
+    from PIL import Image
+    rng = np.random.default_rng(9)
+    for w, h in ((1, 1), (5, 3), (13, 7), (64, 2)):
+        rgb = rng.integers(0, 256, (h, w, 3), dtype=np.uint8)
+        bgrx = (rgb[..., 2].astype(np.uint32) | (rgb[..., 1].astype(np.uint32) << 8) |
+                (rgb[..., 0].astype(np.uint32) << 16))
+        pitch = hjd.default_pitch(w, hjd.OUT_BGR24)
+        rows = np.zeros((h, pitch), np.uint8)
+        rows[:, :3 * w] = rgb[..., ::-1].reshape(h, 3 * w)
+        for data in (hjd.bmp_bytes(bgrx), hjd.bmp_bytes(rows, width=w)):
+            im = Image.open(io.BytesIO(data))
+            assert im.size == (w, h)
+            np.testing.assert_array_equal(np.asarray(im.convert("RGB")), rgb)
+        assert len(hjd.bmp_bytes(rows, width=w)) == 54 + pitch * h
