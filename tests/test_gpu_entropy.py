@@ -280,3 +280,40 @@ def test_gstream_concurrent_submitters(hjd, ctx):
         coefs, _ = hjd.decode_coefs(d)
         exp = O.decode_q16(coefs, info.qt, info.width, info.height, info.sampling)
         np.testing.assert_array_equal(o.cpu().numpy().view(np.uint32), exp)
+
+
+@pytest.mark.parametrize("sub_bits", [32, 96, 1024])
+def test_random_sweep_on_device(hjd, ctx, sub_bits):
+    """The device kernels on seeded random files of all four samplings, with
+    and without restart intervals, pure noise included (the host mirror of
+    the same logic is swept in test_entropy_emulation.py): coefficients equal
+    the host decoder's, batches of 40."""
+    from PIL import Image
+    rng = np.random.default_rng(77 + sub_bits)
+    datas = []
+    while len(datas) < 160:
+        w, h = int(rng.integers(8, 300)), int(rng.integers(8, 200))
+        kw = {}
+        r = int(rng.integers(0, 3))
+        if r == 1:
+            kw["restart_marker_blocks"] = int(rng.integers(1, 6))
+        elif r == 2:
+            kw["restart_marker_rows"] = 1
+        img = (rng.integers(0, 256, (h, w, 3), dtype=np.uint8) if rng.integers(0, 3) == 0 else
+               np.clip(rng.normal(128, rng.uniform(0, 60), (h, w, 3)), 0, 255).astype(np.uint8))
+        im = Image.fromarray(img)
+        if rng.integers(0, 5) == 0:
+            im = im.convert("L")
+        b = io.BytesIO()
+        try:
+            im.save(b, format="JPEG", quality=int(rng.integers(20, 101)), subsampling=int(rng.choice([0, 1, 2])), **kw)
+        except OSError:
+            continue
+        datas.append(b.getvalue())
+    for k in range(0, len(datas), 40):
+        chunk = datas[k:k + 40]
+        got, status = _coefs_gpu(hjd, ctx, chunk, sub_bits)
+        for i, (d, g) in enumerate(zip(chunk, got)):
+            ref, _ = hjd.decode_coefs(d)
+            np.testing.assert_array_equal(g, ref, err_msg=f"file {k + i} S={sub_bits}")
+        assert all(s & ~1 == 0 for s in status)
