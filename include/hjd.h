@@ -55,6 +55,12 @@ enum hjd_out_format {
     HJD_OUT_BGR24 = 1
 };
 
+/* Kernel selection of a plan (hjd_plan_set_kernel).  Both kernels produce
+ * identical pixels; AUTO takes the latency kernel (one workgroup per 48-block
+ * task, six waves sharing it) for launches of few tasks -- a single frame --
+ * and the persistent streaming kernel for batches. */
+enum hjd_kernel_mode { HJD_KERNEL_AUTO = 0, HJD_KERNEL_PERSISTENT = 1, HJD_KERNEL_LATENCY = 2 };
+
 /* Coefficient input format. */
 enum hjd_input_format {
     /* int16 quantised coefficients in zigzag order, exactly as Huffman decoding
@@ -116,6 +122,7 @@ int hjd_plan_destroy(hjd_plan* plan);
  * non-temporal output stores; bit 1: workgroup-interleaved task order.
  * Results are identical for every variant. */
 int hjd_plan_set_variant(hjd_plan* plan, int variant);
+int hjd_plan_set_kernel(hjd_plan* plan, int mode);   /* hjd_kernel_mode */
 int64_t hjd_plan_tasks(const hjd_plan* plan);      /* work items (strips) */
 int64_t hjd_plan_pixels(const hjd_plan* plan);     /* visible pixels */
 int64_t hjd_plan_coef_bytes(const hjd_plan* plan); /* algorithmic input bytes */

@@ -14,6 +14,9 @@ from .backend import (  # noqa: E402
     IN_I32_NATURAL,
     IN_Q16_ZIGZAG,
     OTHER,
+    KERNEL_AUTO,
+    KERNEL_LATENCY,
+    KERNEL_PERSISTENT,
     OUT_BGR24,
     OUT_BGRX,
     OUT_BYTES,
@@ -40,5 +43,5 @@ __all__ = [
     "decode_coefs_batch", "decode_jpeg", "emulate_entropy",
     "parse",
     "Context", "FrameSpec", "Plan", "decode_frame", "device_count", "frame_blocks", "mcu_geometry",
-    "YUV444", "YUV420", "YUV422", "GRAY", "OTHER", "block_components", "OUT_BGRX", "OUT_BGR24", "OUT_BYTES", "default_pitch", "IN_Q16_ZIGZAG", "IN_I32_NATURAL",
+    "YUV444", "YUV420", "YUV422", "GRAY", "OTHER", "block_components", "KERNEL_AUTO", "KERNEL_PERSISTENT", "KERNEL_LATENCY", "OUT_BGRX", "OUT_BGR24", "OUT_BYTES", "default_pitch", "IN_Q16_ZIGZAG", "IN_I32_NATURAL",
 ]

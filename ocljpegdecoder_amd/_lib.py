@@ -62,6 +62,7 @@ SIGNATURES = {
                                        c_i32p, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
     "hjd_plan_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "hjd_plan_set_variant": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "hjd_plan_set_kernel": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "hjd_plan_tasks": (ctypes.c_int64, [ctypes.c_void_p]),
     "hjd_plan_pixels": (ctypes.c_int64, [ctypes.c_void_p]),
     "hjd_plan_coef_bytes": (ctypes.c_int64, [ctypes.c_void_p]),

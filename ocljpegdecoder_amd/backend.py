@@ -26,6 +26,8 @@ _GEOM = {YUV444: (8, 8, 3, 1), YUV420: (16, 16, 6, 4), YUV422: (16, 8, 4, 2), GR
 IN_Q16_ZIGZAG = 0
 IN_I32_NATURAL = 1
 
+KERNEL_AUTO, KERNEL_PERSISTENT, KERNEL_LATENCY = 0, 1, 2   # include/hjd.h hjd_kernel_mode
+
 OUT_BGRX = 0    # 4 B/px: B, G, R, 0 (the reference's RGB32 / 32-bpp BMP rows)
 OUT_BGR24 = 1   # 3 B/px: B, G, R (extension: 24-bpp BMP rows)
 OUT_BYTES = {OUT_BGRX: 4, OUT_BGR24: 3}
@@ -186,6 +188,10 @@ class Plan:
         if t.device.index != self.ctx.device:
             raise ValueError(f"{what} is on {t.device}, plan is for device {self.ctx.device}")
         return t.data_ptr()
+
+    def set_kernel(self, mode: int):
+        """KERNEL_AUTO (default), KERNEL_PERSISTENT or KERNEL_LATENCY; identical outputs."""
+        check(self.lib.hjd_plan_set_kernel(self.handle, int(mode)), "hjd_plan_set_kernel")
 
     def set_variant(self, variant: int):
         """Kernel variant bits (tuning/A-B only; outputs are identical)."""

@@ -48,7 +48,7 @@ int64_t make_frame_record(int width, int height, int sampling, int64_t coef_base
 // qtables (no host synchronisation, safe to call from any host thread).
 int launch_decode(int device, int num_cu, int sampling, int input_format, int variant, const void* d_coefs,
                   const int32_t* d_qt_nat, const FrameRecord* d_frames, int nframes, int64_t tasks, void* d_out,
-                  void* stream, int grid_blocks, int out_format = 0);
+                  void* stream, int grid_blocks, int out_format = 0, int kernel_mode = 0);
 
 // Bytes per output pixel of an HJD_OUT_* format (0 if unknown).
 inline int out_format_bytes(int out_format) { return out_format == 0 ? 4 : out_format == 1 ? 3 : 0; }

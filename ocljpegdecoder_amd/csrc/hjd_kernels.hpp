@@ -244,9 +244,12 @@ __device__ __forceinline__ void emit_row4(uint8_t* __restrict__ row, uint32_t lo
     store4<kFull, kVariant>(row, loff, xa, width, q0, q1, q2, q3);
 }
 
-template <int kSampling, bool kFull, int kVariant>
+// kStride / u0: this wave converts colour units u0, u0 + kStride, ... of the
+// strip (the latency kernel spreads a task's units over its waves; the
+// persistent kernel converts all of them: kStride 1, u0 0).
+template <int kSampling, bool kFull, int kVariant, int kStride = 1>
 __device__ __forceinline__ void colour_stage(const char* __restrict__ slots, int lane, uint8_t* __restrict__ out,
-                                             int pitch, int width, int height, int y_base, int x_base)
+                                             int pitch, int width, int height, int y_base, int x_base, int u0 = 0)
 {
     const int cg = lane & 31;     // 4-pixel column group within the 128-px strip
     const int x0 = cg * 4;
@@ -259,7 +262,9 @@ __device__ __forceinline__ void colour_stage(const char* __restrict__ slots, int
         const int m = cg >> 2;        // MCU within strip
         const int xm = x0 & 15;       // x within MCU: 0,4,8,12
 #pragma unroll
-        for (int it = 0; it < 4; ++it) {
+        for (int k = 0; k < (4 + kStride - 1) / kStride; ++k) {
+            const int it = u0 + k * kStride;
+            if (kStride > 1 && it >= 4) break;
             const int p = it * 2 + (lane >> 5);   // row pair 0..7 within the MCU row
             const int y0 = 2 * p;
             const char* yblk = slots + (m * 6 + (y0 >> 3) * 2 + (xm >> 3)) * kSlotBytes + (xm & 7) * 2;
@@ -291,10 +296,12 @@ __device__ __forceinline__ void colour_stage(const char* __restrict__ slots, int
         const int m = cg >> 1;        // MCU within strip (16 x 8 px)
         const int xm = x0 & 7;        // 0 or 4
 #pragma unroll
-        for (int it = 0; it < 2; ++it) {
+        for (int k = 0; k < (4 + kStride - 1) / kStride; ++k) {
+            const int u = u0 + k * kStride;       // unit = (row pair it, row h)
+            if (kStride > 1 && u >= 4) break;
+            const int it = u >> 1, h = u & 1;
             const int p = it * 2 + (lane >> 5);   // row pair 0..3
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
+            {
                 const int y = 2 * p + h;
                 const char* base = slots + m * 3 * kSlotBytes + y * 16 + xm * 2;
                 const int2 sy = *reinterpret_cast<const int2*>(base);
@@ -324,7 +331,9 @@ __device__ __forceinline__ void colour_stage(const char* __restrict__ slots, int
         // reference's 4:2:0 path does in both directions, src/decoder.cpp:474-483).
         (void)loff;
 #pragma unroll 2
-        for (int it = 0; it < 6; ++it) {
+        for (int k = 0; k < (6 + kStride - 1) / kStride; ++k) {
+            const int it = u0 + k * kStride;
+            if (kStride > 1 && it >= 6) break;
             const int u = it * 64 + lane;
             const int y = u / 48;
             const int cu4 = u - y * 48;       // unit within the row
@@ -355,7 +364,9 @@ __device__ __forceinline__ void colour_stage(const char* __restrict__ slots, int
         // reference's conversion with U = V = 0 (src/decoder.cpp:367-370).
         (void)loff;
 #pragma unroll
-        for (int it = 0; it < 12; ++it) {
+        for (int k = 0; k < (12 + kStride - 1) / kStride; ++k) {
+            const int it = u0 + k * kStride;
+            if (kStride > 1 && it >= 12) break;
             const int u = it * 64 + lane;
             const int y = u / 96;
             const int cu4 = u - y * 96;
@@ -401,6 +412,30 @@ __device__ __forceinline__ constexpr int round_component(int i)
          : kSampling == 0 ? (i % 3)
          : kSampling == 3 ? 0
          : (i < 3 ? 0 : i == 3 ? 1 : i == 5 ? 2 : -1);
+}
+
+// Component (0 = Y, 1 = Cb, 2 = Cr) of task-local block b (MCU-major).
+template <int kSampling>
+__device__ __forceinline__ int block_component(int b)
+{
+    if constexpr (kSampling == 0) {
+        return b % 3;
+    } else if constexpr (kSampling == 1) {
+        const int j = b % 6;
+        return j < 4 ? 0 : j - 3;
+    } else if constexpr (kSampling == 2) {
+        const int j = b & 3;
+        return j < 2 ? 0 : j - 1;
+    } else {
+        return 0;
+    }
+}
+
+// Round i transforms luma blocks (runtime form of round_component(i) == 0).
+template <int kSampling>
+__device__ __forceinline__ bool round_is_luma(int i)
+{
+    return kSampling == 1 ? i < 4 : kSampling == 0 ? i % 3 == 0 : kSampling == 2 ? i < 3 : true;
 }
 
 // One round's row-pass inputs.  kFmt 0: int16 zigzag staged in the LDS slots
@@ -599,6 +634,102 @@ __global__ __launch_bounds__(kGroupThreads, 4) void decode_kernel(const void* __
         }
         wave_lds_sync();
     }
+}
+
+// Latency variant for small launches (one FHD frame: ~1000 tasks, about one
+// wave per SIMD for the persistent kernel, which then runs each task's six
+// IDCT rounds and four colour units back to back).  One 384-thread workgroup
+// per task: wave w stages and transforms round w's 8 blocks (its own transpose
+// buffer), one workgroup barrier, then the waves share the strip's colour
+// units.  Same device functions, same results; the critical path of a task
+// is one round + one colour unit instead of six + four.
+constexpr int kLatWaves = 6;
+constexpr int kLatThreads = 64 * kLatWaves;
+constexpr int kLatLds = kTaskBlocks * kSlotBytes + kLatWaves * 8 * kRowBufBlock;
+
+template <int kSampling, int kFmt, int kVariant>
+__global__ __launch_bounds__(kLatThreads) void decode_kernel_lat(const void* __restrict__ coefs,
+                                                                const int* __restrict__ qt_pool,
+                                                                const FrameDev* __restrict__ frames, int nframes,
+                                                                int64_t total_tasks, uint8_t* __restrict__ out)
+{
+    __shared__ __attribute__((aligned(16))) char lds[kLatLds];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // = this wave's IDCT round
+    const int lane = threadIdx.x & 63;
+    const int g = lane >> 3, r = lane & 7;
+    char* slots = lds;
+    char* rowbuf = lds + kTaskBlocks * kSlotBytes + wave * 8 * kRowBufBlock;
+    const int64_t task = blockIdx.x;
+    if (task >= total_tasks) return;
+    FrameCursor cc;
+    cursor_seek(cc, frames, nframes, total_tasks, task);
+    const TaskGeom tg = task_geom<kSampling>(cc, task);
+
+    const int b = round_block<kSampling>(wave, g);
+    int v[8];
+    if constexpr (kFmt == 0) {
+        // this lane's row of its block's qtable (the block's component may
+        // differ between lane groups in 4:2:2 round 4)
+        const int comp = block_component<kSampling>(b);
+        const int qt = comp == 0 ? cc.qt0 : (comp == 1 ? cc.qt1 : cc.qt2);
+        const int4* qp = reinterpret_cast<const int4*>(qt_pool + qt * 64 + r * 8);
+        const int4 qa = qp[0], qb = qp[1];
+        const int qrow[8] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
+        // stage this round's 8 blocks: lane (g, r) moves 16-B chunk r of block b
+        int4 v4 = make_int4(0, 0, 0, 0);
+        if (b < tg.nblk)
+            v4 = reinterpret_cast<const int4*>(static_cast<const short*>(coefs) + (tg.blk0 + b) * 64)[r];
+        *reinterpret_cast<int4*>(slots + b * kSlotBytes + r * 16) = v4;
+        wave_lds_sync();
+        const char* blk = slots + b * kSlotBytes;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const int coef = *reinterpret_cast<const short*>(blk + 2 * zz_of_natural(r * 8 + c));
+            v[c] = mul24(coef, qrow[c]);   // dequant (src/decoder.cpp:340)
+        }
+    } else {
+        int4 lo = make_int4(0, 0, 0, 0), hi = lo;
+        if (b < tg.nblk) {
+            const int4* p = reinterpret_cast<const int4*>(static_cast<const int*>(coefs) + (tg.blk0 + b) * 64 + r * 8);
+            lo = p[0];
+            hi = p[1];
+        }
+        v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
+        v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+    }
+    idct8<false>(v);
+    {
+        int4* dst = reinterpret_cast<int4*>(rowbuf + g * kRowBufBlock + r * kRowStride);
+        dst[0] = make_int4(v[0], v[1], v[2], v[3]);
+        dst[1] = make_int4(v[4], v[5], v[6], v[7]);
+    }
+    wave_lds_sync();
+    int c8[8];
+    {
+        const char* col = rowbuf + g * kRowBufBlock + r * 4;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) c8[k] = *reinterpret_cast<const int*>(col + k * kRowStride);
+    }
+    if (round_is_luma<kSampling>(wave))
+        idct8<true, kLumaLevel>(c8);
+    else
+        idct8<true>(c8);
+    {
+        char* blk = slots + b * kSlotBytes + r * 2;   // column r
+#pragma unroll
+        for (int k = 0; k < 8; ++k) *reinterpret_cast<short*>(blk + k * 16) = static_cast<short>(c8[k]);
+    }
+    __syncthreads();   // all 48 blocks' samples are in the slots
+
+    constexpr int kRows = KGeom<kSampling>::kMcuH;
+    constexpr int kStripW = KGeom<kSampling>::kStripW;
+    uint8_t* fout = out + cc.out_base;
+    if (cc.vec_ok && tg.x_base + kStripW <= cc.width && tg.y_base + kRows <= cc.height)
+        colour_stage<kSampling, true, kVariant, kLatWaves>(slots, lane, fout, cc.pitch, cc.width, cc.height,
+                                                            tg.y_base, tg.x_base, wave);
+    else
+        colour_stage<kSampling, false, kVariant, kLatWaves>(slots, lane, fout, cc.pitch, cc.width, cc.height,
+                                                             tg.y_base, tg.x_base, wave);
 }
 
 // IDCT only, out of place (the reference's batch_idct): one wave = 8 blocks.

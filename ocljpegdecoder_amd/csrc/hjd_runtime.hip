@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cstdarg>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <new>
@@ -82,7 +83,21 @@ struct hjd_plan {
     int* d_qt = nullptr;        // natural-order tables [nq][64]
     int variant = 0;            // kernel variant bits (hjd_plan_set_variant)
     int out_format = HJD_OUT_BGRX;   // common output format of all frames
+    int kernel_mode = HJD_KERNEL_AUTO;
 };
+
+constexpr int64_t kDefaultLatencyMaxTasks = 1024;   // measured: profiles/r01_latency_kernel.json
+
+// Launches of at most this many tasks take the latency kernel (one workgroup
+// per task) in HJD_KERNEL_AUTO mode; HJD_LAT_TASKS overrides it (tuning).
+static int64_t latency_max_tasks()
+{
+    static const int64_t v = [] {
+        const char* e = getenv("HJD_LAT_TASKS");
+        return e ? static_cast<int64_t>(atoll(e)) : int64_t(kDefaultLatencyMaxTasks);
+    }();
+    return v;
+}
 
 static int geometry(int width, int height, int sampling, int& mcu_w, int& mcu_h, int& bpm, int& tasks_mcus);
 static int decode_grid(int sampling, int fmt, int64_t tasks);
@@ -115,7 +130,8 @@ int64_t hjd_internal::make_frame_record(int width, int height, int sampling, int
 
 int hjd_internal::launch_decode(int device, int num_cu, int sampling, int input_format, int variant,
                                 const void* d_coefs, const int32_t* d_qt_nat, const FrameRecord* d_frames,
-                                int nframes, int64_t tasks, void* d_out, void* stream, int grid_blocks, int out_format)
+                                int nframes, int64_t tasks, void* d_out, void* stream, int grid_blocks, int out_format,
+                                int kernel_mode)
 {
     HJD_HIP(hipSetDevice(device));
     const int fmt = input_format == HJD_IN_Q16_ZIGZAG ? 0 : 1;
@@ -126,6 +142,23 @@ int hjd_internal::launch_decode(int device, int num_cu, int sampling, int input_
     if (out_format != HJD_OUT_BGRX && out_format != HJD_OUT_BGR24)
         return set_error(HJD_E_INVALID, "unknown output format %d", out_format);
     using K = void (*)(const void*, const int*, const FrameDev*, int, int64_t, uint8_t*);
+    const bool latency = kernel_mode == HJD_KERNEL_LATENCY ||
+                         (kernel_mode == HJD_KERNEL_AUTO && grid_blocks == 0 && tasks <= latency_max_tasks());
+    if (latency && (variant & ~3) == 0) {   // [output format][sampling index][input format]
+#define HJD_KL(V) hjd::decode_kernel_lat<0, 0, V>, hjd::decode_kernel_lat<0, 1, V>, \
+                  hjd::decode_kernel_lat<1, 0, V>, hjd::decode_kernel_lat<1, 1, V>, \
+                  hjd::decode_kernel_lat<2, 0, V>, hjd::decode_kernel_lat<2, 1, V>, \
+                  hjd::decode_kernel_lat<3, 0, V>, hjd::decode_kernel_lat<3, 1, V>
+        static const K kLat[16] = {HJD_KL(0), HJD_KL(hjd::kOutBgr24)};
+#undef HJD_KL
+        if (tasks > (int64_t(1) << 31) - 1) return set_error(HJD_E_INVALID, "too many tasks for the latency kernel");
+        const K k = kLat[(out_format == HJD_OUT_BGR24 ? 8 : 0) | (sg.index << 1) | fmt];
+        hipLaunchKernelGGL(k, dim3(static_cast<uint32_t>(tasks)), dim3(hjd::kLatThreads), 0,
+                           static_cast<hipStream_t>(stream), d_coefs, d_qt_nat,
+                           reinterpret_cast<const FrameDev*>(d_frames), nframes, tasks, static_cast<uint8_t*>(d_out));
+        HJD_HIP(hipGetLastError());
+        return HJD_OK;
+    }
     if (out_format == HJD_OUT_BGR24) {   // [sampling index][input format], default variant
         static const K kTable24[8] = {
             hjd::decode_kernel<0, 0, hjd::kOutBgr24>, hjd::decode_kernel<0, 1, hjd::kOutBgr24>,
@@ -350,6 +383,15 @@ int hjd_plan_set_variant(hjd_plan* plan, int variant)
     return HJD_OK;
 }
 
+int hjd_plan_set_kernel(hjd_plan* plan, int mode)
+{
+    if (!plan) return fail(HJD_E_INVALID, "plan is NULL");
+    if (mode != HJD_KERNEL_AUTO && mode != HJD_KERNEL_PERSISTENT && mode != HJD_KERNEL_LATENCY)
+        return fail(HJD_E_INVALID, "unknown kernel mode %d", mode);
+    plan->kernel_mode = mode;
+    return HJD_OK;
+}
+
 int64_t hjd_plan_tasks(const hjd_plan* plan) { return plan ? plan->tasks : -1; }
 int64_t hjd_plan_pixels(const hjd_plan* plan) { return plan ? plan->pixels : -1; }
 int64_t hjd_plan_coef_bytes(const hjd_plan* plan) { return plan ? plan->coef_bytes : -1; }
@@ -364,7 +406,10 @@ int64_t hjd_plan_coef_bytes(const hjd_plan* plan) { return plan ? plan->coef_byt
 // waves take ~8 tasks; 4:2:0 waves take one (4:2:2 and gray: 8, like 4:4:4).
 static int decode_grid(int sampling, int fmt, int64_t tasks)
 {
-    const int64_t per_wave = (sampling == HJD_YUV420 && fmt == 0) ? 1 : 8;
+    // ... but never fewer than ~4 waves per SIMD (256 CUs x 4 SIMDs): a single
+    // 4:4:4 frame at 8 tasks per wave would leave most of the chip idle.
+    int64_t per_wave = (sampling == HJD_YUV420 && fmt == 0) ? 1 : 8;
+    per_wave = std::max<int64_t>(1, std::min<int64_t>(per_wave, tasks / (4 * 1024)));
     const int64_t waves = (tasks + per_wave - 1) / per_wave;
     const int64_t groups = (waves + hjd::kWavesPerGroup - 1) / hjd::kWavesPerGroup;
     return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(groups, int64_t(1) << 24)));
@@ -388,7 +433,8 @@ int hjd_plan_launch(hjd_plan* plan, const void* d_coefs, void* d_out, void* stre
     return hjd_internal::launch_decode(plan->ctx->device, plan->ctx->num_cu, plan->sampling, plan->input_format,
                                        plan->variant, d_coefs, plan->d_qt,
                                        reinterpret_cast<const hjd_internal::FrameRecord*>(plan->d_frames),
-                                       plan->nframes, plan->tasks, d_out, stream, grid_blocks, plan->out_format);
+                                       plan->nframes, plan->tasks, d_out, stream, grid_blocks, plan->out_format,
+                                       plan->kernel_mode);
 }
 
 int hjd_idct_blocks(hjd_ctx* ctx, const int32_t* d_in, int32_t* d_out, int64_t nblocks, void* stream)

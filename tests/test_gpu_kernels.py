@@ -1,0 +1,83 @@
+"""GPU: the two fused kernels -- the persistent streaming kernel and the
+latency kernel (one workgroup per task) -- give the oracle's pixels on every
+sampling, input format, output format and edge geometry.  HJD_KERNEL_AUTO
+sends small launches (single frames) to the latency kernel and batches to the
+persistent one, so both are forced here explicitly."""
+import numpy as np
+import pytest
+
+import oracle_py as O
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [(1, 1), (17, 9), (129, 33), (385, 40), (1920, 1080)]
+
+
+def _run(hjd, ctx, coefs, qt, w, h, s, mode, fmt=0, out_format=0, pad=0):
+    import torch
+    pitch = hjd.default_pitch(w, out_format) + pad
+    guard = 256
+    buf = torch.full((2 * guard + pitch * h,), 0x5A, dtype=torch.uint8, device="cuda")
+    spec = hjd.FrameSpec(w, h, s, out_offset=guard, out_pitch=pitch, qt_index=(0, 1, 2), out_format=out_format)
+    plan = hjd.Plan(ctx, [spec], fmt, qtables=qt if fmt == 0 else None)
+    plan.set_kernel(mode)
+    plan.launch(torch.from_numpy(np.ascontiguousarray(coefs)).cuda(), buf)
+    torch.cuda.synchronize()
+    full = buf.cpu().numpy()
+    mask = np.ones(full.shape, bool)
+    nbytes = hjd.OUT_BYTES[out_format] * w
+    mask[guard:guard + pitch * h].reshape(h, pitch)[:, :nbytes] = False
+    assert (full[mask] == 0x5A).all(), "write outside the frame"
+    return full[guard:guard + pitch * h].reshape(h, pitch)[:, :nbytes]
+
+
+def _expect(bgrx, out_format):
+    b = np.ascontiguousarray(bgrx).view(np.uint8).reshape(bgrx.shape[0], bgrx.shape[1], 4)
+    return b.reshape(bgrx.shape[0], -1) if out_format == 0 else b[..., :3].reshape(bgrx.shape[0], -1)
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("s", [0, 1, 3, 4])
+def test_both_kernels_vs_oracle(hjd, ctx, mode, s):
+    for (w, h) in SIZES:
+        coefs, qt = O.synthetic_coefs(w, h, s, seed=w + h + s)
+        exp = O.decode_q16(coefs, qt, w, h, s)
+        for out_format in (0, 1):
+            got = _run(hjd, ctx, coefs, qt, w, h, s, mode, out_format=out_format, pad=4 * (w % 3))
+            np.testing.assert_array_equal(got, _expect(exp, out_format), err_msg=f"{w}x{h} s={s} fmt={out_format}")
+        nat = O.dequant_natural(coefs, qt, s)
+        got = _run(hjd, ctx, nat, None, w, h, s, mode, fmt=1)
+        np.testing.assert_array_equal(got, _expect(exp, 0), err_msg=f"{w}x{h} s={s} i32")
+
+
+@pytest.mark.parametrize("s", [0, 1, 3])
+def test_latency_kernel_colour_corners(hjd, ctx, s):
+    """The flagged-G path inside the latency kernel's split colour stage."""
+    from test_gpu_extensions import _corner_frame
+    w, h = 260, 50
+    nat = _corner_frame(w, h, s, seed=s + 29)
+    got = _run(hjd, ctx, nat, None, w, h, s, 2, fmt=1)
+    np.testing.assert_array_equal(got, _expect(O.decode_i32(nat, w, h, s), 0))
+
+
+def test_latency_kernel_multi_frame_plan(hjd, ctx):
+    """Several frames of different sizes and qtables in one latency launch."""
+    import torch
+    sizes = [(313, 234), (16, 16), (1920, 40), (33, 95), (1, 300)]
+    specs, coefs, qts, exps, off_blk, off_px = [], [], [], [], 0, 0
+    for i, (w, h) in enumerate(sizes):
+        c, q = O.synthetic_coefs(w, h, 1, seed=50 + i, quality_scale=0.5 + 0.3 * i)
+        specs.append(hjd.FrameSpec(w, h, 1, coef_offset=off_blk, out_offset=off_px * 4,
+                                   qt_index=(3 * i, 3 * i + 1, 3 * i + 2)))
+        coefs.append(c); qts.append(q); exps.append(O.decode_q16(c, q, w, h, 1))
+        off_blk += c.shape[0]; off_px += w * h
+    plan = hjd.Plan(ctx, specs, 0, qtables=np.concatenate(qts))
+    plan.set_kernel(hjd.KERNEL_LATENCY)
+    out = torch.zeros(off_px, dtype=torch.int32, device="cuda")
+    plan.launch(torch.from_numpy(np.concatenate(coefs)).cuda(), out)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint32)
+    pos = 0
+    for (w, h), e in zip(sizes, exps):
+        np.testing.assert_array_equal(got[pos:pos + w * h].reshape(h, w), e)
+        pos += w * h

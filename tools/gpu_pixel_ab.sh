@@ -11,9 +11,15 @@ mkdir -p $O
 cd $R
 for i in $(seq 1 $N); do
   for V in default "$@"; do
-    if [ "$V" = default ]; then LIBV=""; else LIBV=$R/build/variants/$V/libhjd.so; fi
+    # a variant is either build/variants/<name>/libhjd.so (same Python package)
+    # or a snapshot build/variants/<name>/{bench.py,ocljpegdecoder_amd/} of an
+    # older tree, run with its own bench and package
+    B=bench.py; LIBV=""
+    if [ "$V" != default ]; then
+      if [ -f $R/build/variants/$V/bench.py ]; then B=$R/build/variants/$V/bench.py; else LIBV=$R/build/variants/$V/libhjd.so; fi
+    fi
     for wl in 4k444 4k420; do
-      HJD_LIB=$LIBV timeout -k 10 300 python bench.py --workload $wl --no-cpu > $O/${V}_${wl}_$i.json 2> $O/${V}_${wl}_$i.err || { echo BENCH FAILED $V $wl; tail $O/${V}_${wl}_$i.err; exit 1; }
+      HJD_LIB=$LIBV timeout -k 10 300 python $B --workload $wl --no-cpu > $O/${V}_${wl}_$i.json 2> $O/${V}_${wl}_$i.err || { echo BENCH FAILED $V $wl; tail $O/${V}_${wl}_$i.err; exit 1; }
       python3 -c "import json; d=json.load(open('$O/${V}_${wl}_$i.json')); print('$V', '$wl', $i, d['value'], d['roofline']['frac'])"
     done
   done
