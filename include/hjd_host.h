@@ -72,6 +72,9 @@ int hjd_stream_submit(hjd_stream* s, const uint8_t* data, size_t size, void* d_o
 /* Wait for every submitted image; returns the first error, if any.  stats (may
  * be NULL) receives {images, pixels, host_decode_ns, h2d_bytes, kernel_launches}. */
 int hjd_stream_sync(hjd_stream* s, int64_t stats[5]);
+/* Pixel format of subsequent submits: HJD_OUT_BGRX (default) or HJD_OUT_BGR24
+ * (d_out 4-byte aligned, pitch >= 3*width); jobs already queued keep theirs. */
+int hjd_stream_set_output_format(hjd_stream* s, int out_format);
 
 /* ---- GPU entropy decoding ----------------------
  * Replaces the single-threaded scan decode of the reference

@@ -46,6 +46,7 @@ struct Job {
     size_t size;
     void* d_out;
     int32_t pitch;
+    int out_format;   // HJD_OUT_* at submit time
 };
 
 }  // namespace
@@ -70,6 +71,7 @@ struct hjd_stream {
     std::vector<std::thread> workers;
 
     std::atomic<int64_t> images{0}, pixels{0}, decode_ns{0}, h2d_bytes{0}, launches{0};
+    std::atomic<int> out_format{HJD_OUT_BGRX};   // for subsequent submits
     int first_error = HJD_OK;
     std::string first_error_msg;
 
@@ -102,7 +104,8 @@ int hjd_stream::run_job(const Job& job)
     const auto t0 = std::chrono::steady_clock::now();
     int rc = hjd_jpeg_decode_coefs(job.data, job.size, &info, reinterpret_cast<int16_t*>(h + kHeader), max_blocks);
     decode_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
-    if (rc == HJD_OK && job.pitch < 4 * info.width) rc = set_error(HJD_E_INVALID, "output pitch too small");
+    if (rc == HJD_OK && job.pitch < hjd_internal::out_format_bytes(job.out_format) * info.width)
+        rc = set_error(HJD_E_INVALID, "output pitch too small");
 
     const size_t coef_bytes = rc == HJD_OK ? static_cast<size_t>(info.nblocks) * 128 : 0;
     int64_t tasks = 0;
@@ -110,7 +113,7 @@ int hjd_stream::run_job(const Job& job)
         FrameRecord rec;
         const int qti[3] = {0, 1, 2};
         tasks = hjd_internal::make_frame_record(info.width, info.height, info.sampling, 0,
-                                                0, job.pitch, qti, &rec);
+                                                0, job.pitch, qti, &rec, job.out_format);
         if (tasks < 0) rc = static_cast<int>(tasks);
         memcpy(h, &rec, sizeof(rec));
         int32_t* qn = reinterpret_cast<int32_t*>(h + kQtOffset);
@@ -130,7 +133,7 @@ int hjd_stream::run_job(const Job& job)
         lrc = hjd_internal::launch_decode(device, num_cu, info.sampling, HJD_IN_Q16_ZIGZAG, 0, dev[s] + kHeader,
                                           reinterpret_cast<const int32_t*>(dev[s] + kQtOffset),
                                           reinterpret_cast<const FrameRecord*>(dev[s]), 1, tasks, job.d_out,
-                                          compute, 0);
+                                          compute, 0, job.out_format);
         launches++;
     }
     if (e == hipSuccess) e = hipEventRecord(kernel_done[s], compute);
@@ -249,13 +252,23 @@ int hjd_stream_destroy(hjd_stream* st)
 
 int hjd_stream_submit(hjd_stream* st, const uint8_t* data, size_t size, void* d_out, int32_t out_pitch)
 {
-    if (!st || !data || !d_out || out_pitch <= 0 || (out_pitch & 3) || (reinterpret_cast<uintptr_t>(d_out) & 15))
-        return set_error(HJD_E_INVALID, "invalid submit arguments (d_out must be 16-byte aligned)");
+    const int fmt = st ? st->out_format.load() : HJD_OUT_BGRX;
+    const uintptr_t amask = fmt == HJD_OUT_BGR24 ? 3 : 15;
+    if (!st || !data || !d_out || out_pitch <= 0 || (out_pitch & 3) || (reinterpret_cast<uintptr_t>(d_out) & amask))
+        return set_error(HJD_E_INVALID, "invalid submit arguments (d_out must be 16-byte (BGR24: 4-byte) aligned)");
     {
         std::lock_guard<std::mutex> g(st->mu);
-        st->queue.push_back(Job{st->submitted++, data, size, d_out, out_pitch});
+        st->queue.push_back(Job{st->submitted++, data, size, d_out, out_pitch, fmt});
     }
     st->cv_jobs.notify_one();
+    return HJD_OK;
+}
+
+int hjd_stream_set_output_format(hjd_stream* st, int out_format)
+{
+    if (!st) return set_error(HJD_E_INVALID, "stream is NULL");
+    if (!hjd_internal::out_format_bytes(out_format)) return set_error(HJD_E_INVALID, "unknown output format %d", out_format);
+    st->out_format = out_format;   // each job keeps the format it was submitted with
     return HJD_OK;
 }
 

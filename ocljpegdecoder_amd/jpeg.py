@@ -109,7 +109,7 @@ def decode_jpeg(ctx, data: bytes, stream=None, out_format: int = 0):
 class JpegStream:
     """hjd_stream: host Huffman workers -> pinned slots -> H2D -> fused kernel."""
 
-    def __init__(self, ctx, max_blocks: int, nslots: int = 4, nthreads: int = 0):
+    def __init__(self, ctx, max_blocks: int, nslots: int = 4, nthreads: int = 0, out_format: int = 0):
         self.lib = _lib.load()
         self.ctx = ctx
         h = ctypes.c_void_p()
@@ -117,6 +117,12 @@ class JpegStream:
               "hjd_stream_create")
         self.handle = h
         self._keep = []   # bytes must stay alive until sync
+        if out_format:
+            self.set_output_format(out_format)
+
+    def set_output_format(self, out_format: int):
+        """OUT_BGRX or OUT_BGR24 for subsequent submits."""
+        check(self.lib.hjd_stream_set_output_format(self.handle, int(out_format)), "hjd_stream_set_output_format")
 
     def submit(self, data: bytes, out, out_pitch: Optional[int] = None):
         buf = _buf(data) if not isinstance(data, ctypes.Array) else data

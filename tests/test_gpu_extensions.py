@@ -240,3 +240,19 @@ def test_bgr24_jpeg_paths_and_d2h_sink(hjd, ctx):
     for k, (e, i) in enumerate(zip(exps, infos)):
         got = (dev_outs[k].cpu() if k % 2 else host_outs[k]).numpy()
         np.testing.assert_array_equal(got[:, :3 * i.width], _bgr24(e), err_msg=f"frame {k}")
+
+
+def test_bgr24_host_huffman_stream(hjd, ctx):
+    """hjd_stream (host Huffman || H2D || kernel) in BGR24, golden + extension files."""
+    import os
+    import torch
+    datas = [open(os.path.join(O.GOLDEN, n + ".jpg"), "rb").read() for n in O.golden_cases()] + _jpegs()
+    exps, infos = zip(*[_expected(hjd, d) for d in datas])
+    outs = [torch.full((i.height, hjd.default_pitch(i.width, hjd.OUT_BGR24)), 0xA5, dtype=torch.uint8, device="cuda")
+            for i in infos]
+    with hjd.JpegStream(ctx, max(i.nblocks for i in infos), nslots=3, nthreads=2, out_format=hjd.OUT_BGR24) as st:
+        for d, o in zip(datas, outs):
+            st.submit(d, o)
+        st.sync()
+    for o, e, i in zip(outs, exps, infos):
+        np.testing.assert_array_equal(o.cpu().numpy()[:, :3 * i.width], _bgr24(e))
