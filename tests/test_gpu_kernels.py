@@ -81,3 +81,32 @@ def test_latency_kernel_multi_frame_plan(hjd, ctx):
     for (w, h), e in zip(sizes, exps):
         np.testing.assert_array_equal(got[pos:pos + w * h].reshape(h, w), e)
         pos += w * h
+
+
+def _q16_frame(w, h, s, seed):
+    """16-bit-table frame: factors 256-1200, DC and one AC coefficient in
+    {-1, 0, 1}; returns (coefs, qt, max |float IDCT output|)."""
+    rng = np.random.default_rng(seed)
+    nblk = O.frame_blocks(w, h, s)
+    qt = rng.integers(256, 1201, (3, 64)).astype(np.int32)
+    coefs = np.zeros((nblk, 64), np.int16)
+    coefs[:, 0] = rng.integers(-1, 2, nblk)
+    coefs[np.arange(nblk), rng.integers(1, 64, nblk)] = rng.integers(-1, 2, nblk)
+    nat = O.dequant_natural(coefs, qt, s).astype(np.float64).reshape(-1, 8, 8)
+    k = np.arange(8)
+    c = np.where(k == 0, 1 / np.sqrt(2), 1.0)
+    m = np.cos((2 * k[None, :] + 1) * k[:, None] * np.pi / 16) * c[:, None] / 2
+    return coefs, qt, float(np.abs(np.einsum("ux,nuv,vy->nxy", m, nat, m)).max())
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("s", [0, 1, 3, 4])
+def test_16bit_quantisation_tables(hjd, ctx, mode, s):
+    """DQT precision 1 (16-bit entries, T.81 B.2.4.1): factors above 255
+    through the 24-bit dequant multiply of both kernels, on blocks inside the
+    reference's legal domain (column outputs within its iclp[-512, 511])."""
+    w, h = 300, 70
+    coefs, qt, peak = _q16_frame(w, h, s, seed=4000 + s)
+    assert peak < 480, peak   # premise: legal domain, with margin for the integer IDCT's rounding
+    got = _run(hjd, ctx, coefs, qt, w, h, s, mode)
+    np.testing.assert_array_equal(got, _expect(O.decode_q16(coefs, qt, w, h, s), 0))

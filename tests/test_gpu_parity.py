@@ -169,13 +169,21 @@ def test_4k_frame_vs_oracle(hjd, ctx):
     np.testing.assert_array_equal(px, O.decode_q16(coefs, qt, w, h, s))
 
 
-def test_extreme_legal_blocks(hjd, ctx):
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("s", [0, 1])
+def test_extreme_legal_blocks(hjd, ctx, mode, s):
     """Clamp-edge blocks (DC +-2100, q=1 extremes, checkerboards) through the
-    fused path: every block of an MCU is one of the IDCT known-answer vectors."""
+    fused path, both kernels (1 persistent, 2 latency): every block of every
+    MCU is one of the IDCT known-answer vectors."""
+    import torch
     z = np.load(O.GOLDEN + "/idct_vectors.npz")
-    nat = z["inp"]
-    n = (nat.shape[0] // 6) * 6
-    nat = nat[:n]
-    w = 16 * (n // 6)
-    px, _ = _decode(hjd, ctx, nat, None, w, 16, 1, fmt=1)
-    np.testing.assert_array_equal(px, O.decode_i32(nat, w, 16, 1))
+    bpm, mw = (6, 16) if s == 1 else (3, 8)
+    n = (z["inp"].shape[0] // bpm) * bpm
+    nat = np.ascontiguousarray(z["inp"][:n])
+    w, h = mw * (n // bpm), mw
+    plan = hjd.Plan(ctx, [hjd.FrameSpec(w, h, s, qt_index=(0, 1, 2))], 1)
+    plan.set_kernel(mode)
+    out = torch.full((h, w), -1, dtype=torch.int32, device="cuda")
+    plan.launch(torch.from_numpy(nat).cuda(), out)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(to_u32(out), O.decode_i32(nat, w, h, s))
