@@ -182,15 +182,18 @@ def _cpu_model():
     return "unknown"
 
 
-def committed_traffic(workload):
-    """Per-launch HBM bytes from the committed PMC summary for this workload."""
+def committed_traffic(workload, frames):
+    """Per-launch HBM bytes from the committed PMC summary for this workload,
+    if it was profiled at this launch size (else None: the bytes of another
+    launch size would not describe this one)."""
     best = None
     for p in sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json"))):
         try:
             d = json.load(open(p))
         except Exception:
             continue
-        if d.get("workload") == workload and d.get("hbm_bytes_per_launch"):
+        if (d.get("workload") == workload and d.get("hbm_bytes_per_launch") and
+                d.get("frames_per_launch") == frames):
             best = (d["hbm_bytes_per_launch"], os.path.relpath(p, REPO))
     return best
 
@@ -430,7 +433,7 @@ def main():
             pool_host = coefs[:npool].cpu().numpy()
             log("running CPU baseline leg ...")
             cpu = cpu_baseline(pool_host, qt, wl, value)
-        traffic = committed_traffic(args.workload)
+        traffic = committed_traffic(args.workload, nf)
         res = {
             "metric": "Mpixels/s decoded (dequant+IDCT+colour) at 1/2/4/8 GPUs; % HBM roofline",
             "value": round(value, 1),

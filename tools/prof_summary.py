@@ -36,8 +36,10 @@ def main():
     ap.add_argument("--workload", default="4k420")
     ap.add_argument("--kernel", default="decode_kernel")
     ap.add_argument("--note", default="")
+    ap.add_argument("--frames", type=int, default=1024, help="frames per launch of the profiled command (bench.py)")
     args = ap.parse_args()
     out = {"name": args.name, "workload": args.workload, "kernel_match": args.kernel, "note": args.note,
+           "frames_per_launch": args.frames,
            "source_dir": os.path.relpath(args.dir, REPO)}
 
     stats = sorted(glob.glob(os.path.join(args.dir, "**", "*kernel_stats.csv"), recursive=True))
