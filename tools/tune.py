@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--variants", default="0,1")
     ap.add_argument("--grids", default="0")
+    ap.add_argument("--kernels", default="1", help="hjd_kernel_mode list: 1 persistent, 2 latency")
     ap.add_argument("--no-check", action="store_true", help="ablation variants: outputs differ by design")
     args = ap.parse_args()
 
@@ -52,29 +53,31 @@ def main():
     nbytes = plan.coef_bytes + 4 * plan.pixels
     variants = [int(v) for v in args.variants.split(",")]
     grids = [int(g) for g in args.grids.split(",")]
+    kernels = [int(k) for k in args.kernels.split(",")]
     stream = torch.cuda.current_stream()
-    times = {(v, g): [] for v in variants for g in grids}
+    times = {(k, v, g): [] for k in kernels for v in variants for g in grids}
     ref = None
     for rnd in range(args.rounds):
-        for v in variants:
-            for g in grids:
-                plan.set_variant(v)
-                plan.launch(coefs, out, stream, grid_blocks=g)   # warm
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(stream)
-                for _ in range(args.reps):
-                    plan.launch(coefs, out, stream, grid_blocks=g)
-                e1.record(stream)
-                torch.cuda.synchronize()
-                times[(v, g)].append(e0.elapsed_time(e1) / args.reps)
-                if rnd == 0 and not args.no_check:
-                    sig = int(out[:, ::97, ::89].sum().item())
-                    ref = sig if ref is None else ref
-                    assert sig == ref, f"variant {v} grid {g} output differs"
+        for k, v, g in times:
+            plan.set_kernel(k)
+            plan.set_variant(v)
+            plan.launch(coefs, out, stream, grid_blocks=g)   # warm
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(args.reps):
+                plan.launch(coefs, out, stream, grid_blocks=g)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            times[(k, v, g)].append(e0.elapsed_time(e1) / args.reps)
+            if rnd == 0 and not args.no_check:
+                sig = int(out[:, ::97, ::89].sum().item())
+                ref = sig if ref is None else ref
+                assert sig == ref, f"kernel {k} variant {v} grid {g} output differs"
     res = {"workload": args.workload, "frames": nf, "bytes_per_launch": nbytes, "results": []}
-    for (v, g), ts in times.items():
+    for (k, v, g), ts in times.items():
         med = statistics.median(ts)
-        res["results"].append({"variant": v, "grid": g, "median_ms": round(med, 4), "min_ms": round(min(ts), 4),
+        res["results"].append({"kernel": k, "variant": v, "grid": g, "median_ms": round(med, 4),
+                               "min_ms": round(min(ts), 4),
                                "GBps_median": round(nbytes / med / 1e6, 1),
                                "GBps_best": round(nbytes / min(ts) / 1e6, 1)})
     print(json.dumps(res))
