@@ -99,6 +99,79 @@ __host__ __device__ __forceinline__ void idct8(int (&v)[8])
     }
 }
 
+// ---- row pass on packed int16 pairs (the pixel kernel's hot form) -----------
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+
+// v_dot2_i32_i16: a.x*b.x + a.y*b.y + c (no clamp; 32-bit wrap like C int
+// math).  b is an SGPR constant pair (const_pair).  Written as asm: the
+// compiler otherwise selects the accumulate-in-place v_dot2c form and seeds
+// each accumulator with a v_mov.
+template <int kC>
+__host__ __device__ __forceinline__ int sdot2(s16x2 a, s16x2 b)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    int r;
+    if constexpr (kC == 0) {
+        asm("v_dot2_i32_i16 %0, %1, %2, 0" : "=v"(r) : "v"(a), "s"(b));
+    } else {
+        asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(b), "v"(kC));
+    }
+    return r;
+#else
+    return static_cast<int>(a.x) * b.x + static_cast<int>(a.y) * b.y + kC;
+#endif
+}
+
+// Dequantised row coefficients as int16 pairs (v0,v4), (v1,v7), (v3,v5), (v2,v6):
+// the operand pairs of the row pass's rotations.
+struct RowPk {
+    s16x2 p04, p17, p35, p26;
+};
+
+// The row pass of src/cpuIDCT8x8.cpp:36-80 (idctrow) on packed pairs.  Every
+// stage-1/2 value of the reference's row pass is an exact sum of two products
+// (it has no intermediate shifts), e.g. x4 = W7*(x4+x5) + (W1-W7)*x4 =
+// W1*b1 + W7*b7, so each is one v_dot2_i32_i16 of a coefficient pair with a
+// constant pair -- the same integers as idct8<false>.  On the legal domain the
+// dequantised coefficients are int16 (Parseval: |coef| <= ||coef||_2 <= ~4.1e3,
+// see mul24) and no sum overflows int32.
+// A constant int16 pair held in an SGPR: the dot2 products then issue as one
+// VOP3P v_dot2_i32_i16 (SGPR constant, inline 0 accumulator) instead of the
+// literal-operand v_dot2c form, which needs a v_mov to seed its accumulator.
+__host__ __device__ __forceinline__ s16x2 const_pair(int lo, int hi)
+{
+    uint32_t k = (static_cast<uint32_t>(lo) & 0xffffu) | (static_cast<uint32_t>(hi) << 16);
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm("" : "+s"(k));
+#endif
+    return __builtin_bit_cast(s16x2, k);
+}
+
+__host__ __device__ __forceinline__ void idct8_row_pk(const RowPk& p, int (&v)[8])
+{
+    const s16x2 k0p = const_pair(2048, 2048), k0m = const_pair(2048, -2048);
+    const s16x2 k4 = const_pair(kC1, kC7), k5 = const_pair(kC7, -kC1);
+    const s16x2 k6 = const_pair(kC3, kC5), k7 = const_pair(-kC5, kC3);
+    const s16x2 k3 = const_pair(kC2, kC6), k2 = const_pair(kC6, -kC2);
+    const int e8 = sdot2<128>(p.p04, k0p);   // (b0 << 11) + 128 + (b4 << 11)
+    const int e0 = sdot2<128>(p.p04, k0m);   // (b0 << 11) + 128 - (b4 << 11)
+    const int o4 = sdot2<0>(p.p17, k4);
+    const int o5 = sdot2<0>(p.p17, k5);
+    const int o6 = sdot2<0>(p.p35, k6);
+    const int o7 = sdot2<0>(p.p35, k7);
+    const int e3 = sdot2<0>(p.p26, k3);
+    const int e2 = sdot2<0>(p.p26, k2);
+
+    const int a1 = o4 + o6, a4 = o4 - o6;
+    const int a6 = o5 + o7, a5 = o5 - o7;
+    const int f7 = e8 + e3, f8 = e8 - e3;
+    const int f3 = e0 + e2, f0 = e0 - e2;
+    const int g2 = (mul181(a4 + a5) + 128) >> 8;
+    const int g4 = (mul181(a4 - a5) + 128) >> 8;
+    v[0] = (f7 + a1) >> 8; v[1] = (f3 + g2) >> 8; v[2] = (f0 + g4) >> 8; v[3] = (f8 + a6) >> 8;
+    v[4] = (f8 - a6) >> 8; v[5] = (f0 - g4) >> 8; v[6] = (f3 - g2) >> 8; v[7] = (f7 - a1) >> 8;
+}
+
 // ---------------------------------------------------------------------------
 // Colour conversion.  Reference (src/decoder.cpp:367-370 + src/macro.h:121-145):
 //   R = (int)(Y + 1.402*V + 128), G = (int)(Y - 0.34414*U - 0.71414*V + 128),
@@ -194,7 +267,6 @@ __device__ __forceinline__ ChromaTerms chroma_terms(uint32_t uw, uint32_t vw)
 __device__ __forceinline__ bool g_flagged(const ChromaTerms& t) { return static_cast<uint16_t>(t.g) == 0xffffu; }
 
 // ---- packed (2 x int16 per VGPR) pixel math ---------------------------------
-typedef short s16x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ uint32_t pk_add16(uint32_t a, uint32_t b)
 {

@@ -438,36 +438,61 @@ __device__ __forceinline__ bool round_is_luma(int i)
     return kSampling == 1 ? i < 4 : kSampling == 0 ? i % 3 == 0 : kSampling == 2 ? i < 3 : true;
 }
 
-// One round's row-pass inputs.  kFmt 0: int16 zigzag staged in the LDS slots
-// (dequant fused); kFmt 1: int32 natural rows read straight from global memory.
-template <int kSampling, int kFmt>
-__device__ __forceinline__ void load_round(const char* __restrict__ slots, int lane, int i, const int (&zoff)[8],
-                                           const uint32_t (&q)[3][4], const int* __restrict__ src32, int nblk,
-                                           int (&v)[8])
+// One round's row-pass inputs, kFmt 0: int16 zigzag coefficients staged in
+// the LDS slots, gathered as the row pass's operand pairs and dequantised two
+// at a time (v_pk_mul_lo_u16: the low 16 bits of the product, which is the
+// reference's int on the legal domain, where dequantised coefficients fit
+// int16 -- idct8_row_pk).  q[c][k]: this lane's row of component c's table as
+// the pairs (q0,q4), (q1,q7), (q3,q5), (q2,q6) (load_qrow_pk).
+template <int kSampling>
+__device__ __forceinline__ RowPk load_round_pk(const char* __restrict__ slots, int lane, int i, const int (&zoff)[8],
+                                               const uint32_t (&q)[3][4])
+{
+    const int g = lane >> 3;
+    const int b = round_block<kSampling>(i, g);
+    const int comp = round_component<kSampling>(i);
+    const char* blk = slots + b * kSlotBytes;
+    auto pair = [&](int ca, int cb, int k) {
+        const s16x2 c = {*reinterpret_cast<const short*>(blk + zoff[ca]),
+                         *reinterpret_cast<const short*>(blk + zoff[cb])};
+        // a mixed round (4:2:2 round 4) selects the table per lane
+        const uint32_t qq = comp >= 0 ? q[comp < 0 ? 0 : comp][k] : (g < 4 ? q[1][k] : q[2][k]);
+        return c * __builtin_bit_cast(s16x2, qq);   // dequant (src/decoder.cpp:340)
+    };
+    RowPk p;
+    p.p04 = pair(0, 4, 0);
+    p.p17 = pair(1, 7, 1);
+    p.p35 = pair(3, 5, 2);
+    p.p26 = pair(2, 6, 3);
+    return p;
+}
+
+// One round's row-pass inputs, kFmt 1: int32 natural rows (already
+// dequantised: the idct.h format) read straight from global memory.
+template <int kSampling>
+__device__ __forceinline__ void load_round_i32(int lane, int i, const int* __restrict__ src32, int nblk, int (&v)[8])
 {
     const int g = lane >> 3, r = lane & 7;
     const int b = round_block<kSampling>(i, g);
-    const int comp = round_component<kSampling>(i);
-    if constexpr (kFmt == 0) {
-        const char* blk = slots + b * kSlotBytes;
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            const int coef = *reinterpret_cast<const short*>(blk + zoff[c]);
-            // two 16-bit factors per VGPR; a mixed round selects per lane
-            const uint32_t qq = comp >= 0 ? q[comp < 0 ? 0 : comp][c >> 1] : (g < 4 ? q[1][c >> 1] : q[2][c >> 1]);
-            const int qc = (c & 1) ? static_cast<int>(qq >> 16) : static_cast<int>(qq & 0xffffu);
-            v[c] = mul24(coef, qc);   // dequant (src/decoder.cpp:340)
-        }
-    } else {
-        int4 lo = make_int4(0, 0, 0, 0), hi = lo;
-        if (b < nblk) {   // lanes past the strip's last block compute on zeros
-            const int4* p = reinterpret_cast<const int4*>(src32 + b * 64 + r * 8);
-            lo = p[0];
-            hi = p[1];
-        }
-        v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
-        v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+    int4 lo = make_int4(0, 0, 0, 0), hi = lo;
+    if (b < nblk) {   // lanes past the strip's last block compute on zeros
+        const int4* p = reinterpret_cast<const int4*>(src32 + b * 64 + r * 8);
+        lo = p[0];
+        hi = p[1];
     }
+    v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
+    v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+}
+
+// Row r of the natural-order table qt_pool[t*64 ..] as the load_round_pk pairs.
+__device__ __forceinline__ void load_qrow_pk(const int* __restrict__ qt_pool, int t, int r, uint32_t (&q)[4])
+{
+    const int4* qp = reinterpret_cast<const int4*>(qt_pool + t * 64 + r * 8);
+    const int4 a = qp[0], b = qp[1];   // DQT entries are <= 65535
+    q[0] = (a.x & 0xffff) | (b.x << 16);   // q0, q4
+    q[1] = (a.y & 0xffff) | (b.w << 16);   // q1, q7
+    q[2] = (a.w & 0xffff) | (b.y << 16);   // q3, q5
+    q[3] = (a.z & 0xffff) | (b.z << 16);   // q2, q6
 }
 
 // IDCT of the task's 48 blocks (6 rounds).  kFmt 0: int16 zigzag staged in the
@@ -481,12 +506,19 @@ __device__ __forceinline__ void idct_stage(char* __restrict__ slots, char* __res
                                            const int* __restrict__ src32, int nblk)
 {
     const int g = lane >> 3, r = lane & 7;
+    RowPk pk;
     int v[8];
-    load_round<kSampling, kFmt>(slots, lane, 0, zoff, q, src32, nblk, v);
+    if constexpr (kFmt == 0)
+        pk = load_round_pk<kSampling>(slots, lane, 0, zoff, q);
+    else
+        load_round_i32<kSampling>(lane, 0, src32, nblk, v);
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
         const int b = round_block<kSampling>(i, g);
-        idct8<false>(v);
+        if constexpr (kFmt == 0)
+            idct8_row_pk(pk, v);
+        else
+            idct8<false>(v);
         {
             int4* dst = reinterpret_cast<int4*>(rowbuf + g * kRowBufBlock + r * kRowStride);
             dst[0] = make_int4(v[0], v[1], v[2], v[3]);
@@ -499,7 +531,12 @@ __device__ __forceinline__ void idct_stage(char* __restrict__ slots, char* __res
 #pragma unroll
             for (int k = 0; k < 8; ++k) c8[k] = *reinterpret_cast<const int*>(col + k * kRowStride);
         }
-        if (i + 1 < 6) load_round<kSampling, kFmt>(slots, lane, i + 1, zoff, q, src32, nblk, v);
+        if (i + 1 < 6) {
+            if constexpr (kFmt == 0)
+                pk = load_round_pk<kSampling>(slots, lane, i + 1, zoff, q);
+            else
+                load_round_i32<kSampling>(lane, i + 1, src32, nblk, v);
+        }
         if (round_component<kSampling>(i) == 0)
             idct8<true, kLumaLevel>(c8);   // luma leaves the IDCT level-shifted (Ys = Y + 128)
         else
@@ -590,14 +627,7 @@ __global__ __launch_bounds__(kGroupThreads, 4) void decode_kernel(const void* __
             if (cc.qt0 != q_tables[0] || cc.qt1 != q_tables[1] || cc.qt2 != q_tables[2]) {
                 q_tables[0] = cc.qt0; q_tables[1] = cc.qt1; q_tables[2] = cc.qt2;
 #pragma unroll
-                for (int c = 0; c < 3; ++c) {
-                    const int4* qp = reinterpret_cast<const int4*>(qt_pool + q_tables[c] * 64 + r * 8);
-                    const int4 a = qp[0], b = qp[1];   // DQT entries are <= 65535
-                    q[c][0] = (a.x & 0xffff) | (a.y << 16);
-                    q[c][1] = (a.z & 0xffff) | (a.w << 16);
-                    q[c][2] = (b.x & 0xffff) | (b.y << 16);
-                    q[c][3] = (b.z & 0xffff) | (b.w << 16);
-                }
+                for (int c = 0; c < 3; ++c) load_qrow_pk(qt_pool, q_tables[c], r, q[c]);
             }
 #pragma unroll
             for (int k = 0; k < 6; ++k) {

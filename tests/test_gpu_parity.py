@@ -187,3 +187,26 @@ def test_extreme_legal_blocks(hjd, ctx, mode, s):
     plan.launch(torch.from_numpy(nat).cuda(), out)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(to_u32(out), O.decode_i32(nat, w, h, s))
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("s", [0, 1])
+def test_extreme_legal_blocks_q16(hjd, ctx, mode, s):
+    """The same clamp-edge blocks in the hot int16 zigzag format (all-ones
+    qtables), so the largest legal dequantised values go through the packed
+    row pass (v_pk_mul_lo_u16 dequant + v_dot2_i32_i16 rotations)."""
+    import torch
+    z = np.load(O.GOLDEN + "/idct_vectors.npz")
+    bpm, mw = (6, 16) if s == 1 else (3, 8)
+    n = (z["inp"].shape[0] // bpm) * bpm
+    nat = np.ascontiguousarray(z["inp"][:n])
+    assert np.abs(nat).max() < 32768
+    coefs = np.ascontiguousarray(nat[:, O.ZIGZAG].astype(np.int16))   # natural -> zigzag, q = 1
+    qt = np.ones((3, 64), np.int32)
+    w, h = mw * (n // bpm), mw
+    plan = hjd.Plan(ctx, [hjd.FrameSpec(w, h, s, qt_index=(0, 1, 2))], 0, qtables=qt)
+    plan.set_kernel(mode)
+    out = torch.full((h, w), -1, dtype=torch.int32, device="cuda")
+    plan.launch(torch.from_numpy(coefs).cuda(), out)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(to_u32(out), O.decode_i32(nat, w, h, s))

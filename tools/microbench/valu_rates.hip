@@ -32,6 +32,14 @@ __global__ __launch_bounds__(256) void probe(uint32_t* out, uint32_t seed)
             if constexpr (OP == 11) asm volatile("v_cvt_flr_i32_f32 %0, %0" : "+v"(x));
             if constexpr (OP == 12) asm volatile("v_lshl_add_u32 %0, %0, 2, %1" : "+v"(x) : "v"(k));
             if constexpr (OP == 13) asm volatile("v_add3_u32 %0, %0, %1, %1" : "+v"(x) : "v"(k));
+            if constexpr (OP == 14) asm volatile("v_dot2_i32_i16 %0, %0, %1, %1" : "+v"(x) : "v"(k));
+            if constexpr (OP == 15) asm volatile("v_pk_mul_lo_u16 %0, %0, %1" : "+v"(x) : "v"(k));
+            if constexpr (OP == 16) asm volatile("v_pk_mad_i16 %0, %0, %1, %1" : "+v"(x) : "v"(k));
+            if constexpr (OP == 17) asm volatile("v_alignbit_b32 %0, %0, %1, %0" : "+v"(x) : "v"(k));
+            if constexpr (OP == 18) asm volatile("v_bfe_u32 %0, %0, %1, 5" : "+v"(x) : "v"(k));
+            if constexpr (OP == 19) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(x) : "v"(k));
+            if constexpr (OP == 20) asm volatile("v_mov_b32 %0, %1" : "+v"(x) : "v"(k + x));
+            if constexpr (OP == 21) asm volatile("v_lshlrev_b64 %0, 3, %0" : "+v"(*reinterpret_cast<uint64_t*>(&a[i & ~1])));
             a[i] = x;
         }
     }
@@ -79,5 +87,12 @@ int main()
     run<11>(out, blocks, "v_cvt_flr_i32_f32");
     run<12>(out, blocks, "v_lshl_add_u32");
     run<13>(out, blocks, "v_add3_u32");
+    run<14>(out, blocks, "v_dot2_i32_i16");
+    run<15>(out, blocks, "v_pk_mul_lo_u16");
+    run<16>(out, blocks, "v_pk_mad_i16");
+    run<17>(out, blocks, "v_alignbit_b32");
+    run<18>(out, blocks, "v_bfe_u32");
+    run<19>(out, blocks, "v_cndmask_b32");
+    run<21>(out, blocks, "v_lshlrev_b64");
     return 0;
 }
