@@ -57,8 +57,9 @@ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 // Host preparation
 // ---------------------------------------------------------------------------
 
-// Canonical Huffman code (T.81 C.2 / F.2.2.3) -> first-level LUT + MAXCODE.
-int build_lut(HuffLut& t, const uint8_t counts[16], const uint8_t* syms, int nsym)
+// Canonical Huffman code (T.81 C.2 / F.2.2.3) -> first-level LUT of unit
+// entries + MAXCODE.  dc: the table's class (T.81 B.2.4.2 Tc = 0).
+int build_lut(HuffLut& t, const uint8_t counts[16], const uint8_t* syms, int nsym, bool dc)
 {
     memset(&t, 0, sizeof(t));
     int code = 0, k = 0;
@@ -71,7 +72,7 @@ int build_lut(HuffLut& t, const uint8_t counts[16], const uint8_t* syms, int nsy
             if (len <= kLutBits) {
                 const int shift = kLutBits - len;
                 for (int r = 0; r < (1 << shift); ++r)
-                    t.lut[(code << shift) | r] = static_cast<uint16_t>((len << 8) | syms[k]);
+                    t.lut[(code << shift) | r] = static_cast<uint16_t>(unit_entry(len, syms[k], dc));
             }
         }
         t.maxcode[len] = n ? code - 1 : -1;
@@ -172,7 +173,8 @@ int prepare(const uint8_t* data, size_t size, uint8_t* dst, size_t cap, Prepared
             if (s < 0) {
                 if (pf.ntab >= kMaxTables) return set_error(HJD_E_INVALID, "too many Huffman tables");
                 s = pf.ntab++;
-                if (build_lut(pf.tabs[s], h.counts[cls][ids[cls]], h.symbols[cls][ids[cls]], h.nsym[cls][ids[cls]]))
+                if (build_lut(pf.tabs[s], h.counts[cls][ids[cls]], h.symbols[cls][ids[cls]], h.nsym[cls][ids[cls]],
+                              cls == 0))
                     return set_error(HJD_E_INVALID, "invalid Huffman table");
             }
             slot[cls] = s;
@@ -247,19 +249,25 @@ struct EntBatchDev {
     uint32_t nframes, nwg, sub_bits, ntab_max;   // ntab_max: tables of the largest frame (dynamic LDS)
 };
 
-__host__ __device__ __forceinline__ RunCtx make_ctx(const EntBatchDev& b, const EntFrame& F, const HuffLut* tabs)
+// `blocks`: the frame's block_info() records (fill_blocks), LDS on the device.
+__host__ __device__ __forceinline__ RunCtx make_ctx(const EntBatchDev& b, const EntFrame& F, const HuffLut* tabs,
+                                                    const BlockInfo* blocks)
 {
     RunCtx c;
     c.data = b.data + F.data_off;
     c.seg_end = b.seg_end + F.seg_base;
     c.tabs = tabs;
+    c.blocks = blocks;
     c.nseg = F.nseg;
     c.data_bits = F.data_bits;
     c.bpm = F.bpm;
-    c.jinfo_q = F.jinfo[0] | (static_cast<uint64_t>(F.jinfo[1]) << 16) | (static_cast<uint64_t>(F.jinfo[2]) << 32) |
-                (static_cast<uint64_t>(F.jinfo[3]) << 48);
-    c.jinfo_hi = F.jinfo[4] | (static_cast<uint32_t>(F.jinfo[5]) << 16);
     return c;
+}
+
+// Host side of the block records (the kernels fill their LDS copy per thread).
+inline void fill_blocks(BlockInfo (&t)[kMaxBpm], const EntFrame& F)
+{
+    for (int j = 0; j < kMaxBpm; ++j) t[j] = block_info(F.jinfo[j]);
 }
 
 __host__ __device__ __forceinline__ uint64_t guess_entry(const RunCtx& c, uint32_t start)
@@ -279,12 +287,17 @@ __host__ __device__ __forceinline__ int64_t group_sub(uint32_t gl, int t)
 // Kernels (gfx950)
 // ---------------------------------------------------------------------------
 
-__device__ __forceinline__ void load_tables(HuffLut* lds, const HuffLut* g, int ntab, int tid, int nthreads)
+// The frame's Huffman tables and block records into LDS (caller syncs).  The
+// jinfo entries are read from the global frame record (a per-thread index into
+// a register copy would put the record in scratch).
+__device__ __forceinline__ void load_tables(HuffLut* lds, BlockInfo* blocks, const HuffLut* g, const EntFrame& F,
+                                            const EntFrame* Fg, int tid, int nthreads)
 {
     const u32x4* src = reinterpret_cast<const u32x4*>(g);
     u32x4* dst = reinterpret_cast<u32x4*>(lds);
-    const int n = ntab * static_cast<int>(sizeof(HuffLut) / 16);
+    const int n = F.ntab * static_cast<int>(sizeof(HuffLut) / 16);
     for (int i = tid; i < n; i += nthreads) dst[i] = src[i];
+    if (tid < kMaxBpm) blocks[tid] = block_info(Fg->jinfo[tid]);
 }
 
 __device__ __forceinline__ SubStats shfl_down_stats(const SubStats& s, int d)
@@ -348,8 +361,9 @@ __global__ __launch_bounds__(kGroupSubs) void ent_sync_kernel(EntBatchDev b)
     const EntFrame F = b.frames[f];
     const uint32_t gl = w - F.wg_base;
     const uint32_t S = b.sub_bits;
-    const RunCtx c = make_ctx(b, F, tabs);
-    load_tables(tabs, b.tabs + F.tab_base, F.ntab, tid, kGroupSubs);
+    __shared__ BlockInfo blocks[kMaxBpm];
+    const RunCtx c = make_ctx(b, F, tabs, blocks);
+    load_tables(tabs, blocks, b.tabs + F.tab_base, F, b.frames + f, tid, kGroupSubs);
     if (tid < 2) L.nlist[tid] = 0;
     __syncthreads();
     const int64_t k0 = group_sub(gl, 0);
@@ -455,10 +469,11 @@ __global__ __launch_bounds__(256) void ent_link_kernel(EntBatchDev b)
 // the true chain meets the recorded chain again, rewriting entries/statistics
 // on the way; then recompute the aggregates of the groups touched.  Chains are
 // deterministic, so once two agree at a boundary they agree from there on.
-__host__ __device__ __forceinline__ void repair_frame(const EntBatchDev& b, uint32_t f, const HuffLut* tabs)
+__host__ __device__ __forceinline__ void repair_frame(const EntBatchDev& b, uint32_t f, const HuffLut* tabs,
+                                                     const BlockInfo* blocks)
 {
     const EntFrame& F = b.frames[f];
-    const RunCtx c = make_ctx(b, F, tabs);
+    const RunCtx c = make_ctx(b, F, tabs, blocks);
     const uint32_t ng = frame_groups(F.nsub);
     uint32_t done = 0;          // subsequences < done are verified
     uint32_t g_lo = ng, g_hi = 0;
@@ -494,13 +509,14 @@ __host__ __device__ __forceinline__ void repair_frame(const EntBatchDev& b, uint
 __global__ __launch_bounds__(64) void ent_fallback_kernel(EntBatchDev b)
 {
     __shared__ HuffLut tabs[kMaxTables];
+    __shared__ BlockInfo blocks[kMaxBpm];
     const int lane = threadIdx.x;
     const uint32_t f = blockIdx.x;
     if (!(b.status[f] & kStatusFallback)) return;
     const EntFrame F = b.frames[f];
-    load_tables(tabs, b.tabs + F.tab_base, F.ntab, lane, 64);
+    load_tables(tabs, blocks, b.tabs + F.tab_base, F, b.frames + f, lane, 64);
     __syncthreads();
-    if (lane == 0) repair_frame(b, f, tabs);
+    if (lane == 0) repair_frame(b, f, tabs, blocks);
 }
 
 __global__ __launch_bounds__(kGroupSubs) void ent_write_kernel(EntBatchDev b)
@@ -516,7 +532,8 @@ __global__ __launch_bounds__(kGroupSubs) void ent_write_kernel(EntBatchDev b)
     const EntFrame F = b.frames[f];
     const uint32_t gl = w - F.wg_base;
     const uint32_t S = b.sub_bits;
-    load_tables(tabs, b.tabs + F.tab_base, F.ntab, tid, kGroupSubs);
+    __shared__ BlockInfo blocks[kMaxBpm];
+    load_tables(tabs, blocks, b.tabs + F.tab_base, F, b.frames + f, tid, kGroupSubs);
     // block index / DC predictors at this group's start: all previous groups of the frame
     SubStats pre = stats_identity();
     for (uint32_t base = 0; base < gl; base += kGroupSubs) {
@@ -534,7 +551,7 @@ __global__ __launch_bounds__(kGroupSubs) void ent_write_kernel(EntBatchDev b)
     const SubStats excl = stats_combine(pre, tid > 0 ? buf[tid - 1] : stats_identity());
     __syncthreads();   // scratch reads done before blocks are staged
     if (!own) return;
-    const RunCtx c = make_ctx(b, F, tabs);
+    const RunCtx c = make_ctx(b, F, tabs, blocks);
     RunOut o;
     o.coefs = b.coefs + F.coef_off * 64;
     o.stage = stage + tid * kStageStride;
@@ -560,7 +577,9 @@ void emulate(const EntBatchDev& b)
     // sync: per group, phase 1 then the rounds
     for (uint32_t w = 0; w < b.nwg; ++w) {
         const EntFrame& F = b.frames[b.wg_frame[w]];
-        const RunCtx c = make_ctx(b, F, b.tabs + F.tab_base);
+        BlockInfo blocks[kMaxBpm];
+        fill_blocks(blocks, F);
+        const RunCtx c = make_ctx(b, F, b.tabs + F.tab_base, blocks);
         const uint32_t gl = w - F.wg_base;
         std::vector<uint64_t> used(kGroupSubs, 0), x(kGroupSubs, 0), xs0(kGroupSubs, 0), xs1(kGroupSubs, 0);
         std::vector<SubStats> st(kGroupSubs, stats_identity());
@@ -618,13 +637,19 @@ void emulate(const EntBatchDev& b)
         if (!joined) b.status[f] |= kStatusFallback;
     }
     // repair
-    for (uint32_t f = 0; f < b.nframes; ++f)
-        if (b.status[f] & kStatusFallback) repair_frame(b, f, b.tabs + b.frames[f].tab_base);
+    for (uint32_t f = 0; f < b.nframes; ++f) {
+        if (!(b.status[f] & kStatusFallback)) continue;
+        BlockInfo blocks[kMaxBpm];
+        fill_blocks(blocks, b.frames[f]);
+        repair_frame(b, f, b.tabs + b.frames[f].tab_base, blocks);
+    }
     // write (group order = subsequence order)
     alignas(16) int16_t stage[kStageStride];
     for (uint32_t f = 0; f < b.nframes; ++f) {
         const EntFrame& F = b.frames[f];
-        const RunCtx c = make_ctx(b, F, b.tabs + F.tab_base);
+        BlockInfo blocks[kMaxBpm];
+        fill_blocks(blocks, F);
+        const RunCtx c = make_ctx(b, F, b.tabs + F.tab_base, blocks);
         SubStats pre = stats_identity();
         for (uint32_t i = 0; i < F.nsub; ++i) {
             RunOut o;
@@ -1082,7 +1107,9 @@ int hjd_debug_entropy_syncstats(const uint8_t* data, size_t size, int sub_bits, 
     memset(&b, 0, sizeof(b));
     b.data = buf.data();
     b.seg_end = p.seg_end.data();
-    const RunCtx c = make_ctx(b, F, p.tabs);
+    BlockInfo blocks[kMaxBpm];
+    fill_blocks(blocks, F);
+    const RunCtx c = make_ctx(b, F, p.tabs, blocks);
     // true states at every unit boundary: decode one unit at a time (stop = pos + 1)
     std::vector<uint16_t> truth(p.data_bits + 1, 0xFFFF);
     uint64_t cur = pack_state(0, 0, 0, 0);

@@ -46,9 +46,26 @@ constexpr int kOwn = kGroupSubs - kWarm;        // subsequences a group is respo
 constexpr int kDefaultSubBits = 2048;           // S
 constexpr int kStageStride = 24;                // int16 per lane in the staging buffer: one 16-coefficient quarter (+pad)
 
+// A decoded unit (one Huffman symbol + its extra bits) in table form, 16 bits:
+//   [4:0]  total: code length + extra bits s (the bits the unit consumes, >= 1)
+//   [8:5]  s (extra bits = magnitude category)
+//   [15:9] zk: how far the unit moves z, the next coefficient index --
+//          DC 1 (127: a DC symbol > 11, an error), AC value r + 1 (the run
+//          plus the coefficient), ZRL (r = 15, s = 0) 16, EOB (s = 0, r != 15)
+//          64, which ends the block from any z.
+// Precomputing these per code makes the device's symbol step branch-free on
+// its common path (no DC/AC/EOB/ZRL cases).
+__host__ __device__ __forceinline__ uint32_t unit_entry(uint32_t len, uint32_t sym, bool dc)
+{
+    const uint32_t s = sym & 15, r = sym >> 4;
+    const uint32_t zk = dc ? (sym > 11 ? 127u : 1u) : (s ? r + 1 : (r == 15 ? 16u : 64u));
+    return (len + s) | (s << 5) | (zk << 9);
+}
+constexpr uint32_t kZkDcError = 127;
+
 // One Huffman table in device form (2448 B, 16-B multiple).
 struct HuffLut {
-    uint16_t lut[1 << kLutBits];   // (len << 8) | symbol for codes <= kLutBits bits, 0: longer code
+    uint16_t lut[1 << kLutBits];   // unit_entry() for codes <= kLutBits bits, 0: longer code
     int32_t maxcode[17];           // largest code of each length, -1 if none (T.81 F.2.2.3)
     int32_t delta[17];             // valptr[len] - mincode[len]
     uint8_t vals[256];
@@ -161,24 +178,70 @@ __host__ __device__ __forceinline__ uint32_t jinfo_make(int dc_slot, int ac_slot
     return static_cast<uint32_t>(dc_slot | (ac_slot << 3) | (comp << 6) | (out_slot << 8));
 }
 
+// What the symbol step needs about bitstream block j of an MCU: the byte
+// offsets of its DC and AC tables from RunCtx::tabs, its component as 0/1
+// multipliers (the DC sums accumulate with multiply-adds, no branch), and its
+// jinfo.  One 32-B record per j, in LDS on the device, read when j changes.
+struct alignas(16) BlockInfo {
+    uint32_t tdc, tac;
+    int32_t m0, m1, m2;
+    uint32_t ji;
+    uint32_t pad[2];
+};
+static_assert(sizeof(BlockInfo) == 32, "BlockInfo layout");
+
+__host__ __device__ __forceinline__ BlockInfo block_info(uint32_t ji)
+{
+    BlockInfo b;
+    b.tdc = (ji & 7) * static_cast<uint32_t>(sizeof(HuffLut));
+    b.tac = ((ji >> 3) & 7) * static_cast<uint32_t>(sizeof(HuffLut));
+    const uint32_t comp = (ji >> 6) & 3;
+    b.m0 = comp == 0;
+    b.m1 = comp == 1;
+    b.m2 = comp == 2;
+    b.ji = ji;
+    b.pad[0] = b.pad[1] = 0;
+    return b;
+}
+
+constexpr int kMaxBpm = 6;   // blocks per MCU of the supported samplings (4:2:0)
+
 // Everything a run needs about its frame.  `tabs` points at the frame's
-// tables (LDS on the device), `data` at its destuffed bytes (4-B aligned).
+// tables and `blocks` at its block_info() records (both LDS on the device),
+// `data` at its destuffed bytes (4-B aligned).
 struct RunCtx {
     const uint8_t* data;
     const uint32_t* seg_end;   // bit offsets, nseg entries
     const HuffLut* tabs;
+    const BlockInfo* blocks;   // [bpm]
     uint32_t nseg, data_bits;
     int bpm;
-    uint64_t jinfo_q;    // jinfo[0..3], 16 bits each
-    uint32_t jinfo_hi;   // jinfo[4..5]
 };
 
-// Blend (not select) between the two words so the context stays in registers.
-__host__ __device__ __forceinline__ uint32_t jinfo_of(const RunCtx& c, uint32_t j)
+// The record of bitstream block j.
+__host__ __device__ __forceinline__ BlockInfo block_of(const RunCtx& c, uint32_t j) { return c.blocks[j]; }
+
+// (x >> off) & ((1 << w) - 1), w <= 31 (v_bfe_u32); off + w <= 32
+__host__ __device__ __forceinline__ uint32_t ubfe(uint32_t x, uint32_t off, uint32_t w)
 {
-    const uint64_t m = 0ull - static_cast<uint64_t>(j < 4);
-    const uint64_t q = (c.jinfo_q & m) | (static_cast<uint64_t>(c.jinfo_hi) & ~m);
-    return static_cast<uint32_t>(q >> ((j & 3) * 16)) & 0xFFFF;
+#ifdef __HIP_DEVICE_COMPILE__
+    return __builtin_amdgcn_ubfe(x, off, w);
+#else
+    return (x >> off) & ((1u << w) - 1);
+#endif
+}
+
+// a * b + c for |a|, |b| < 2^23 (v_mad_i32_i24; b is a 0/1 multiplier here).
+// asm: the compiler otherwise widens the pattern to v_mad_u64_u32.
+__host__ __device__ __forceinline__ int32_t mad24(int32_t a, int32_t b, int32_t c)
+{
+#ifdef __HIP_DEVICE_COMPILE__
+    int32_t r;
+    asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+#else
+    return a * b + c;
+#endif
 }
 
 // Output side of a write-mode run.
@@ -227,54 +290,66 @@ __host__ __device__ __forceinline__ u32x4 load_chunk(const RunCtx& c, uint32_t c
     return reinterpret_cast<const u32x4*>(c.data)[ci];
 }
 
-// Per-lane bit window: w0:w1 are the (byte-swapped) words under the read
-// position; q holds the following words and r the next raw 16-B chunk, still
-// in flight -- about 18 symbols of lead, enough to hide an HBM miss (each lane
-// streams its own lines, so every line crossing misses the caches).  r is only
-// consumed (swapped into q) four word-advances after its load is issued, so
-// the wait lands there; only fixed register moves, no indexed registers.
+// Word k (0..3) of a chunk: a two-level select, no indexed registers.
+__host__ __device__ __forceinline__ uint32_t pick(const u32x4& v, uint32_t k)
+{
+    const uint32_t lo = (k & 1) ? v.y : v.x, hi = (k & 1) ? v.w : v.z;
+    return (k & 2) ? hi : lo;
+}
+
+__host__ __device__ __forceinline__ u32x4 bswap4(const u32x4& v)
+{
+    u32x4 s;
+    s.x = bswap32(v.x);
+    s.y = bswap32(v.y);
+    s.z = bswap32(v.z);
+    s.w = bswap32(v.w);
+    return s;
+}
+
+// Per-lane bit window: w0:w1 are the (byte-swapped) words wi, wi+1 under the
+// read position; the following words come from the swapped 16-B chunk `cur`
+// (word ci next), and `r`, the raw chunk after it, is in flight -- a lead of
+// 4-8 words (~26-52 symbols), enough to hide an HBM miss (each lane streams
+// its own lines, so every line crossing misses the caches).  r is only read
+// (swapped into cur) when cur runs out, four advances after its load was
+// issued, so the wait lands there, and every definition of r is a load, so
+// the new load can target r's registers.  An advance moves one word and picks
+// one: no shifted queue, so divergent advances cost few instructions.
 struct BitWindow {
-    uint32_t w0, w1, q0, q1, q2, q3, q4, q5;
-    u32x4 r;
-    uint32_t nq, next, wi;
+    uint32_t w0, w1;
+    u32x4 cur, r;
+    uint32_t ci, next, wi;
 
     __host__ __device__ __forceinline__ void advance(const RunCtx& c)
     {
         w0 = w1;
-        w1 = q0;
-        q0 = q1;
-        q1 = q2;
-        q2 = q3;
-        q3 = q4;
-        q4 = q5;
+        w1 = pick(cur, ci);
+#ifdef __HIP_DEVICE_COMPILE__
+        // take the word before cur can be replaced: otherwise the select sinks
+        // below the refill and cur is copied around it
+        asm volatile("" : "+v"(w1)::"memory");
+#endif
         ++wi;
-        if (--nq == 0) {
-            q0 = bswap32(r.x);
-            q1 = bswap32(r.y);
-            q2 = bswap32(r.z);
-            q3 = bswap32(r.w);
-            nq = 4;
+        if (++ci == 4) {
+            cur = bswap4(r);
+            ci = 0;
             r = load_chunk(c, next++);
         }
     }
 
     __host__ __device__ __forceinline__ void seek(const RunCtx& c, uint32_t word)
     {
-        const uint32_t ci = word >> 2;
-        const u32x4 a = load_chunk(c, ci), b = load_chunk(c, ci + 1);
-        r = load_chunk(c, ci + 2);
-        next = ci + 3;
-        w0 = bswap32(a.x);
-        w1 = bswap32(a.y);
-        q0 = bswap32(a.z);
-        q1 = bswap32(a.w);
-        q2 = bswap32(b.x);
-        q3 = bswap32(b.y);
-        q4 = bswap32(b.z);
-        q5 = bswap32(b.w);
-        nq = 6;
-        wi = ci * 4;
-        for (uint32_t i = 0; i < (word & 3); ++i) advance(c);
+        const uint32_t q = word >> 2, k = word & 3;
+        const u32x4 a = load_chunk(c, q), b = load_chunk(c, q + 1);
+        const bool lo = k < 2;   // word + 2 is still in a
+        r = load_chunk(c, lo ? q + 1 : q + 2);
+        next = lo ? q + 2 : q + 3;
+        w0 = bswap32(pick(a, k));
+        w1 = bswap32(k < 3 ? pick(a, k + 1) : b.x);
+        wi = word;
+        cur = bswap4(lo ? a : b);
+        ci = lo ? k + 2 : k - 2;
     }
 };
 
@@ -320,19 +395,22 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
         uint32_t seg_end = c.seg_end[seg];
         if (seg_end < pos) flags |= kError;   // consumed before the window loads are issued
         BitWindow bw;
-        bw.seek(c, pos >> 5);
         bool owned = false;                            // write mode: current block started in this run
         int16_t* cur = nullptr;                        // write mode: its destination (null: not written)
         uint32_t quarter = 0;                          // write mode: quarter of the block being staged
-        uint32_t ji = jinfo_of(c, j);
+        BlockInfo bi = block_of(c, j);
         result = 0;
         bool done = false;
-        while (!done) {
+        bw.seek(c, pos >> 5);
+        // One loop: a nested re-seek loop (so the window never merges with a
+        // seek) measured 13% slower -- its extra exits cost more exec-mask
+        // bookkeeping per unit than the merge copies.
+        for (;;) {
             if (pos >= stop && (!kWrite || !owned)) break;
             const uint32_t nwi = pos >> 5;
             if (nwi != bw.wi) {
                 if (nwi == bw.wi + 1) bw.advance(c);
-                else bw.seek(c, nwi);
+                else bw.seek(c, nwi);   // an overrun of a restart pad moved pos back
             }
             const uint32_t peek = funnel(bw.w0, bw.w1, pos & 31);
             // ---- restart-interval end: < 8 bits left, all ones (or overrun) ----
@@ -345,7 +423,7 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
                     ++seg;
                     j = 0;
                     z = 0;
-                    ji = jinfo_of(c, 0);
+                    bi = block_of(c, 0);
                     owned = false;
                     cur = nullptr;
                     flags |= kReset;
@@ -354,25 +432,21 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
                     if (seg >= c.nseg) {
                         result = pack_state(c.data_bits, 0, 0, c.nseg);
                         done = true;
-                    } else {
-                        seg_end = c.seg_end[seg];
-                        // consume the load inside this rare branch, so the loop
-                        // head does not wait for every outstanding memory op
-                        if (seg_end < pos) flags |= kError;
+                        break;
                     }
+                    seg_end = c.seg_end[seg];
+                    // consume the load inside this rare branch, so the loop
+                    // head does not wait for every outstanding memory op
+                    if (seg_end < pos) flags |= kError;
                     continue;
                 }
             }
-            // ---- one Huffman symbol + its extra bits ----
-            const uint32_t comp = (ji >> 6) & 3;
+            // ---- one unit: Huffman symbol + extra bits (unit_entry fields) ----
             const bool dc = z == 0;
-            const HuffLut& t = c.tabs[dc ? (ji & 7) : ((ji >> 3) & 7)];
-            const uint32_t e = t.lut[peek >> (32 - kLutBits)];
-            uint32_t len, sym;
-            if (e != 0) {
-                len = e >> 8;
-                sym = e & 0xFF;
-            } else {
+            const HuffLut& t = *reinterpret_cast<const HuffLut*>(reinterpret_cast<const char*>(c.tabs) +
+                                                                 (dc ? bi.tdc : bi.tac));
+            uint32_t e = t.lut[peek >> (32 - kLutBits)];
+            if (e == 0) {
                 // Codes longer than the LUT (T.81 F.2.2.3): the length is the first
                 // l with code_l <= MAXCODE[l]; the six compares use independent
                 // loads and selects instead of a dependent loop.
@@ -382,70 +456,65 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
                 const int32_t c15 = static_cast<int32_t>(peek >> 17), c16 = static_cast<int32_t>(peek >> 16);
                 const bool p11 = c11 <= t.maxcode[11], p12 = c12 <= t.maxcode[12], p13 = c13 <= t.maxcode[13];
                 const bool p14 = c14 <= t.maxcode[14], p15 = c15 <= t.maxcode[15], p16 = c16 <= t.maxcode[16];
-                len = p11 ? 11u : p12 ? 12u : p13 ? 13u : p14 ? 14u : p15 ? 15u : 16u;
+                const uint32_t len = p11 ? 11u : p12 ? 12u : p13 ? 13u : p14 ? 14u : p15 ? 15u : 16u;
                 const int32_t code = static_cast<int32_t>(peek >> (32 - len));
-                sym = t.vals[(code + t.delta[len]) & 255];
+                uint32_t sym = t.vals[(code + t.delta[len]) & 255];
                 if (!(p11 || p12 || p13 || p14 || p15 || p16)) {
                     flags |= kError;   // consumes 16 bits as a zero symbol
                     sym = 0;
                 }
+                e = unit_entry(len, sym, dc);
             }
-            const uint32_t s = sym & 15;
-            const uint32_t r = dc ? 0 : sym >> 4;
-            if (dc && sym > 11) flags |= kError;
-            int32_t v = 0;
-            if (s) {
-                const uint32_t bits = (peek << len) >> (32 - s);
-                v = bits < (1u << (s - 1)) ? static_cast<int32_t>(bits) - static_cast<int32_t>((1u << s) - 1)
-                                           : static_cast<int32_t>(bits);
+            const uint32_t total = e & 31, s = (e >> 5) & 15;
+            uint32_t zk = e >> 9;
+            if (zk == kZkDcError) {   // DC symbol > 11
+                flags |= kError;
+                zk = 1;
             }
-            pos += len + s;
-            if (dc) {
-                nblk += 1;
-                d0 += comp == 0 ? v : 0;
-                d1 += comp == 1 ? v : 0;
-                d2 += comp == 2 ? v : 0;
-                if (kWrite) {
+            // extra bits -> value (T.81 F.2.2.1 EXTEND); s = 0 gives 0
+            const uint32_t bits = ubfe(peek, 32 - total, s);
+            const uint32_t m = (1u << s) - 1;
+            const int32_t v = bits <= (m >> 1) ? static_cast<int32_t>(bits - m) : static_cast<int32_t>(bits);
+            pos += total;
+            const uint32_t zn = z + zk;
+            if (zn > 64 && s != 0) flags |= kError;   // AC coefficient past index 63
+            // DC unit: a block starts (per-component sums by 0/1 multipliers, no branch)
+            const int32_t dv = dc ? v : 0;
+            nblk += dc ? 1 : 0;
+            d0 = mad24(dv, bi.m0, d0);
+            d1 = mad24(dv, bi.m1, d1);
+            d2 = mad24(dv, bi.m2, d2);
+            if (kWrite) {
+                if (dc) {
                     owned = true;
-                    p0 += comp == 0 ? v : 0;
-                    p1 += comp == 1 ? v : 0;
-                    p2 += comp == 2 ? v : 0;
+                    p0 = mad24(v, bi.m0, p0);
+                    p1 = mad24(v, bi.m1, p1);
+                    p2 = mad24(v, bi.m2, p2);
                     // MCU-major destination; on valid data blk % bpm == j.  Blocks past
                     // the frame's count are ignored (as the host decoder stops there).
-                    const uint32_t dst = blk - j + (ji >> 8);
+                    const uint32_t dst = blk - j + (bi.ji >> 8);
                     cur = nullptr;
                     if (blk < out->nblocks) {
                         if (dst < out->nblocks && blk % static_cast<uint32_t>(c.bpm) == j) {
                             cur = out->coefs + static_cast<uint64_t>(dst) * 64;
                             zero_quarter(out->stage);
-                            out->stage[0] = static_cast<int16_t>(comp == 0 ? p0 : (comp == 1 ? p1 : p2));
+                            out->stage[0] = static_cast<int16_t>(p0 * bi.m0 + p1 * bi.m1 + p2 * bi.m2);
                             quarter = 0;
                         } else {
                             flags |= kError;   // a restart interval ended inside an MCU
                         }
                     }
-                }
-                z = 1;
-            } else if (s == 0) {
-                z = r == 15 ? z + 16 : 64;       // ZRL / EOB
-            } else {
-                z += r;
-                if (z > 63) {
-                    flags |= kError;
-                    z = 64;
-                } else {
-                    if (kWrite && cur) {
-                        const uint32_t qz = z >> 4;
-                        if (qz != quarter) {
-                            flush_quarters(cur, out->stage, quarter, qz);
-                            quarter = qz;
-                        }
-                        out->stage[z & 15] = static_cast<int16_t>(v);
+                } else if (s != 0 && zn <= 64 && cur) {
+                    const uint32_t zi = zn - 1;   // the coefficient's index: z + run
+                    const uint32_t qz = zi >> 4;
+                    if (qz != quarter) {
+                        flush_quarters(cur, out->stage, quarter, qz);
+                        quarter = qz;
                     }
-                    ++z;
+                    out->stage[zi & 15] = static_cast<int16_t>(v);
                 }
             }
-            if (z >= 64) {
+            if (zn >= 64) {   // EOB, ZRL or a coefficient reaching the end, or an error
                 if (kWrite && owned) {
                     if (cur) flush_quarters(cur, out->stage, quarter, 4);   // the rest of the block
                     blk += 1;
@@ -454,7 +523,9 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
                 }
                 z = 0;
                 j = j + 1 == static_cast<uint32_t>(c.bpm) ? 0 : j + 1;
-                ji = jinfo_of(c, j);
+                bi = block_of(c, j);
+            } else {
+                z = zn;
             }
         }
         if (!done) result = pack_state(pos, j, z, seg);
