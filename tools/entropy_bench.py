@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--sampling", default="420", choices=["420", "444"])
     ap.add_argument("--pool", type=int, default=8)
     ap.add_argument("--pixels", action="store_true", help="also run the fused pixel kernel (full decode)")
+    ap.add_argument("--no-check", action="store_true",
+                    help="timing experiments whose outputs are wrong by design (HJD_LIB variants)")
     args = ap.parse_args()
 
     import torch
@@ -52,10 +54,18 @@ def main():
         else:
             gd.decode_coefs(datas, coefs, stream)
 
+    def sync():
+        try:
+            return gd.sync()
+        except Exception:
+            if not args.no_check:
+                raise
+            return [0] * args.frames
+
     call()
-    status = gd.sync()
+    status = sync()
     # exactness spot check against the host decoder (first distinct frames)
-    if not args.pixels:
+    if not args.pixels and not args.no_check:
         offs = gd.decode_coefs(datas, coefs, stream)
         gd.sync()
         got = coefs.cpu().numpy()
@@ -69,7 +79,7 @@ def main():
     for _ in range(args.reps):
         call()
     e1.record(stream)
-    gd.sync()
+    sync()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     dev_ms = e0.elapsed_time(e1) / args.reps

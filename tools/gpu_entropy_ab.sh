@@ -19,7 +19,7 @@ for rep in 1 2; do
     v=$(basename $(dirname $lib))
     if [ $lib = new ]; then v=new; unset HJD_LIB; else export HJD_LIB=$R/$lib; fi
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_${v}_$rep -o ent -- \
-        python3 $R/tools/entropy_bench.py --frames 64 --reps 3 > $O/run_${v}_$rep.json 2> $O/run_${v}_$rep.err \
+        python3 $R/tools/entropy_bench.py --frames 64 --reps 3 ${EB_ARGS:-} > $O/run_${v}_$rep.json 2> $O/run_${v}_$rep.err \
         || { echo PROF $v FAILED; tail $O/run_${v}_$rep.err; exit 1; }
     echo "$v $rep: $(find $O/kt_${v}_$rep -name '*kernel_stats.csv' -exec cat {} \; | grep -E 'ent_(sync|write)' | cut -d, -f4 | tr '\n' ' ')"
   done
