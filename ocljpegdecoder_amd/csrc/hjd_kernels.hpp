@@ -96,10 +96,24 @@ __device__ __forceinline__ void cursor_load(FrameCursor& c, const FrameDev* __re
     c.qt2 = f.qt[2];
 }
 
-// Scalar binary search for the frame owning `task` (once per wave).
+// The frame owning `task` (once per wave, scalar).  Batches of equal frames
+// (the common case) have task_begin[i] = i * K: the guess task / K is checked
+// against the record it loads anyway, so a wave start costs two dependent
+// scalar loads instead of a ~log2(nframes)-deep binary search, which is the
+// fallback for mixed plans.
 __device__ __forceinline__ void cursor_seek(FrameCursor& c, const FrameDev* __restrict__ fr, int nframes,
                                             int64_t total, int64_t task)
 {
+    if (nframes > 1) {
+        const int64_t k = fr[1].task_begin;   // tasks of frame 0
+        if (k > 0 && task < (int64_t(1) << 32)) {
+            const int64_t g = static_cast<uint32_t>(task) / static_cast<uint32_t>(k);   // 32-bit udiv
+            if (g < nframes) {
+                cursor_load(c, fr, nframes, total, static_cast<int>(g));
+                if (c.begin <= task && task < c.end) return;
+            }
+        }
+    }
     int lo = 0, hi = nframes - 1;
     while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
