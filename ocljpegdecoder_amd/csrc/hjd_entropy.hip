@@ -370,30 +370,63 @@ __global__ __launch_bounds__(kGroupSubs) void ent_sync_kernel(EntBatchDev b)
     const int64_t k = k0 + tid;
     const bool valid = k >= 0 && k < static_cast<int64_t>(F.nsub);
     const uint32_t ku = static_cast<uint32_t>(k);
-    // phase 1: every subsequence from its guessed entry
+    // phase 1: every subsequence from its guessed entry, in two runs split at
+    // its middle (the checkpoint), keeping the state there and the statistics
+    // of the second half
+    const uint32_t mid = ku * S + S / 2;
     uint64_t used = valid ? guess_entry(c, ku * S) : 0;
-    SubStats st = stats_identity();
-    uint64_t x = valid ? run<false>(c, used, (ku + 1) * S, st, nullptr) : used;
+    SubStats st = stats_identity(), suf = stats_identity();
+    uint64_t cp = used, x = used;
+    if (valid) {
+        cp = run<false>(c, used, mid, st, nullptr);
+        x = run<false>(c, cp, (ku + 1) * S, suf, nullptr);
+        st = stats_combine(st, suf);
+    }
     L.x[tid] = x;
     __syncthreads();
-    // round 0: every subsequence from its predecessor's exit (all lanes busy)
-    bool changed = false;
+    // round 0, step A: every subsequence from its predecessor's exit, first to
+    // the checkpoint only (all lanes busy).  A run that arrives in phase 1's
+    // checkpoint state continues exactly as phase 1 did (a run is a function of
+    // its state), so its exit and second-half statistics are known; the
+    // others are "pending" and go on in step B.  Measured (syncstats): at
+    // 4:2:0 53% of guessed runs are in step by mid-subsequence, at 4:4:4 94%,
+    // so round 0 decodes 0.74 / 0.53 of the bits it decoded in full.
+    bool pending = false;
+    uint64_t resume = 0;
     if (valid && tid > 0 && k > 0) {
         const uint64_t e = L.x[tid - 1];
         if (!same_state(e, used)) {
             SubStats s2 = stats_identity();
-            const uint64_t x2 = run<false>(c, e, (ku + 1) * S, s2, nullptr);
-            changed = !same_state(x2, x);
+            resume = run<false>(c, e, mid, s2, nullptr);
             used = e;
-            st = s2;
-            x = x2;
+            if (same_state(resume, cp)) {
+                st = stats_combine(s2, suf);
+            } else {
+                pending = true;
+                st = s2;
+            }
         }
     }
     L.used[tid] = used;
     L.st[tid] = st;
     __syncthreads();   // everyone has read L.x (old) before it is overwritten
-    L.x[tid] = x;
-    if (changed && tid + 1 < kGroupSubs && k + 1 < static_cast<int64_t>(F.nsub))
+    if (pending) {     // park the resume state where the exit goes
+        L.x[tid] = resume;
+        L.list[1][atomicAdd(&L.nlist[1], 1)] = static_cast<uint16_t>(tid);
+    }
+    __syncthreads();
+    // step B: the pending second halves, compacted onto the first lanes
+    if (tid < L.nlist[1]) {
+        const int item = L.list[1][tid];
+        const uint32_t kk = static_cast<uint32_t>(k0 + item);
+        SubStats s2 = stats_identity();
+        const uint64_t x2 = run<false>(c, L.x[item], (kk + 1) * S, s2, nullptr);
+        L.st[item] = stats_combine(L.st[item], s2);
+        L.x[item] = x2;
+    }
+    __syncthreads();
+    // a changed exit changes the successor's entry
+    if (pending && !same_state(L.x[tid], x) && tid + 1 < kGroupSubs && k + 1 < static_cast<int64_t>(F.nsub))
         L.list[0][atomicAdd(&L.nlist[0], 1)] = static_cast<uint16_t>(tid + 1);
     __syncthreads();
     // later rounds: only the subsequences whose entry changed, compacted onto the
@@ -582,24 +615,41 @@ void emulate(const EntBatchDev& b)
         const RunCtx c = make_ctx(b, F, b.tabs + F.tab_base, blocks);
         const uint32_t gl = w - F.wg_base;
         std::vector<uint64_t> used(kGroupSubs, 0), x(kGroupSubs, 0), xs0(kGroupSubs, 0), xs1(kGroupSubs, 0);
-        std::vector<SubStats> st(kGroupSubs, stats_identity());
+        std::vector<SubStats> st(kGroupSubs, stats_identity()), suf(kGroupSubs, stats_identity());
+        std::vector<uint64_t> cp(kGroupSubs, 0);
         auto valid = [&](int t) { const int64_t k = group_sub(gl, t); return k >= 0 && k < int64_t(F.nsub); };
-        for (int t = 0; t < kGroupSubs; ++t) {
+        for (int t = 0; t < kGroupSubs; ++t) {   // phase 1, split at the checkpoint
             if (!valid(t)) continue;
             const uint32_t k = static_cast<uint32_t>(group_sub(gl, t));
             used[t] = guess_entry(c, k * S);
-            x[t] = run<false>(c, used[t], (k + 1) * S, st[t], nullptr);
+            cp[t] = run<false>(c, used[t], k * S + S / 2, st[t], nullptr);
+            x[t] = run<false>(c, cp[t], (k + 1) * S, suf[t], nullptr);
+            st[t] = stats_combine(st[t], suf[t]);
             xs0[t] = x[t];
         }
         std::vector<uint64_t>* cur = &xs0;
         std::vector<uint64_t>* nxt = &xs1;
-        for (;;) {
+        for (int round = 0;; ++round) {
             bool changed = false;
             for (int t = 0; t < kGroupSubs; ++t) {
                 const int64_t k = group_sub(gl, t);
                 if (valid(t) && t > 0 && k > 0 && !same_state((*cur)[t - 1], used[t])) {
+                    const uint32_t ku = static_cast<uint32_t>(k);
                     SubStats s2 = stats_identity();
-                    const uint64_t x2 = run<false>(c, (*cur)[t - 1], (static_cast<uint32_t>(k) + 1) * S, s2, nullptr);
+                    uint64_t x2;
+                    if (round == 0) {   // round 0: to the checkpoint, on if phase 1 is not joined there
+                        const uint64_t r = run<false>(c, (*cur)[t - 1], ku * S + S / 2, s2, nullptr);
+                        if (same_state(r, cp[t])) {
+                            x2 = x[t];
+                            s2 = stats_combine(s2, suf[t]);
+                        } else {
+                            SubStats s3 = stats_identity();
+                            x2 = run<false>(c, r, (ku + 1) * S, s3, nullptr);
+                            s2 = stats_combine(s2, s3);
+                        }
+                    } else {
+                        x2 = run<false>(c, (*cur)[t - 1], (ku + 1) * S, s2, nullptr);
+                    }
                     changed |= !same_state(x2, x[t]);
                     used[t] = (*cur)[t - 1];
                     st[t] = s2;
