@@ -1,0 +1,56 @@
+"""bench.py's N-rank path on the one-GPU box: two ranks launched exactly as the
+driver launches the scaling bench (torch.distributed.run, 127.0.0.1), but
+with HJD_BENCH_SAME_DEVICE=1 and the gloo process group so both ranks share
+device 0 (RCCL cannot put two ranks on one GPU).  Checks the contract fields
+of the single JSON line rank 0 prints: n_gpus, whole-job value, weak scaling,
+no data-path collective.  The real N>1 run (RCCL over xGMI) is the driver's."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(workload, frames, extra=()):
+    env = dict(os.environ, HJD_BENCH_SAME_DEVICE="1", MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="4")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+           "--workload", workload, "--frames", str(frames), "--no-cpu", "--dist-backend", "gloo", *extra]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout[-3000:]           # rank 0 only, one line
+    return json.loads(lines[0])
+
+
+@pytest.mark.gpu
+def test_two_ranks_pixel_bench():
+    r = _run("4k420", 8)
+    assert r["n_gpus"] == 2 and r["steps"] == 3 and r["warmup"] == 1
+    assert r["scaling"] == "weak" and r["higher_is_better"] is True
+    assert r["value"] > 0 and r["ms_per_step"] > 0
+    # whole-job value: both ranks' pixels over the max-over-ranks wall time
+    px = 2 * 3 * 8 * 3840 * 2160
+    assert abs(r["value"] - px / (r["ms_per_step"] * 3 / 1e3) / 1e6) / r["value"] < 0.02
+    assert "no collective" in r["config"]["parallelism"] or "x2" in r["config"]["parallelism"]
+
+
+@pytest.mark.gpu
+def test_two_ranks_stream_bench():
+    r = _run("stream4k420", 16)
+    assert r["n_gpus"] == 2 and r["value"] > 0
+    assert r["end_to_end"]["output_checked_vs_oracle"] is True
+    assert r["config"]["entropy_decode"] == "gpu"
