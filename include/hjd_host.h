@@ -39,8 +39,17 @@ typedef struct hjd_jpeg_info {
     int64_t nblocks;           /* coefficient blocks (64 int16 each) */
     int32_t qt[3][64];         /* quantisation table of each component, file (zigzag) order */
     int32_t qt_precision[3];   /* 0 = 8-bit DQT entries, 1 = 16-bit */
-    int64_t scan_offset;       /* byte offset of the entropy-coded segment */
+    int64_t scan_offset;       /* byte offset of the (first) entropy-coded segment */
+    int32_t process;           /* 0 = baseline (SOF0), 1 = extended sequential (SOF1), 2 = progressive (SOF2) */
+    int32_t single_scan;       /* 1: one interleaved sequential scan holds the image (GPU entropy decodable) */
 } hjd_jpeg_info;
+
+/* Besides the reference's single interleaved baseline scan, the host decoder
+ * takes sequential files with several scans (SOF0/SOF1: non-interleaved or
+ * partly interleaved components) and progressive files (SOF2: spectral
+ * selection + successive approximation, EOB runs, restarts); the result is the
+ * same coefficient layout.  For those, qt[] is final after decode (tables
+ * latch at each component's first scan). */
 
 /* Parse headers up to SOS.  Returns HJD_OK, or HJD_E_INVALID for malformed or
  * unsupported files (hjd_last_error() says why). */

@@ -45,6 +45,8 @@ class HjdJpegInfo(ctypes.Structure):
         ("qt", (ctypes.c_int32 * 64) * 3),
         ("qt_precision", ctypes.c_int32 * 3),
         ("scan_offset", ctypes.c_int64),
+        ("process", ctypes.c_int32),
+        ("single_scan", ctypes.c_int32),
     ]
 
 

@@ -36,16 +36,27 @@ struct Component {
     int td = 0, ta = 0;      // DC / AC Huffman table ids (from SOS)
 };
 
+// One scan's header (T.81 B.2.3): its components (frame indices) and, for a
+// progressive scan, the spectral band ss..se and successive-approximation bits.
+struct ScanSpec {
+    int ns = 0;
+    int comp[3] = {0, 1, 2};
+    int ss = 0, se = 63, ah = 0, al = 0;
+    size_t offset = 0;       // first byte of the entropy-coded segment
+};
+
 struct Frame {
     int width = 0, height = 0, ncomp = 0;
+    int process = -1;        // 0 = baseline (SOF0), 1 = extended sequential (SOF1), 2 = progressive (SOF2)
     Component comp[3];
-    int32_t qt[4][64];
+    int32_t qt[4][64] = {};
     int qt_prec[4] = {-1, -1, -1, -1};
     HuffTable dc[4], ac[4];
     int restart_interval = 0;
-    int scan_order[3] = {0, 1, 2};   // frame component index of each scan component
+    int scan_order[3] = {0, 1, 2};   // frame component index of each scan component (first scan)
     size_t scan_offset = 0;
     int sampling = -1;
+    ScanSpec scan;                   // the scan parse_segments stopped at
 };
 
 inline int be16(const uint8_t* p) { return (p[0] << 8) | p[1]; }
@@ -78,18 +89,116 @@ int build_table(HuffTable& t, const uint8_t counts[16], const uint8_t* symbols, 
     return 0;
 }
 
-int parse(const uint8_t* d, size_t n, Frame& f)
+int parse_sof(const uint8_t* s, int sl, int marker, Frame& f)
 {
-    if (n < 4 || d[0] != 0xFF || d[1] != 0xD8) return set_error(HJD_E_INVALID, "SOI missing");
-    size_t p = 2;
-    bool have_sof = false;
+    if (f.process >= 0) return set_error(HJD_E_INVALID, "second SOF marker");
+    if (sl < 6) return set_error(HJD_E_INVALID, "truncated SOF");
+    if (s[0] != 8) return set_error(HJD_E_INVALID, "unsupported bit depth %d", s[0]);
+    f.process = marker - 0xC0;
+    f.height = be16(s + 1);
+    f.width = be16(s + 3);
+    f.ncomp = s[5];
+    if (f.ncomp != 3 && f.ncomp != 1)
+        return set_error(HJD_E_INVALID, "unsupported number of components %d", f.ncomp);
+    if (sl < 6 + 3 * f.ncomp) return set_error(HJD_E_INVALID, "truncated SOF");
+    if (f.width <= 0 || f.height <= 0) return set_error(HJD_E_INVALID, "invalid dimensions");
+    for (int c = 0; c < f.ncomp; ++c) {
+        f.comp[c].id = s[6 + 3 * c];
+        f.comp[c].h = s[7 + 3 * c] >> 4;
+        f.comp[c].v = s[7 + 3 * c] & 15;
+        f.comp[c].tq = s[8 + 3 * c];
+        if (f.comp[c].tq > 3) return set_error(HJD_E_INVALID, "bad quantisation table id");
+        if (f.comp[c].h < 1 || f.comp[c].h > 4 || f.comp[c].v < 1 || f.comp[c].v > 4)
+            return set_error(HJD_E_INVALID, "bad sampling factors");
+    }
+    // src/decoder.cpp:58-69 accepts H2V2/H1V1/H1V1 and all-H1V1; H2V1/H1V1/H1V1
+    // (4:2:2) and one component (gray) are this library's extensions
+    // (SURVEY.md s8(f) rank 4).  A one-component scan is non-interleaved:
+    // its MCU is one block whatever the sampling factors (T.81 A.2.2).
+    const Component* c = f.comp;
+    const bool chroma11 = f.ncomp == 3 && c[1].h == 1 && c[1].v == 1 && c[2].h == 1 && c[2].v == 1;
+    if (f.ncomp == 1)
+        f.sampling = HJD_GRAY;
+    else if (chroma11 && c[0].h == 2 && c[0].v == 2)
+        f.sampling = HJD_YUV420;
+    else if (chroma11 && c[0].h == 1 && c[0].v == 1)
+        f.sampling = HJD_YUV444;
+    else if (chroma11 && c[0].h == 2 && c[0].v == 1)
+        f.sampling = HJD_YUV422;
+    else
+        return set_error(HJD_E_INVALID, "unsupported sampling (4:2:0, 4:4:4, 4:2:2 or gray)");
+    return HJD_OK;
+}
+
+// SOS (src/parser.cpp:132-154; T.81 B.2.3).  The reference takes one scan
+// holding every component; sequential files with several scans (one or two
+// components each) and progressive scans (G.1.1.1.1 band rules) are this
+// library's extensions.
+int parse_sos(const uint8_t* s, int sl, Frame& f, ScanSpec& sc)
+{
+    if (f.process < 0) return set_error(HJD_E_INVALID, "SOS before SOF");
+    if (sl < 1) return set_error(HJD_E_INVALID, "truncated SOS");
+    const int ns = s[0];
+    if (ns < 1 || ns > f.ncomp || sl < 1 + 2 * ns + 3) return set_error(HJD_E_INVALID, "bad SOS component count");
+    sc.ns = ns;
+    for (int i = 0; i < ns; ++i) {
+        const int cid = s[1 + 2 * i], tdta = s[2 + 2 * i];
+        int fc = -1;
+        for (int c = 0; c < f.ncomp; ++c)
+            if (f.comp[c].id == cid) fc = c;
+        if (fc < 0) return set_error(HJD_E_INVALID, "scan component %d not in frame", cid);
+        for (int j = 0; j < i; ++j)
+            if (sc.comp[j] == fc) return set_error(HJD_E_INVALID, "component %d twice in one scan", cid);
+        sc.comp[i] = fc;
+        f.comp[fc].td = tdta >> 4;
+        f.comp[fc].ta = tdta & 15;
+        if (f.comp[fc].td > 3 || f.comp[fc].ta > 3) return set_error(HJD_E_INVALID, "bad Huffman table id");
+    }
+    const uint8_t* tail = s + 1 + 2 * ns;
+    sc.ss = tail[0];
+    sc.se = tail[1];
+    sc.ah = tail[2] >> 4;
+    sc.al = tail[2] & 15;
+    const bool prog = f.process == 2;
+    if (!prog) {
+        if (sc.ss != 0 || sc.se != 63 || sc.ah != 0 || sc.al != 0)
+            return set_error(HJD_E_INVALID, "not a sequential scan (Ss/Se/Ah/Al)");
+    } else {
+        const bool dc = sc.ss == 0;
+        if ((dc && sc.se != 0) || (!dc && (sc.se < sc.ss || sc.se > 63 || ns != 1)) || sc.al > 13 ||
+            (sc.ah != 0 && sc.ah != sc.al + 1))
+            return set_error(HJD_E_INVALID, "bad progressive scan (Ss=%d Se=%d Ah=%d Al=%d Ns=%d)", sc.ss, sc.se,
+                             sc.ah, sc.al, ns);
+    }
+    for (int i = 0; i < ns; ++i) {
+        const Component& c = f.comp[sc.comp[i]];
+        if (f.qt_prec[c.tq] < 0) return set_error(HJD_E_INVALID, "missing quantisation table");
+        const bool need_dc = sc.ss == 0 && sc.ah == 0, need_ac = sc.se > 0;
+        if (need_dc && !f.dc[c.td].defined) return set_error(HJD_E_INVALID, "missing DC Huffman table");
+        if (need_ac && !f.ac[c.ta].defined) return set_error(HJD_E_INVALID, "missing AC Huffman table");
+    }
+    return HJD_OK;
+}
+
+// Marker segments from d[p] up to the next SOS (returns HJD_OK with f.scan set
+// and *p past the SOS) or, after the first scan, EOI / end of data (*eoi).
+int parse_segments(const uint8_t* d, size_t n, size_t* pp, Frame& f, bool after_scan, bool* eoi)
+{
+    size_t p = *pp;
+    *eoi = false;
     for (;;) {
         while (p < n && d[p] != 0xFF) ++p;           // tolerate garbage between segments
         while (p < n && d[p] == 0xFF) ++p;           // fill bytes
-        if (p >= n) return set_error(HJD_E_INVALID, "no SOS marker");
+        if (p >= n) {
+            if (after_scan) { *eoi = true; return HJD_OK; }   // missing EOI: take what was decoded
+            return set_error(HJD_E_INVALID, "no SOS marker");
+        }
         const uint8_t m = d[p++];
         if (m == 0xD8 || (m >= 0xD0 && m <= 0xD7) || m == 0x01) continue;   // no length
-        if (m == 0xD9) return set_error(HJD_E_INVALID, "EOI before SOS");
+        if (m == 0xD9) {
+            if (after_scan) { *eoi = true; *pp = p; return HJD_OK; }
+            return set_error(HJD_E_INVALID, "EOI before SOS");
+        }
         if (p + 2 > n) return set_error(HJD_E_INVALID, "truncated marker segment");
         const int len = be16(d + p);
         if (len < 2 || p + len > n) return set_error(HJD_E_INVALID, "bad segment length");
@@ -109,45 +218,14 @@ int parse(const uint8_t* d, size_t n, Frame& f)
             }
             break;
         }
-        case 0xC0: {   // SOF0 (src/parser.cpp:102-130)
-            if (sl < 6) return set_error(HJD_E_INVALID, "truncated SOF0");
-            if (s[0] != 8) return set_error(HJD_E_INVALID, "unsupported bit depth %d", s[0]);
-            f.height = be16(s + 1);
-            f.width = be16(s + 3);
-            f.ncomp = s[5];
-            if (f.ncomp != 3 && f.ncomp != 1)
-                return set_error(HJD_E_INVALID, "unsupported number of components %d", f.ncomp);
-            if (sl < 6 + 3 * f.ncomp) return set_error(HJD_E_INVALID, "truncated SOF0");
-            if (f.width <= 0 || f.height <= 0) return set_error(HJD_E_INVALID, "invalid dimensions");
-            for (int c = 0; c < f.ncomp; ++c) {
-                f.comp[c].id = s[6 + 3 * c];
-                f.comp[c].h = s[7 + 3 * c] >> 4;
-                f.comp[c].v = s[7 + 3 * c] & 15;
-                f.comp[c].tq = s[8 + 3 * c];
-                if (f.comp[c].tq > 3) return set_error(HJD_E_INVALID, "bad quantisation table id");
-            }
-            // src/decoder.cpp:58-69 accepts H2V2/H1V1/H1V1 and all-H1V1; H2V1/H1V1/H1V1
-            // (4:2:2) and one component (gray) are this library's extensions
-            // (SURVEY.md s8(f) rank 4).  A one-component scan is non-interleaved:
-            // its MCU is one block whatever the sampling factors (T.81 A.2.2).
-            const Component* c = f.comp;
-            const bool chroma11 = f.ncomp == 3 && c[1].h == 1 && c[1].v == 1 && c[2].h == 1 && c[2].v == 1;
-            if (f.ncomp == 1)
-                f.sampling = HJD_GRAY;
-            else if (chroma11 && c[0].h == 2 && c[0].v == 2)
-                f.sampling = HJD_YUV420;
-            else if (chroma11 && c[0].h == 1 && c[0].v == 1)
-                f.sampling = HJD_YUV444;
-            else if (chroma11 && c[0].h == 2 && c[0].v == 1)
-                f.sampling = HJD_YUV422;
-            else
-                return set_error(HJD_E_INVALID, "unsupported sampling (4:2:0, 4:4:4, 4:2:2 or gray)");
-            have_sof = true;
+        case 0xC0: case 0xC1: case 0xC2: {   // SOF0 (src/parser.cpp:102-130); SOF1/SOF2: extensions
+            const int rc = parse_sof(s, sl, m, f);
+            if (rc) return rc;
             break;
         }
-        case 0xC1: case 0xC2: case 0xC3: case 0xC5: case 0xC6: case 0xC7:
+        case 0xC3: case 0xC5: case 0xC6: case 0xC7:
         case 0xC9: case 0xCA: case 0xCB: case 0xCD: case 0xCE: case 0xCF:
-            return set_error(HJD_E_INVALID, "only baseline (SOF0) JPEG is supported");
+            return set_error(HJD_E_INVALID, "only Huffman-coded sequential or progressive JPEG is supported");
         case 0xC4: {   // DHT (src/parser.cpp:170-270)
             int q = 0;
             while (q < sl) {
@@ -167,31 +245,11 @@ int parse(const uint8_t* d, size_t n, Frame& f)
             if (sl < 2) return set_error(HJD_E_INVALID, "truncated DRI");
             f.restart_interval = be16(s);
             break;
-        case 0xDA: {   // SOS (src/parser.cpp:132-154)
-            if (!have_sof) return set_error(HJD_E_INVALID, "SOS before SOF0");
-            const int ns = f.ncomp;
-            if (sl < 1 || s[0] != ns || sl < 1 + 2 * ns + 3)
-                return set_error(HJD_E_INVALID, "unsupported scan (needs all components interleaved)");
-            for (int i = 0; i < ns; ++i) {
-                const int cid = s[1 + 2 * i], tdta = s[2 + 2 * i];
-                int fc = -1;
-                for (int c = 0; c < ns; ++c)
-                    if (f.comp[c].id == cid) fc = c;
-                if (fc < 0) return set_error(HJD_E_INVALID, "scan component %d not in frame", cid);
-                f.scan_order[i] = fc;
-                f.comp[fc].td = tdta >> 4;
-                f.comp[fc].ta = tdta & 15;
-                if (f.comp[fc].td > 3 || f.comp[fc].ta > 3) return set_error(HJD_E_INVALID, "bad Huffman table id");
-            }
-            const uint8_t* tail = s + 1 + 2 * ns;
-            if (tail[0] != 0 || tail[1] != 63 || tail[2] != 0)
-                return set_error(HJD_E_INVALID, "not a baseline scan (Ss/Se/Ah/Al)");
-            for (int c = 0; c < ns; ++c) {
-                if (f.qt_prec[f.comp[c].tq] < 0) return set_error(HJD_E_INVALID, "missing quantisation table");
-                if (!f.dc[f.comp[c].td].defined) return set_error(HJD_E_INVALID, "missing DC Huffman table");
-                if (!f.ac[f.comp[c].ta].defined) return set_error(HJD_E_INVALID, "missing AC Huffman table");
-            }
-            f.scan_offset = p + len;
+        case 0xDA: {   // SOS
+            const int rc = parse_sos(s, sl, f, f.scan);
+            if (rc) return rc;
+            f.scan.offset = p + len;
+            *pp = p + len;
             return HJD_OK;
         }
         default:       // APPn, COM, DNL, ...: skip (src/parser.cpp:295-322 skips APPn)
@@ -200,6 +258,23 @@ int parse(const uint8_t* d, size_t n, Frame& f)
         p += len;
     }
 }
+
+// Headers up to the first SOS.
+int parse(const uint8_t* d, size_t n, Frame& f)
+{
+    if (n < 4 || d[0] != 0xFF || d[1] != 0xD8) return set_error(HJD_E_INVALID, "SOI missing");
+    size_t p = 2;
+    bool eoi = false;
+    const int rc = parse_segments(d, n, &p, f, false, &eoi);
+    if (rc) return rc;
+    for (int i = 0; i < f.scan.ns; ++i) f.scan_order[i] = f.scan.comp[i];
+    f.scan_offset = f.scan.offset;
+    return HJD_OK;
+}
+
+// One interleaved sequential scan holds the whole image: the reference's
+// case (src/decoder.cpp:308-344) and the GPU entropy decoder's.
+inline bool single_scan(const Frame& f) { return f.process != 2 && f.scan.ns == f.ncomp; }
 
 void fill_info(const Frame& f, hjd_jpeg_info* info)
 {
@@ -219,6 +294,8 @@ void fill_info(const Frame& f, hjd_jpeg_info* info)
         info->qt_precision[c] = f.qt_prec[f.comp[fc].tq];
     }
     info->scan_offset = static_cast<int64_t>(f.scan_offset);
+    info->process = f.process;
+    info->single_scan = single_scan(f) ? 1 : 0;
 }
 
 // Entropy-coded segment reader: 64-bit MSB-first accumulator, FF00 de-stuffing,
@@ -356,6 +433,240 @@ int decode_scan(const uint8_t* d, size_t n, const Frame& f, const hjd_jpeg_info&
     return HJD_OK;
 }
 
+// ---- several scans per frame: sequential multi-scan and progressive -------
+// (extensions; the reference decodes one interleaved sequential scan)
+
+// Where block (by, bx) of frame component c lives in the MCU-major output, and
+// the component's block grid in a non-interleaved scan (T.81 A.2.2: ceil of
+// the component's own dimensions, not padded to whole MCUs; blocks outside it
+// are never coded and stay zero).
+struct CoefLayout {
+    int mcu_w = 0, mcu_h = 0, bpm = 0;
+    int hs[3] = {1, 1, 1}, vs[3] = {1, 1, 1}, base[3] = {0, 0, 0};
+    int bw[3] = {0, 0, 0}, bh[3] = {0, 0, 0};
+
+    CoefLayout(const Frame& f, const hjd_jpeg_info& info) : mcu_w(info.mcu_w), mcu_h(info.mcu_h)
+    {
+        if (f.ncomp == 1) {
+            bpm = 1;
+            bw[0] = (f.width + 7) / 8;
+            bh[0] = (f.height + 7) / 8;
+            return;
+        }
+        const int hmax = f.comp[0].h, vmax = f.comp[0].v;   // chroma is H1V1 in every admitted sampling
+        for (int c = 0; c < 3; ++c) {
+            hs[c] = f.comp[c].h;
+            vs[c] = f.comp[c].v;
+            const int cw = (f.width * hs[c] + hmax - 1) / hmax, ch = (f.height * vs[c] + vmax - 1) / vmax;
+            bw[c] = (cw + 7) / 8;
+            bh[c] = (ch + 7) / 8;
+        }
+        base[1] = hs[0] * vs[0];
+        base[2] = base[1] + 1;
+        bpm = base[2] + 1;
+    }
+    int16_t* at(int16_t* coefs, int c, int by, int bx) const
+    {
+        const int64_t mcu = static_cast<int64_t>(by / vs[c]) * mcu_w + bx / hs[c];
+        return coefs + (mcu * bpm + base[c] + (by % vs[c]) * hs[c] + bx % hs[c]) * 64;
+    }
+};
+
+inline int get_bit(BitReader& br)
+{
+    if (br.nbits < 1) br.refill();
+    const int b = static_cast<int>(br.peek(1));
+    br.skip(1);
+    return b;
+}
+
+inline int receive_bits(BitReader& br, int n)
+{
+    if (n == 0) return 0;
+    if (br.nbits < n) br.refill();
+    const int v = static_cast<int>(br.peek(n));
+    br.skip(n);
+    return v;
+}
+
+inline bool fits16(int v) { return v >= -32768 && v <= 32767; }
+
+// Progressive decoding procedures (T.81 G.1.2.1-G.1.2.3).  Coefficients are
+// kept in zigzag order, as the fused kernel takes them.
+struct ProgState {
+    int pred[3] = {0, 0, 0};
+    int eobrun = 0;
+};
+
+inline bool dc_first(BitReader& br, const HuffTable& dc, int& pred, int al, int16_t* blk)
+{
+    const int s = decode_symbol(br, dc);
+    if (s < 0 || s > 11) return false;
+    pred += receive_extend(br, s);
+    const int v = pred * (1 << al);
+    if (!fits16(v)) return false;
+    blk[0] = static_cast<int16_t>(v);
+    return true;
+}
+
+inline bool ac_first(BitReader& br, const HuffTable& ac, const ScanSpec& sc, int& eobrun, int16_t* blk)
+{
+    if (eobrun > 0) {
+        --eobrun;
+        return true;
+    }
+    for (int k = sc.ss; k <= sc.se;) {
+        const int rs = decode_symbol(br, ac);
+        if (rs < 0) return false;
+        const int r = rs >> 4, s = rs & 15;
+        if (s) {
+            k += r;
+            if (k > sc.se) return false;
+            const int v = receive_extend(br, s) * (1 << sc.al);
+            if (!fits16(v)) return false;
+            blk[k++] = static_cast<int16_t>(v);
+        } else if (r == 15) {
+            k += 16;   // ZRL
+        } else {       // EOBr: this block and (2^r - 1 + r bits) more end here
+            eobrun = (1 << r) - 1 + receive_bits(br, r);
+            break;
+        }
+    }
+    return true;
+}
+
+// Correction bit of an already-nonzero coefficient (G.1.2.3).
+inline void refine(BitReader& br, int16_t& coef, int p1)
+{
+    if (get_bit(br) && (coef & p1) == 0) coef = static_cast<int16_t>(coef >= 0 ? coef + p1 : coef - p1);
+}
+
+inline bool ac_refine(BitReader& br, const HuffTable& ac, const ScanSpec& sc, int& eobrun, int16_t* blk)
+{
+    const int p1 = 1 << sc.al;
+    int k = sc.ss;
+    if (eobrun == 0) {
+        for (; k <= sc.se; ++k) {
+            const int rs = decode_symbol(br, ac);
+            if (rs < 0) return false;
+            int r = rs >> 4;
+            const int s = rs & 15;
+            int val = 0;
+            if (s) {
+                if (s != 1) return false;   // a newly significant coefficient is +-1 << Al
+                val = get_bit(br) ? p1 : -p1;
+            } else if (r != 15) {
+                eobrun = (1 << r) + receive_bits(br, r);
+                break;                      // the EOB run starts with this block's remainder
+            }
+            // skip r still-zero coefficients (refining the nonzero ones passed
+            // on the way), then place val on the next zero one
+            for (; k <= sc.se; ++k) {
+                int16_t& coef = blk[k];
+                if (coef != 0)
+                    refine(br, coef, p1);
+                else if (--r < 0)
+                    break;
+            }
+            if (val) {
+                if (k > sc.se) return false;
+                blk[k] = static_cast<int16_t>(val);
+            }
+        }
+    }
+    if (eobrun > 0) {   // inside an EOB run: only correction bits for nonzero coefficients
+        for (; k <= sc.se; ++k)
+            if (blk[k] != 0) refine(br, blk[k], p1);
+        --eobrun;
+    }
+    return true;
+}
+
+// One scan of a multi-scan frame.  Returns HJD_OK and *end = the byte after
+// the scan's entropy-coded segment (the next marker).
+int decode_scan_any(const uint8_t* d, size_t n, const Frame& f, const CoefLayout& L, int16_t* coefs, size_t* end)
+{
+    const ScanSpec& sc = f.scan;
+    BitReader br{d + sc.offset, d + n};
+    ProgState st;
+    const bool prog = f.process == 2;
+    // interleaved scan: MCUs of the frame; non-interleaved: the component's blocks
+    const int c0 = sc.comp[0];
+    const int uw = sc.ns == 1 ? L.bw[c0] : L.mcu_w;
+    const int64_t units = sc.ns == 1 ? static_cast<int64_t>(L.bw[c0]) * L.bh[c0]
+                                     : static_cast<int64_t>(L.mcu_w) * L.mcu_h;
+    auto block = [&](int c, int16_t* blk) -> bool {
+        if (!prog) return decode_block(br, f.dc[f.comp[c].td], f.ac[f.comp[c].ta], st.pred[c], blk);
+        if (sc.ss == 0) {
+            if (sc.ah == 0) return dc_first(br, f.dc[f.comp[c].td], st.pred[c], sc.al, blk);
+            if (get_bit(br)) blk[0] = static_cast<int16_t>(blk[0] | (1 << sc.al));
+            return true;
+        }
+        return sc.ah == 0 ? ac_first(br, f.ac[f.comp[c].ta], sc, st.eobrun, blk)
+                          : ac_refine(br, f.ac[f.comp[c].ta], sc, st.eobrun, blk);
+    };
+    int restarts = 0, since = 0;
+    for (int64_t u = 0; u < units; ++u) {
+        if (f.restart_interval > 0 && since == f.restart_interval) {
+            if (!br.restart(restarts))
+                return set_error(HJD_E_INVALID, "expected RST%d before MCU %lld", restarts & 7, static_cast<long long>(u));
+            ++restarts;
+            since = 0;
+            st = ProgState();
+        }
+        ++since;
+        const int uy = static_cast<int>(u / uw), ux = static_cast<int>(u % uw);
+        bool ok = true;
+        if (sc.ns == 1) {
+            ok = block(c0, L.at(coefs, c0, uy, ux));
+        } else {
+            for (int si = 0; si < sc.ns && ok; ++si) {
+                const int c = sc.comp[si];
+                for (int yy = 0; yy < L.vs[c] && ok; ++yy)
+                    for (int xx = 0; xx < L.hs[c] && ok; ++xx)
+                        ok = block(c, L.at(coefs, c, uy * L.vs[c] + yy, ux * L.hs[c] + xx));
+            }
+        }
+        if (!ok) return set_error(HJD_E_INVALID, "corrupt entropy data in MCU %lld", static_cast<long long>(u));
+    }
+    // next marker: the reader stops in front of one, or is short of it by the
+    // bytes it has not needed yet (entropy data: 0xFF only as FF00 / RSTn)
+    const uint8_t* q = br.p;
+    while (q + 1 < d + n && !(q[0] == 0xFF && q[1] != 0x00 && (q[1] < 0xD0 || q[1] > 0xD7))) ++q;
+    *end = static_cast<size_t>(q - d);
+    return HJD_OK;
+}
+
+int decode_multiscan(const uint8_t* d, size_t n, Frame& f, hjd_jpeg_info* info, int16_t* coefs)
+{
+    memset(coefs, 0, static_cast<size_t>(info->nblocks) * 64 * sizeof(int16_t));
+    const CoefLayout L(f, *info);
+    bool latched[3] = {false, false, false};
+    for (;;) {
+        for (int i = 0; i < f.scan.ns; ++i) {   // quantisation tables latch at a component's first scan
+            const int c = f.scan.comp[i];
+            if (!latched[c]) {
+                memcpy(info->qt[c], f.qt[f.comp[c].tq], sizeof(info->qt[c]));
+                info->qt_precision[c] = f.qt_prec[f.comp[c].tq];
+                latched[c] = true;
+            }
+        }
+        size_t p = 0;
+        int rc = decode_scan_any(d, n, f, L, coefs, &p);
+        if (rc) return rc;
+        bool eoi = false;
+        rc = parse_segments(d, n, &p, f, true, &eoi);
+        if (rc) return rc;
+        if (eoi) break;
+    }
+    if (f.ncomp == 1) {   // gray: the Y table in all three slots, as fill_info()
+        memcpy(info->qt[1], info->qt[0], sizeof(info->qt[0]));
+        memcpy(info->qt[2], info->qt[0], sizeof(info->qt[0]));
+        info->qt_precision[1] = info->qt_precision[2] = info->qt_precision[0];
+    }
+    return HJD_OK;
+}
+
 int decode_one(const uint8_t* data, size_t size, hjd_jpeg_info* info, int16_t* coefs, int64_t capacity)
 {
     if (!data || !info) return set_error(HJD_E_INVALID, "NULL argument");
@@ -367,7 +678,8 @@ int decode_one(const uint8_t* data, size_t size, hjd_jpeg_info* info, int16_t* c
     if (capacity < info->nblocks)
         return set_error(HJD_E_INVALID, "capacity %lld < %lld blocks", static_cast<long long>(capacity),
                          static_cast<long long>(info->nblocks));
-    return decode_scan(data, size, f, *info, coefs);
+    if (single_scan(f)) return decode_scan(data, size, f, *info, coefs);
+    return decode_multiscan(data, size, f, info, coefs);
 }
 
 }  // namespace
@@ -378,6 +690,10 @@ int hjd_internal::parse_scan_header(const uint8_t* data, size_t size, ScanHeader
     Frame f;
     int rc = parse(data, size, f);
     if (rc) return rc;
+    if (!single_scan(f))
+        return set_error(HJD_E_INVALID, "%s JPEG: the GPU entropy decoder takes one interleaved sequential scan "
+                         "(decode it with the host decoder, hjd_jpeg_decode_coefs / hjd_stream)",
+                         f.process == 2 ? "progressive" : "multi-scan");
     hjd_jpeg_info info;
     fill_info(f, &info);
     h->width = f.width;

@@ -37,11 +37,14 @@ class JpegInfo:
     qt: np.ndarray            # [3][64] file (zigzag) order, per component
     qt_precision: tuple
     scan_offset: int
+    process: int = 0          # 0 baseline, 1 extended sequential, 2 progressive
+    single_scan: bool = True  # one interleaved sequential scan (GPU entropy decodable)
 
     @classmethod
     def from_c(cls, c: HjdJpegInfo) -> "JpegInfo":
         return cls(c.width, c.height, c.sampling, c.restart_interval, c.mcu_w, c.mcu_h, c.nblocks,
-                   np.array(c.qt, dtype=np.int32), tuple(c.qt_precision), c.scan_offset)
+                   np.array(c.qt, dtype=np.int32), tuple(c.qt_precision), c.scan_offset,
+                   c.process, bool(c.single_scan))
 
 
 def _buf(data: bytes):

@@ -317,3 +317,16 @@ def test_random_sweep_on_device(hjd, ctx, sub_bits):
             ref, _ = hjd.decode_coefs(d)
             np.testing.assert_array_equal(g, ref, err_msg=f"file {k + i} S={sub_bits}")
         assert all(s & ~1 == 0 for s in status)
+
+
+def test_progressive_rejected_loudly(hjd, ctx):
+    """The device decoder takes one interleaved sequential scan; a progressive
+    file is refused with a message naming the host path (no silent fallback)."""
+    import torch
+    prog = _pil(64, 48, 90, 2, seed=3, progressive=True)
+    info = hjd.parse(prog)
+    assert info.process == 2 and not info.single_scan
+    coefs = torch.zeros((info.nblocks, 64), dtype=torch.int16, device="cuda")
+    with hjd.GpuDecoder(ctx, 1, len(prog), info.nblocks) as gd:
+        with pytest.raises(hjd._lib.HjdError, match="host decoder"):
+            gd.decode_coefs([prog], coefs)

@@ -77,8 +77,10 @@ def test_rejects_unsupported(lib):
     import io
     from PIL import Image
     img = Image.fromarray(np.zeros((16, 16, 3), np.uint8))
-    b = io.BytesIO(); img.save(b, format="JPEG", progressive=True)
-    assert decode(lib, b.getvalue())[0] != 0            # progressive: SOF2
+    b = io.BytesIO(); img.save(b, format="JPEG")
+    data = bytearray(b.getvalue())
+    data[data.index(b"\xff\xc0") + 1] = 0xC3               # lossless (SOF3); progressive: test_jpeg_multiscan.py
+    assert decode(lib, bytes(data))[0] != 0
     # 4:4:0 (Y H1V2): patch the luma sampling byte of a 4:2:2 file's SOF0
     b = io.BytesIO(); img.save(b, format="JPEG", subsampling=1)
     data = bytearray(b.getvalue())

@@ -85,3 +85,34 @@ def test_4k_jpeg_end_to_end(hjd, ctx):
     out = hjd.decode_jpeg(ctx, data)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), O.decode_q16(coefs, info.qt, 3840, 2160, 1))
+
+
+def test_progressive_and_multiscan_files(hjd, ctx):
+    """Progressive (SOF2) and multi-scan sequential files go through the host
+    decoder into the same fused kernel: decode_jpeg and the stream pipeline
+    give exactly the pixels of the baseline file with the same coefficients
+    (tests/test_jpeg_multiscan.py pins the coefficients)."""
+    import torch
+    import jpeg_writer as JW
+    files = []
+    for i, (w, h, sub, kw) in enumerate([(333, 177, 2, {}), (96, 64, 0, {"restart_marker_blocks": 3}),
+                                         (200, 120, 1, {}), (1, 1, 2, {})]):
+        base = _pil(w, h, 85, sub, seed=40 + i, **kw)
+        prog = _pil(w, h, 85, sub, seed=40 + i, progressive=True, **kw)
+        c0, i0 = hjd.decode_coefs(base)
+        exp = O.decode_q16(c0, i0.qt, w, h, i0.sampling)
+        files += [(base, exp), (prog, exp)]
+        ms, _ = JW.rewrite_scans(base, c0, [(0,), (2,), (1,)], 4)
+        files.append((ms, exp))
+    for d, e in files:
+        out = hjd.decode_jpeg(ctx, d)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), e)
+    max_blocks = max(hjd.parse(d).nblocks for d, _ in files)
+    outs = [torch.full(e.shape, -1, dtype=torch.int32, device="cuda") for _, e in files]
+    with hjd.JpegStream(ctx, max_blocks, nslots=3, nthreads=4) as st:
+        for (d, _), o in zip(files, outs):
+            st.submit(d, o)
+        st.sync()
+    for (d, e), o in zip(files, outs):
+        np.testing.assert_array_equal(o.cpu().numpy().view(np.uint32), e)
