@@ -49,6 +49,10 @@ WORKLOADS = {
                   desc="extension (SURVEY s8(f) rank 4): batch of 1024 synthetic 3840x2160 4:2:2 frames"),
     "4kgray": dict(width=3840, height=2160, sampling=4, frames=1024,
                    desc="extension (SURVEY s8(f) rank 4): batch of 1024 synthetic 3840x2160 grayscale frames"),
+    "4k411": dict(width=3840, height=2160, sampling=5, frames=1024,
+                  desc="extension: batch of 1024 synthetic 3840x2160 4:1:1 (Y H4V1) frames"),
+    "4k440": dict(width=3840, height=2160, sampling=6, frames=1024,
+                  desc="extension: batch of 1024 synthetic 3840x2160 4:4:0 (Y H1V2) frames"),
     "4k420_bgr24": dict(width=3840, height=2160, sampling=1, frames=1024, out_format=1,
                         desc="extension (SURVEY s8(f) rank 4): configs[2] with 3-byte BGR24 output (24-bpp BMP "
                              "rows) instead of BGRX"),
@@ -93,7 +97,7 @@ ZIGZAG = [0, 1, 8, 16, 9, 2, 3, 10, 17, 24, 32, 25, 18, 11, 4, 5,
           58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63]
 
 
-SAMPLING_NAMES = {0: "4:4:4", 1: "4:2:0", 3: "4:2:2", 4: "gray"}
+SAMPLING_NAMES = {0: "4:4:4", 1: "4:2:0", 3: "4:2:2", 4: "gray", 5: "4:1:1", 6: "4:4:0"}
 
 
 def synth_frame_gpu(torch, nblk, sampling, qt, seed, device):

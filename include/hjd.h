@@ -41,8 +41,13 @@ enum hjd_status {
  * are extensions the reference rejects (src/decoder.cpp:58-69; SURVEY.md
  * s8(f) rank 4): the same IDCT and the same colour arithmetic with nearest
  * (horizontal) chroma replication, and R = G = B = clamp(Y + 128) for gray
- * (the reference's formula with U = V = 0). */
-enum hjd_sampling { HJD_YUV444 = 0, HJD_YUV420 = 1, HJD_OTHER = 2, HJD_YUV422 = 3, HJD_GRAY = 4 };
+ * (the reference's formula with U = V = 0).  HJD_YUV411_H4V1 (true 4:1:1:
+ * Y H4V1, chroma H1V1; not the reference's "YUV411", which is H2V2) and
+ * HJD_YUV440 (Y H1V2) are further extensions with nearest replication along
+ * the subsampled axis. */
+enum hjd_sampling {
+    HJD_YUV444 = 0, HJD_YUV420 = 1, HJD_OTHER = 2, HJD_YUV422 = 3, HJD_GRAY = 4, HJD_YUV411_H4V1 = 5, HJD_YUV440 = 6
+};
 
 /* Output pixel format. */
 enum hjd_out_format {

@@ -21,8 +21,10 @@ from .backend import (  # noqa: E402
     OUT_BGRX,
     OUT_BYTES,
     GRAY,
+    YUV411_H4V1,
     YUV420,
     YUV422,
+    YUV440,
     YUV444,
     block_components,
     Context,
@@ -43,5 +45,5 @@ __all__ = [
     "decode_coefs_batch", "decode_jpeg", "emulate_entropy",
     "parse",
     "Context", "FrameSpec", "Plan", "decode_frame", "device_count", "frame_blocks", "mcu_geometry",
-    "YUV444", "YUV420", "YUV422", "GRAY", "OTHER", "block_components", "KERNEL_AUTO", "KERNEL_PERSISTENT", "KERNEL_LATENCY", "OUT_BGRX", "OUT_BGR24", "OUT_BYTES", "default_pitch", "IN_Q16_ZIGZAG", "IN_I32_NATURAL",
+    "YUV444", "YUV420", "YUV422", "GRAY", "YUV411_H4V1", "YUV440", "OTHER", "block_components", "KERNEL_AUTO", "KERNEL_PERSISTENT", "KERNEL_LATENCY", "OUT_BGRX", "OUT_BGR24", "OUT_BYTES", "default_pitch", "IN_Q16_ZIGZAG", "IN_I32_NATURAL",
 ]

@@ -19,9 +19,12 @@ YUV420 = 1  # == the reference's ColorSpace::YUV411 (src/macro.h:114-119), H2V2
 OTHER = 2
 YUV422 = 3  # extension (Y H2V1), include/hjd.h
 GRAY = 4    # extension (one component), include/hjd.h
+YUV411_H4V1 = 5  # extension (Y H4V1: true 4:1:1, not the reference's "YUV411"), include/hjd.h
+YUV440 = 6  # extension (Y H1V2), include/hjd.h
 
 # sampling -> (MCU px width, MCU px height, blocks per MCU, luma blocks per MCU)
-_GEOM = {YUV444: (8, 8, 3, 1), YUV420: (16, 16, 6, 4), YUV422: (16, 8, 4, 2), GRAY: (8, 8, 1, 1)}
+_GEOM = {YUV444: (8, 8, 3, 1), YUV420: (16, 16, 6, 4), YUV422: (16, 8, 4, 2), GRAY: (8, 8, 1, 1),
+         YUV411_H4V1: (32, 8, 6, 4), YUV440: (8, 16, 4, 2)}
 
 IN_Q16_ZIGZAG = 0
 IN_I32_NATURAL = 1

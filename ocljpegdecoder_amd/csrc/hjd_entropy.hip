@@ -767,8 +767,9 @@ struct hjd_gdec {
     int assemble(uint8_t* blob, int16_t* coefs, int64_t* block_offsets, void* const* d_outs, const int32_t* pitches,
                  EntBatchDev& d);
     // pixel-kernel launch groups, one per sampling (hjd_internal::SamplingGeom::index)
-    static constexpr int kClasses = 4;
-    static constexpr int kClassSampling[kClasses] = {HJD_YUV444, HJD_YUV420, HJD_YUV422, HJD_GRAY};
+    static constexpr int kClasses = 6;
+    static constexpr int kClassSampling[kClasses] = {HJD_YUV444, HJD_YUV420,      HJD_YUV422,
+                                                     HJD_GRAY,   HJD_YUV411_H4V1, HJD_YUV440};
     int nrec[kClasses] = {};
     int64_t tasks[kClasses] = {};
     uint8_t* out_base[kClasses] = {};

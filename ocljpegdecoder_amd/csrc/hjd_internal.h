@@ -15,7 +15,7 @@ int set_error(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3
 // Per-sampling geometry shared by the parser, the plans and the kernels.  A
 // pixel-kernel task is always 48 coefficient blocks (hjd::kTaskBlocks).
 struct SamplingGeom {
-    int index;          // kernel template index: 0 4:4:4, 1 4:2:0, 2 4:2:2, 3 gray
+    int index;          // kernel template index: 0 4:4:4, 1 4:2:0, 2 4:2:2, 3 gray, 4 4:1:1, 5 4:4:0
     int mcu_px_w, mcu_px_h;
     int bpm;            // blocks per MCU
     int mcus_per_task;  // 48 / bpm
@@ -27,6 +27,8 @@ inline bool sampling_geom(int sampling, SamplingGeom* g)
     case 1: *g = {1, 16, 16, 6, 8}; return true;   // HJD_YUV420
     case 3: *g = {2, 16, 8, 4, 12}; return true;   // HJD_YUV422
     case 4: *g = {3, 8, 8, 1, 48}; return true;    // HJD_GRAY
+    case 5: *g = {4, 32, 8, 6, 8}; return true;    // HJD_YUV411_H4V1
+    case 6: *g = {5, 8, 16, 4, 12}; return true;   // HJD_YUV440
     default: return false;
     }
 }

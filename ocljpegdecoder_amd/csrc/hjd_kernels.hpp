@@ -123,12 +123,14 @@ __device__ __forceinline__ void cursor_seek(FrameCursor& c, const FrameDev* __re
 }
 
 // Compile-time geometry of the kernel's sampling index (hjd_internal::
-// sampling_geom): 0 4:4:4, 1 4:2:0, 2 4:2:2 (extension), 3 gray (extension).
+// sampling_geom): 0 4:4:4, 1 4:2:0, 2 4:2:2 (extension), 3 gray (extension),
+// 4 4:1:1 = Y H4V1 (extension), 5 4:4:0 = Y H1V2 (extension).
 template <int kSampling>
 struct KGeom {
-    static constexpr int kBpm = kSampling == 0 ? 3 : kSampling == 1 ? 6 : kSampling == 2 ? 4 : 1;
-    static constexpr int kMcuW = kSampling == 0 || kSampling == 3 ? 8 : 16;   // MCU pixels
-    static constexpr int kMcuH = kSampling == 1 ? 16 : 8;
+    static constexpr int kBpm = kSampling == 0 ? 3 : kSampling == 1 || kSampling == 4 ? 6
+                              : kSampling == 2 || kSampling == 5 ? 4 : 1;
+    static constexpr int kMcuW = kSampling == 4 ? 32 : kSampling == 1 || kSampling == 2 ? 16 : 8;   // MCU pixels
+    static constexpr int kMcuH = kSampling == 1 || kSampling == 5 ? 16 : 8;
     static constexpr int kMcus = kTaskBlocks / kBpm;                          // MCUs per task
     static constexpr int kStripW = kMcus * kMcuW;                            // strip pixels
     static_assert(kMcus * kBpm == kTaskBlocks, "a task is 48 whole MCUs' blocks");
@@ -372,6 +374,70 @@ __device__ __forceinline__ void colour_stage(const char* __restrict__ slots, int
                     emit_row4<false, kVariant, kFull>(strip, lo, xu, width, sy.x, sy.y, p0, p1, &c0, &c0, &c1, &c1);
             }
         }
+    } else if constexpr (kSampling == 4) {
+        // 4:1:1 (extension, Y H4V1): 256x8 strip of 8 MCUs (Y0-Y3 Cb Cr,
+        // 32x8 px); units of 4 px x 1 row, 64 per row (one per lane), 8 rows;
+        // each chroma sample serves 4 horizontally adjacent pixels (nearest
+        // replication).
+        (void)loff;
+#pragma unroll 2
+        for (int k = 0; k < (8 + kStride - 1) / kStride; ++k) {
+            const int y = u0 + k * kStride;   // row of the strip
+            if (kStride > 1 && y >= 8) break;
+            const int m = lane >> 3;
+            const int xm = (lane & 7) * 4;    // x within MCU: 0..28
+            const int2 sy = *reinterpret_cast<const int2*>(slots + (6 * m + (xm >> 3)) * kSlotBytes + y * 16 +
+                                                           (xm & 7) * 2);
+            const int coff = y * 16 + (xm >> 2) * 2;
+            const uint32_t cu = *reinterpret_cast<const unsigned short*>(slots + (6 * m + 4) * kSlotBytes + coff);
+            const uint32_t cv = *reinterpret_cast<const unsigned short*>(slots + (6 * m + 5) * kSlotBytes + coff);
+            const ChromaTerms c0 = chroma_terms<0>(cu, cv);
+            const ChromaPair p0 = pair_of(c0, c0);
+            const uint32_t lo = static_cast<uint32_t>(y) * static_cast<uint32_t>(pitch) +
+                                static_cast<uint32_t>(lane * 4 * kPx);
+            const int xu = x_base + lane * 4;
+            if (kFull || y_base + y < height) {
+                if (__builtin_amdgcn_ballot_w64(p0.flagged != 0))
+                    emit_row4<true, kVariant, kFull>(strip, lo, xu, width, sy.x, sy.y, p0, p0, &c0, &c0, &c0, &c0);
+                else
+                    emit_row4<false, kVariant, kFull>(strip, lo, xu, width, sy.x, sy.y, p0, p0, &c0, &c0, &c0, &c0);
+            }
+        }
+    } else if constexpr (kSampling == 5) {
+        // 4:4:0 (extension, Y H1V2): 96x16 strip of 12 MCUs (Y0 above Y1, Cb,
+        // Cr; 8x16 px); units of 4 px x 1 row, 24 per row, 6 per lane; each
+        // chroma row serves 2 vertically adjacent pixel rows.
+        (void)loff;
+#pragma unroll 2
+        for (int k = 0; k < (6 + kStride - 1) / kStride; ++k) {
+            const int it = u0 + k * kStride;
+            if (kStride > 1 && it >= 6) break;
+            const int u = it * 64 + lane;
+            const int y = u / 24;
+            const int cu4 = u - y * 24;       // unit within the row
+            const int m = cu4 >> 1;
+            const int xm = (cu4 & 1) * 4;     // x within MCU: 0 or 4
+            const int2 sy = *reinterpret_cast<const int2*>(slots + (4 * m + (y >> 3)) * kSlotBytes + (y & 7) * 16 +
+                                                           xm * 2);
+            const int coff = (y >> 1) * 16 + xm * 2;
+            const uint2 su = *reinterpret_cast<const uint2*>(slots + (4 * m + 2) * kSlotBytes + coff);
+            const uint2 sv = *reinterpret_cast<const uint2*>(slots + (4 * m + 3) * kSlotBytes + coff);
+            const ChromaTerms c0 = chroma_terms<0>(su.x, sv.x);
+            const ChromaTerms c1 = chroma_terms<1>(su.x, sv.x);
+            const ChromaTerms c2 = chroma_terms<0>(su.y, sv.y);
+            const ChromaTerms c3 = chroma_terms<1>(su.y, sv.y);
+            const ChromaPair p01 = pair_of(c0, c1), p23 = pair_of(c2, c3);
+            const uint32_t lo = static_cast<uint32_t>(y) * static_cast<uint32_t>(pitch) +
+                                static_cast<uint32_t>(cu4 * 4 * kPx);
+            const int xu = x_base + cu4 * 4;
+            if (kFull || y_base + y < height) {
+                if (__builtin_amdgcn_ballot_w64((p01.flagged | p23.flagged) != 0))
+                    emit_row4<true, kVariant, kFull>(strip, lo, xu, width, sy.x, sy.y, p01, p23, &c0, &c1, &c2, &c3);
+                else
+                    emit_row4<false, kVariant, kFull>(strip, lo, xu, width, sy.x, sy.y, p01, p23, &c0, &c1, &c2,
+                                                      &c3);
+            }
+        }
     } else {
         // gray (extension): 384x8 strip of 48 one-block MCUs; units of 4 px x
         // 1 row, 96 per row, 12 per lane; R = G = B = clamp(Y + 128), the
@@ -402,7 +468,12 @@ __device__ __forceinline__ void colour_stage(const char* __restrict__ slots, int
 // and luma level shift): 4:4:4 / 4:2:0 / gray blocks are MCU-interleaved with
 // a period dividing 6, so 6g + i works; 4:2:2 MCUs are (Y0, Y1, Cb, Cr), so
 // rounds 0-2 take the 24 luma blocks, rounds 3-5 the 12 Cb then 12 Cr blocks.
-template <int kSampling>
+// The IDCT rounds depend only on the MCU's block order: 4:1:1 MCUs (Y0-Y3,
+// Cb, Cr) are transformed like 4:2:0 ones, 4:4:0 MCUs (Y0, Y1, Cb, Cr) like
+// 4:2:2 ones.
+constexpr int round_class(int s) { return s == 4 ? 1 : s == 5 ? 2 : s; }
+
+template <int kSampling0, int kSampling = round_class(kSampling0)>
 __device__ __forceinline__ int round_block(int i, int g)
 {
     if constexpr (kSampling == 2) {
@@ -419,7 +490,7 @@ __device__ __forceinline__ int round_block(int i, int g)
 
 // Component (0 = Y, 1 = Cb, 2 = Cr) of round i's blocks; -1 where it differs
 // between lane groups (4:2:2 round 4: groups 0-3 Cb, 4-7 Cr).
-template <int kSampling>
+template <int kSampling0, int kSampling = round_class(kSampling0)>
 __device__ __forceinline__ constexpr int round_component(int i)
 {
     return kSampling == 1 ? (i < 4 ? 0 : i - 3)
@@ -429,7 +500,7 @@ __device__ __forceinline__ constexpr int round_component(int i)
 }
 
 // Component (0 = Y, 1 = Cb, 2 = Cr) of task-local block b (MCU-major).
-template <int kSampling>
+template <int kSampling0, int kSampling = round_class(kSampling0)>
 __device__ __forceinline__ int block_component(int b)
 {
     if constexpr (kSampling == 0) {
@@ -446,7 +517,7 @@ __device__ __forceinline__ int block_component(int b)
 }
 
 // Round i transforms luma blocks (runtime form of round_component(i) == 0).
-template <int kSampling>
+template <int kSampling0, int kSampling = round_class(kSampling0)>
 __device__ __forceinline__ bool round_is_luma(int i)
 {
     return kSampling == 1 ? i < 4 : kSampling == 0 ? i % 3 == 0 : kSampling == 2 ? i < 3 : true;

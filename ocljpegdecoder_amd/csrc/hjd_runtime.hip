@@ -148,11 +148,13 @@ int hjd_internal::launch_decode(int device, int num_cu, int sampling, int input_
 #define HJD_KL(V) hjd::decode_kernel_lat<0, 0, V>, hjd::decode_kernel_lat<0, 1, V>, \
                   hjd::decode_kernel_lat<1, 0, V>, hjd::decode_kernel_lat<1, 1, V>, \
                   hjd::decode_kernel_lat<2, 0, V>, hjd::decode_kernel_lat<2, 1, V>, \
-                  hjd::decode_kernel_lat<3, 0, V>, hjd::decode_kernel_lat<3, 1, V>
-        static const K kLat[16] = {HJD_KL(0), HJD_KL(hjd::kOutBgr24)};
+                  hjd::decode_kernel_lat<3, 0, V>, hjd::decode_kernel_lat<3, 1, V>, \
+                  hjd::decode_kernel_lat<4, 0, V>, hjd::decode_kernel_lat<4, 1, V>, \
+                  hjd::decode_kernel_lat<5, 0, V>, hjd::decode_kernel_lat<5, 1, V>
+        static const K kLat[24] = {HJD_KL(0), HJD_KL(hjd::kOutBgr24)};
 #undef HJD_KL
         if (tasks > (int64_t(1) << 31) - 1) return set_error(HJD_E_INVALID, "too many tasks for the latency kernel");
-        const K k = kLat[(out_format == HJD_OUT_BGR24 ? 8 : 0) | (sg.index << 1) | fmt];
+        const K k = kLat[(out_format == HJD_OUT_BGR24 ? 12 : 0) + ((sg.index << 1) | fmt)];
         hipLaunchKernelGGL(k, dim3(static_cast<uint32_t>(tasks)), dim3(hjd::kLatThreads), 0,
                            static_cast<hipStream_t>(stream), d_coefs, d_qt_nat,
                            reinterpret_cast<const FrameDev*>(d_frames), nframes, tasks, static_cast<uint8_t*>(d_out));
@@ -160,11 +162,13 @@ int hjd_internal::launch_decode(int device, int num_cu, int sampling, int input_
         return HJD_OK;
     }
     if (out_format == HJD_OUT_BGR24) {   // [sampling index][input format], default variant
-        static const K kTable24[8] = {
+        static const K kTable24[12] = {
             hjd::decode_kernel<0, 0, hjd::kOutBgr24>, hjd::decode_kernel<0, 1, hjd::kOutBgr24>,
             hjd::decode_kernel<1, 0, hjd::kOutBgr24>, hjd::decode_kernel<1, 1, hjd::kOutBgr24>,
             hjd::decode_kernel<2, 0, hjd::kOutBgr24>, hjd::decode_kernel<2, 1, hjd::kOutBgr24>,
-            hjd::decode_kernel<3, 0, hjd::kOutBgr24>, hjd::decode_kernel<3, 1, hjd::kOutBgr24>};
+            hjd::decode_kernel<3, 0, hjd::kOutBgr24>, hjd::decode_kernel<3, 1, hjd::kOutBgr24>,
+            hjd::decode_kernel<4, 0, hjd::kOutBgr24>, hjd::decode_kernel<4, 1, hjd::kOutBgr24>,
+            hjd::decode_kernel<5, 0, hjd::kOutBgr24>, hjd::decode_kernel<5, 1, hjd::kOutBgr24>};
         if (variant != 0) return set_error(HJD_E_INVALID, "kernel variants are BGRX-only");
         hipLaunchKernelGGL(kTable24[(sg.index << 1) | fmt], dim3(grid), dim3(hjd::kGroupThreads), 0,
                            static_cast<hipStream_t>(stream), d_coefs, d_qt_nat,
@@ -196,8 +200,9 @@ int hjd_internal::launch_decode(int device, int num_cu, int sampling, int input_
     const int key = (sg.index << 3) | (fmt << 2) | (variant & 3);
 #define HJD_K4(S, F) hjd::decode_kernel<S, F, 0>, hjd::decode_kernel<S, F, 1>, hjd::decode_kernel<S, F, 2>, \
                      hjd::decode_kernel<S, F, 3>
-    static const K kTable[32] = {HJD_K4(0, 0), HJD_K4(0, 1), HJD_K4(1, 0), HJD_K4(1, 1),
-                                 HJD_K4(2, 0), HJD_K4(2, 1), HJD_K4(3, 0), HJD_K4(3, 1)};
+    static const K kTable[48] = {HJD_K4(0, 0), HJD_K4(0, 1), HJD_K4(1, 0), HJD_K4(1, 1),
+                                 HJD_K4(2, 0), HJD_K4(2, 1), HJD_K4(3, 0), HJD_K4(3, 1),
+                                 HJD_K4(4, 0), HJD_K4(4, 1), HJD_K4(5, 0), HJD_K4(5, 1)};
 #undef HJD_K4
     hipLaunchKernelGGL(kTable[key], dim3(grid), dim3(hjd::kGroupThreads), 0, static_cast<hipStream_t>(stream),
                        d_coefs, d_qt_nat, reinterpret_cast<const FrameDev*>(d_frames), nframes, tasks,
@@ -259,7 +264,8 @@ static int geometry(int width, int height, int sampling, int& mcu_w, int& mcu_h,
         return fail(HJD_E_INVALID, "invalid dimensions %dx%d", width, height);
     SamplingGeom g;
     if (!sampling_geom(sampling, &g))
-        return fail(HJD_E_INVALID, "unsupported sampling %d (4:4:4, 4:2:0, 4:2:2 or gray)", sampling);
+        return fail(HJD_E_INVALID, "unsupported sampling %d (4:4:4, 4:2:0, 4:2:2, gray, 4:1:1 or 4:4:0)",
+                    sampling);
     bpm = g.bpm;
     tasks_mcus = g.mcus_per_task;
     mcu_w = (width - 1) / g.mcu_px_w + 1;   // src/decoder.cpp:189-190

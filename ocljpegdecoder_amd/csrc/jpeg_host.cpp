@@ -125,8 +125,12 @@ int parse_sof(const uint8_t* s, int sl, int marker, Frame& f)
         f.sampling = HJD_YUV444;
     else if (chroma11 && c[0].h == 2 && c[0].v == 1)
         f.sampling = HJD_YUV422;
+    else if (chroma11 && c[0].h == 4 && c[0].v == 1)
+        f.sampling = HJD_YUV411_H4V1;
+    else if (chroma11 && c[0].h == 1 && c[0].v == 2)
+        f.sampling = HJD_YUV440;
     else
-        return set_error(HJD_E_INVALID, "unsupported sampling (4:2:0, 4:4:4, 4:2:2 or gray)");
+        return set_error(HJD_E_INVALID, "unsupported sampling (4:2:0, 4:4:4, 4:2:2, 4:1:1, 4:4:0 or gray)");
     return HJD_OK;
 }
 

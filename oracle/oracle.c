@@ -162,6 +162,32 @@ static void put_mcu(const int32_t (*m)[64], int sampling, int mx, int my, int wi
                 out[(int64_t)py * pitch + px] = oracle_yuv_to_bgrx(Y, m[2][c], m[3][c]);
             }
         }
+    } else if (sampling == ORACLE_YUV411_H4V1) {
+        /* extension: 32x8 MCU (Y0..Y3 side by side), one chroma sample per 4 px */
+        for (y = 0; y < 8; y++) {
+            int py = my * 8 + y;
+            if (py >= height) break;
+            for (x = 0; x < 32; x++) {
+                int px = mx * 32 + x;
+                if (px >= width) break;
+                int Y = m[x >> 3][(y << 3) | (x & 7)];
+                int c = (y << 3) + (x >> 2);
+                out[(int64_t)py * pitch + px] = oracle_yuv_to_bgrx(Y, m[4][c], m[5][c]);
+            }
+        }
+    } else if (sampling == ORACLE_YUV440) {
+        /* extension: 8x16 MCU (Y0 above Y1), one chroma row per 2 pixel rows */
+        for (y = 0; y < 16; y++) {
+            int py = my * 16 + y;
+            if (py >= height) break;
+            for (x = 0; x < 8; x++) {
+                int px = mx * 8 + x;
+                if (px >= width) break;
+                int Y = m[y >> 3][((y & 7) << 3) | x];
+                int c = ((y >> 1) << 3) + x;
+                out[(int64_t)py * pitch + px] = oracle_yuv_to_bgrx(Y, m[2][c], m[3][c]);
+            }
+        }
     } else if (sampling == ORACLE_GRAY) {
         /* extension: one component, the reference's conversion with U = V = 0 */
         for (y = 0; y < 8; y++) {
@@ -197,6 +223,8 @@ static int frame_geometry(int width, int height, int sampling, int* mcw, int* mc
     case ORACLE_YUV420: mw = 16; mh = 16; *bpm = 6; *nluma = 4; break;
     case ORACLE_YUV422: mw = 16; mh = 8; *bpm = 4; *nluma = 2; break;
     case ORACLE_GRAY: mw = 8; mh = 8; *bpm = 1; *nluma = 1; break;
+    case ORACLE_YUV411_H4V1: mw = 32; mh = 8; *bpm = 6; *nluma = 4; break;
+    case ORACLE_YUV440: mw = 8; mh = 16; *bpm = 4; *nluma = 2; break;
     default: return -1;
     }
     *mcw = (width - 1) / mw + 1; /* decoder.cpp:189-190 */

@@ -44,8 +44,12 @@ void oracle_yuv_to_bgrx_n(const int32_t* y, const int32_t* u, const int32_t* v, 
  * same IDCT and colour arithmetic with nearest horizontal chroma replication,
  * gray as the conversion with U = V = 0.  Parity for them is unpinned by the
  * reference (it has no such path); tests pin the HIP path to this
- * restatement. */
-enum { ORACLE_YUV444 = 0, ORACLE_YUV420 = 1, ORACLE_YUV422 = 3, ORACLE_GRAY = 4 };
+ * restatement.  ORACLE_YUV411_H4V1 (Y H4V1) and ORACLE_YUV440 (Y H1V2) likewise,
+ * with nearest replication along the subsampled axis. */
+enum {
+    ORACLE_YUV444 = 0, ORACLE_YUV420 = 1, ORACLE_YUV422 = 3, ORACLE_GRAY = 4, ORACLE_YUV411_H4V1 = 5,
+    ORACLE_YUV440 = 6
+};
 
 /*
  * Whole frame from int16 quantised zigzag coefficients, MCU-major

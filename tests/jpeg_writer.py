@@ -85,17 +85,7 @@ def _encode_block(bw, blk, pred, dct, act):
     return int(blk[0])
 
 
-def rewrite_scans(data: bytes, coefs: np.ndarray, scans, restart_interval=0):
-    """scans: list of tuples of frame component indices, e.g. [(0,), (1, 2)].
-    coefs: the source's coefficients (MCU-major, zigzag) from the decoder under
-    test's baseline path, which the tests pin against the reference.
-    Returns (jpeg bytes, expected coefficients): a non-interleaved scan codes
-    only the component's own block grid (T.81 A.2.2), so MCU-padding blocks
-    outside it are expected as zeros (they lie wholly outside the image)."""
-    segs = _segments(data)
-    sof = next(p for m, p in segs if m in (0xC0, 0xC1))
-    h, w, nc = (sof[1] << 8) | sof[2], (sof[3] << 8) | sof[4], sof[5]
-    comps = [(sof[6 + 3 * c], sof[7 + 3 * c] >> 4, sof[7 + 3 * c] & 15) for c in range(nc)]
+def _dht_codes(segs):
     dht = {}
     for m, p in segs:
         if m != 0xC4:
@@ -107,15 +97,12 @@ def rewrite_scans(data: bytes, coefs: np.ndarray, scans, restart_interval=0):
             n = sum(counts)
             dht[(tc, th)] = _codes(counts, list(p[q + 17:q + 17 + n]))
             q += 17 + n
-    # table ids of each component: copy the source's first SOS
-    p = 2
-    while not (data[p] == 0xFF and data[p + 1] == 0xDA):
-        p += 2 + ((data[p + 2] << 8) | data[p + 3])
-    ns0 = data[p + 4]
-    tabs = {}
-    for i in range(ns0):
-        cid, t = data[p + 5 + 2 * i], data[p + 6 + 2 * i]
-        tabs[[c[0] for c in comps].index(cid)] = (t >> 4, t & 15)
+    return dht
+
+
+def _emit(header, comps, tabs, dht, w, h, coefs, scans, restart_interval):
+    """SOI + header segments + DRI + the scans + EOI; returns (bytes, expect)."""
+    nc = len(comps)
     # geometry (T.81 A.2): MCU-major layout of the coefficients
     hmax, vmax = max(c[1] for c in comps), max(c[2] for c in comps)
     if nc == 1:
@@ -134,9 +121,7 @@ def rewrite_scans(data: bytes, coefs: np.ndarray, scans, restart_interval=0):
         return blocks[(by // vs[c]) * mcu_w + bx // hs[c], base[c] + (by % vs[c]) * hs[c] + bx % hs[c]]
 
     out = bytearray(b"\xff\xd8")
-    for m, p in segs:
-        if m in (0xDD,):
-            continue
+    for m, p in header:
         out += bytes([0xFF, m, (len(p) + 2) >> 8, (len(p) + 2) & 255]) + p
     if restart_interval:
         out += bytes([0xFF, 0xDD, 0, 4, restart_interval >> 8, restart_interval & 255])
@@ -171,3 +156,52 @@ def rewrite_scans(data: bytes, coefs: np.ndarray, scans, restart_interval=0):
         out += bw.out
     out += b"\xff\xd9"
     return bytes(out), expect.reshape(coefs.shape)
+
+
+def rewrite_scans(data: bytes, coefs: np.ndarray, scans, restart_interval=0):
+    """scans: list of tuples of frame component indices, e.g. [(0,), (1, 2)].
+    coefs: the source's coefficients (MCU-major, zigzag) from the decoder under
+    test's baseline path, which the tests pin against the reference.
+    Returns (jpeg bytes, expected coefficients): a non-interleaved scan codes
+    only the component's own block grid (T.81 A.2.2), so MCU-padding blocks
+    outside it are expected as zeros (they lie wholly outside the image)."""
+    segs = _segments(data)
+    sof = next(p for m, p in segs if m in (0xC0, 0xC1))
+    h, w, nc = (sof[1] << 8) | sof[2], (sof[3] << 8) | sof[4], sof[5]
+    comps = [(sof[6 + 3 * c], sof[7 + 3 * c] >> 4, sof[7 + 3 * c] & 15) for c in range(nc)]
+    dht = _dht_codes(segs)
+    # table ids of each component: copy the source's first SOS
+    p = 2
+    while not (data[p] == 0xFF and data[p + 1] == 0xDA):
+        p += 2 + ((data[p + 2] << 8) | data[p + 3])
+    ns0 = data[p + 4]
+    tabs = {}
+    for i in range(ns0):
+        cid, t = data[p + 5 + 2 * i], data[p + 6 + 2 * i]
+        tabs[[c[0] for c in comps].index(cid)] = (t >> 4, t & 15)
+    header = [(m, p) for m, p in segs if m != 0xDD]
+    return _emit(header, comps, tabs, dht, w, h, coefs, scans, restart_interval)
+
+
+def encode_frame(coefs: np.ndarray, width: int, height: int, factors, qt, huff_src: bytes, scans=None,
+                 restart_interval=0) -> bytes:
+    """A baseline JPEG of the given quantised coefficients (MCU-major, zigzag)
+    with SOF sampling factors `factors` [(H, V) per component] -- e.g. the
+    4:1:1 (H4V1) and 4:4:0 (H1V2) layouts Pillow cannot write.  qt: zigzag
+    tables (Y; chroma).  The Huffman tables are copied from huff_src (a
+    libjpeg file with the standard tables: DC/AC 0 for Y, 1 for chroma)."""
+    nc = len(factors)
+    comps = [(c + 1, hf, vf) for c, (hf, vf) in enumerate(factors)]
+    header = []
+    for t in range(min(nc, 2)):
+        header.append((0xDB, bytes([t]) + bytes(int(v) for v in qt[t])))
+    sof = bytes([8, height >> 8, height & 255, width >> 8, width & 255, nc])
+    for c, (cid, hf, vf) in enumerate(comps):
+        sof += bytes([cid, (hf << 4) | vf, 0 if c == 0 else 1])
+    header.append((0xC0, sof))
+    src = _segments(huff_src)
+    header += [(m, p) for m, p in src if m == 0xC4]
+    tabs = {c: (0, 0) if c == 0 else (1, 1) for c in range(nc)}
+    if scans is None:
+        scans = [tuple(range(nc))]
+    return _emit(header, comps, tabs, _dht_codes(src), width, height, coefs, scans, restart_interval)[0]

@@ -174,8 +174,9 @@ def std_qtables(scale=1.0):
 
 
 # sampling (include/hjd.h codes) -> (MCU px width, MCU px height, blocks per MCU,
-# luma blocks per MCU); 3 (4:2:2) and 4 (gray) are the extensions of oracle.h
-GEOM = {0: (8, 8, 3, 1), 1: (16, 16, 6, 4), 3: (16, 8, 4, 2), 4: (8, 8, 1, 1)}
+# luma blocks per MCU); 3 (4:2:2), 4 (gray), 5 (4:1:1, Y H4V1) and 6 (4:4:0,
+# Y H1V2) are the extensions of oracle.h
+GEOM = {0: (8, 8, 3, 1), 1: (16, 16, 6, 4), 3: (16, 8, 4, 2), 4: (8, 8, 1, 1), 5: (32, 8, 6, 4), 6: (8, 16, 4, 2)}
 
 
 def frame_blocks(width, height, sampling):

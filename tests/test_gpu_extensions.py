@@ -3,7 +3,10 @@ and one-component (gray) frames -- through every entry point: the fused
 kernel (both input formats), the host-Huffman JPEG path, the stream, and the
 GPU entropy decoder.
 
-The reference rejects both samplings (src/decoder.cpp:58-69), so there is no
+4:1:1 (Y H4V1) and 4:4:0 (Y H1V2) follow the same rules (test_411_440_jpeg_paths;
+CPU side: tests/test_samplings.py).
+
+The reference rejects these samplings (src/decoder.cpp:58-69), so there is no
 reference output: the HIP path is pinned bit-exactly to the oracle's
 restatement (oracle/oracle.c put_mcu: the reference's IDCT and colour
 arithmetic, nearest horizontal chroma replication, gray = the conversion with
@@ -19,12 +22,13 @@ from test_gpu_parity import _decode, to_u32
 
 pytestmark = pytest.mark.gpu
 
-YUV422, GRAY = 3, 4
+YUV422, GRAY, YUV411, YUV440 = 3, 4, 5, 6
+EXT = [YUV422, GRAY, YUV411, YUV440]
 
 
-@pytest.mark.parametrize("s", [YUV422, GRAY])
+@pytest.mark.parametrize("s", EXT)
 @pytest.mark.parametrize("w,h", [(1, 1), (8, 8), (16, 8), (17, 9), (191, 8), (193, 9), (383, 17), (385, 16),
-                                 (1920, 40), (2049, 31)])
+                                 (1920, 40), (2049, 31), (95, 16), (97, 33), (255, 8), (257, 17)])
 def test_random_frames_vs_oracle(hjd, ctx, s, w, h):
     coefs, qt = O.synthetic_coefs(w, h, s, seed=w * 31 + h + s)
     px, _ = _decode(hjd, ctx, coefs, qt, w, h, s)
@@ -34,7 +38,7 @@ def test_random_frames_vs_oracle(hjd, ctx, s, w, h):
         assert (b[..., 0] == b[..., 1]).all() and (b[..., 1] == b[..., 2]).all() and (b[..., 3] == 0).all()
 
 
-@pytest.mark.parametrize("s", [YUV422, GRAY])
+@pytest.mark.parametrize("s", EXT)
 def test_i32_natural_input(hjd, ctx, s):
     w, h = 777, 45
     coefs, qt = O.synthetic_coefs(w, h, s, seed=5)
@@ -43,7 +47,7 @@ def test_i32_natural_input(hjd, ctx, s):
     np.testing.assert_array_equal(px, O.decode_q16(coefs, qt, w, h, s))
 
 
-@pytest.mark.parametrize("s", [YUV422, GRAY])
+@pytest.mark.parametrize("s", EXT)
 def test_no_writes_outside_frame(hjd, ctx, s):
     w, h = 45, 37
     coefs, qt = O.synthetic_coefs(w, h, s, seed=3)
@@ -69,14 +73,14 @@ def _corner_frame(w, h, s, seed):
     ny = int((comp == 0).sum())
     blocks[comp == 0, 0] = 8 * rng.integers(-256, 256, ny)
     blocks[comp == 0, 1:10] = rng.integers(-40, 41, (ny, 9))
-    mcu = np.arange(nblk) // {0: 3, 1: 6, 3: 4, 4: 1}[s]
+    mcu = np.arange(nblk) // {0: 3, 1: 6, 3: 4, 4: 1, 5: 6, 6: 4}[s]
     for c in (1, 2):
         sel = comp == c
         blocks[sel, 0] = [8 * corners[m % 4][c - 1] for m in mcu[sel]]
     return blocks
 
 
-@pytest.mark.parametrize("s", [0, 1, YUV422])
+@pytest.mark.parametrize("s", [0, 1, YUV422, YUV411, YUV440])
 def test_colour_corners_through_the_kernel(hjd, ctx, s):
     """The kernel's wave-uniform corrected-G path (hjd_device.hpp g_fix) on
     every sampling with chroma, against the oracle's literal fp64 conversion."""
@@ -179,7 +183,7 @@ def _decode24(hjd, ctx, coefs, qt, w, h, s, pitch, guard=64, fmt=0):
     return rows[:, :3 * w]
 
 
-@pytest.mark.parametrize("s", [0, 1, YUV422, GRAY])
+@pytest.mark.parametrize("s", [0, 1] + EXT)
 @pytest.mark.parametrize("w,h,pad", [(1, 1, 0), (17, 9, 0), (129, 33, 4), (385, 16, 0), (1920, 40, 0),
                                      (2049, 31, 12)])
 def test_bgr24_vs_oracle(hjd, ctx, s, w, h, pad):
@@ -256,3 +260,58 @@ def test_bgr24_host_huffman_stream(hjd, ctx):
         st.sync()
     for o, e, i in zip(outs, exps, infos):
         np.testing.assert_array_equal(o.cpu().numpy()[:, :3 * i.width], _bgr24(e))
+
+
+def _jw_jpegs():
+    """4:1:1 and 4:4:0 files (Pillow cannot write them): tests/jpeg_writer.py
+    from synthetic coefficients, with and without DRI, edge geometries."""
+    import io
+    from PIL import Image
+    import jpeg_writer as JW
+    b = io.BytesIO()
+    Image.fromarray(np.zeros((16, 16, 3), np.uint8)).save(b, format="JPEG", quality=90)
+    src = b.getvalue()
+    fac = {YUV411: [(4, 1), (1, 1), (1, 1)], YUV440: [(1, 2), (1, 1), (1, 1)]}
+    out = []
+    for s in (YUV411, YUV440):
+        for w, h, dri in ((640, 480, 0), (333, 77, 2), (1921, 1081, 0), (1, 1, 0)):
+            coefs, qt = O.synthetic_coefs(w, h, s, seed=w + s)
+            out.append(JW.encode_frame(coefs, w, h, fac[s], qt, src, restart_interval=dri))
+    return out
+
+
+def test_411_440_jpeg_paths(hjd, ctx):
+    """decode_jpeg, the host-Huffman stream, the GPU entropy decoder (in a
+    batch mixing all six samplings) and the GPU-entropy stream on 4:1:1 and
+    4:4:0 files: bit-exact to the oracle on the host-decoded coefficients."""
+    import torch
+    datas = _jw_jpegs()
+    mixed = datas + _jpegs() + [_pil(500, 300, 90, 2, seed=1), _pil(300, 200, 90, 0, seed=2)]
+    exps, infos = zip(*[_expected(hjd, d) for d in mixed])
+    assert {i.sampling for i in infos} == {0, 1, YUV422, GRAY, YUV411, YUV440}
+    for d, e in zip(datas, exps):
+        np.testing.assert_array_equal(to_u32(hjd.decode_jpeg(ctx, d)), e)
+    for sub_bits in (64, 2048):
+        outs = [torch.full((i.height, i.width), -1, dtype=torch.int32, device="cuda") for i in infos]
+        with hjd.GpuDecoder(ctx, len(mixed), sum(map(len, mixed)), sum(i.nblocks for i in infos), sub_bits) as gd:
+            gd.decode(mixed, outs)
+            status = gd.sync()
+        for k, (o, e) in enumerate(zip(outs, exps)):
+            np.testing.assert_array_equal(to_u32(o), e, err_msg=f"file {k} S={sub_bits}")
+        assert all(s & ~1 == 0 for s in status)
+    n = len(datas)
+    outs = [torch.full((i.height, i.width), -1, dtype=torch.int32, device="cuda") for i in infos[:n]]
+    with hjd.JpegStream(ctx, max(i.nblocks for i in infos[:n]), nslots=2, nthreads=2) as st:
+        for d, o in zip(datas, outs):
+            st.submit(d, o)
+        st.sync()
+    for o, e in zip(outs, exps):
+        np.testing.assert_array_equal(to_u32(o), e)
+    outs = [torch.full((i.height, i.width), -1, dtype=torch.int32, device="cuda") for i in infos[:n]]
+    with hjd.GpuJpegStream(ctx, max_frames=3, max_scan_bytes=sum(map(len, datas)),
+                           max_blocks=sum(i.nblocks for i in infos[:n])) as gs:
+        for d, o in zip(datas, outs):
+            gs.submit(d, o)
+        gs.sync()
+    for o, e in zip(outs, exps):
+        np.testing.assert_array_equal(to_u32(o), e)

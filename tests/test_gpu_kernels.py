@@ -37,7 +37,7 @@ def _expect(bgrx, out_format):
 
 
 @pytest.mark.parametrize("mode", [1, 2])
-@pytest.mark.parametrize("s", [0, 1, 3, 4])
+@pytest.mark.parametrize("s", [0, 1, 3, 4, 5, 6])
 def test_both_kernels_vs_oracle(hjd, ctx, mode, s):
     for (w, h) in SIZES:
         coefs, qt = O.synthetic_coefs(w, h, s, seed=w + h + s)
@@ -50,7 +50,7 @@ def test_both_kernels_vs_oracle(hjd, ctx, mode, s):
         np.testing.assert_array_equal(got, _expect(exp, 0), err_msg=f"{w}x{h} s={s} i32")
 
 
-@pytest.mark.parametrize("s", [0, 1, 3])
+@pytest.mark.parametrize("s", [0, 1, 3, 5, 6])
 def test_latency_kernel_colour_corners(hjd, ctx, s):
     """The flagged-G path inside the latency kernel's split colour stage."""
     from test_gpu_extensions import _corner_frame
@@ -100,7 +100,7 @@ def _q16_frame(w, h, s, seed):
 
 
 @pytest.mark.parametrize("mode", [1, 2])
-@pytest.mark.parametrize("s", [0, 1, 3, 4])
+@pytest.mark.parametrize("s", [0, 1, 3, 4, 5, 6])
 def test_16bit_quantisation_tables(hjd, ctx, mode, s):
     """DQT precision 1 (16-bit entries, T.81 B.2.4.1): factors above 255
     through the 24-bit dequant multiply of both kernels, on blocks inside the

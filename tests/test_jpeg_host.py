@@ -81,12 +81,12 @@ def test_rejects_unsupported(lib):
     data = bytearray(b.getvalue())
     data[data.index(b"\xff\xc0") + 1] = 0xC3               # lossless (SOF3); progressive: test_jpeg_multiscan.py
     assert decode(lib, bytes(data))[0] != 0
-    # 4:4:0 (Y H1V2): patch the luma sampling byte of a 4:2:2 file's SOF0
+    # Y H3V1 (no such layout is supported): patch the luma sampling byte of a 4:2:2 file's SOF0
     b = io.BytesIO(); img.save(b, format="JPEG", subsampling=1)
     data = bytearray(b.getvalue())
     sof = data.index(b"\xff\xc0")
     assert data[sof + 11] == 0x21
-    data[sof + 11] = 0x12
+    data[sof + 11] = 0x31
     assert decode(lib, bytes(data))[0] != 0
     assert decode(lib, b"\x00\x01garbage")[0] != 0
     good = _pil_jpeg(32, 32, 90, 2)
