@@ -44,7 +44,10 @@ constexpr int kGroupSubs = 256;                 // subsequences per workgroup (o
 constexpr int kWarm = 8;                        // leading subsequences a group shares with its predecessor
 constexpr int kOwn = kGroupSubs - kWarm;        // subsequences a group is responsible for
 constexpr int kDefaultSubBits = 2048;           // S
-constexpr int kStageStride = 24;                // int16 per lane in the staging buffer: one 16-coefficient quarter (+pad)
+// int16 per lane in the staging buffer: one 16-coefficient quarter + 8 B pad.
+// 40 B (8-B aligned, accessed as 8-B pieces) keeps the write kernel's LDS
+// (256 slots + the tables) under 20 KiB, i.e. 8 groups per CU.
+constexpr int kStageStride = 20;
 
 // A decoded unit (one Huffman symbol + its extra bits) in table form, 16 bits:
 //   [4:0]  total: code length + extra bits s (the bits the unit consumes, >= 1)
@@ -255,16 +258,20 @@ struct RunOut {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
 // Write-mode staging: only the quarter of the block being filled (16
 // coefficients, z order) lives in LDS; quarters are flushed with two 16-B
 // stores as z moves past them, so every block is still written exactly once
-// as 8 x 16 B, while the LDS per lane is 48 B instead of a whole block.
+// as 8 x 16 B, while the LDS per lane is 40 B instead of a whole block.
 __host__ __device__ __forceinline__ void zero_quarter(int16_t* stage)
 {
-    u32x4* p = reinterpret_cast<u32x4*>(stage);
-    const u32x4 zv = {0u, 0u, 0u, 0u};
+    u32x2* p = reinterpret_cast<u32x2*>(stage);
+    const u32x2 zv = {0u, 0u};
     p[0] = zv;
     p[1] = zv;
+    p[2] = zv;
+    p[3] = zv;
 }
 
 // Store the staged quarter q to the block, zeros for quarters q+1 .. qn-1,
@@ -272,16 +279,16 @@ __host__ __device__ __forceinline__ void zero_quarter(int16_t* stage)
 __host__ __device__ __forceinline__ void flush_quarters(int16_t* blk, int16_t* stage, uint32_t q, uint32_t qn)
 {
     u32x4* d = reinterpret_cast<u32x4*>(blk);
-    u32x4* sp = reinterpret_cast<u32x4*>(stage);
-    d[2 * q] = sp[0];
-    d[2 * q + 1] = sp[1];
+    u32x2* sp = reinterpret_cast<u32x2*>(stage);
+    const u32x2 a = sp[0], b = sp[1], c = sp[2], e = sp[3];
+    d[2 * q] = u32x4{a.x, a.y, b.x, b.y};
+    d[2 * q + 1] = u32x4{c.x, c.y, e.x, e.y};
     const u32x4 zv = {0u, 0u, 0u, 0u};
     for (uint32_t i = q + 1; i < qn; ++i) {
         d[2 * i] = zv;
         d[2 * i + 1] = zv;
     }
-    sp[0] = zv;
-    sp[1] = zv;
+    zero_quarter(stage);
 }
 
 // Raw (little-endian) 16-B chunk of the frame's bit string.
