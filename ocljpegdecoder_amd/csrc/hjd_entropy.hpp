@@ -380,12 +380,13 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
     int32_t nblk = static_cast<int32_t>(st.nblk), d0 = st.dc[0], d1 = st.dc[1], d2 = st.dc[2];
     uint32_t flags = st.flags;
     int32_t p0 = 0, p1 = 0, p2 = 0;
-    uint32_t blk = 0;
+    uint32_t blk = 0, blk_j = 0;   // write mode: global block index and blk % bpm (kept incrementally)
     if (kWrite) {
         p0 = out->pred[0];
         p1 = out->pred[1];
         p2 = out->pred[2];
         blk = out->blk;
+        blk_j = blk % static_cast<uint32_t>(c.bpm);
     }
     uint64_t result;
     if (seg >= c.nseg) {
@@ -502,7 +503,7 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
                     const uint32_t dst = blk - j + (bi.ji >> 8);
                     cur = nullptr;
                     if (blk < out->nblocks) {
-                        if (dst < out->nblocks && blk % static_cast<uint32_t>(c.bpm) == j) {
+                        if (dst < out->nblocks && blk_j == j) {
                             cur = out->coefs + static_cast<uint64_t>(dst) * 64;
                             zero_quarter(out->stage);
                             out->stage[0] = static_cast<int16_t>(p0 * bi.m0 + p1 * bi.m1 + p2 * bi.m2);
@@ -525,6 +526,7 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
                 if (kWrite && owned) {
                     if (cur) flush_quarters(cur, out->stage, quarter, 4);   // the rest of the block
                     blk += 1;
+                    blk_j = blk_j + 1 == static_cast<uint32_t>(c.bpm) ? 0 : blk_j + 1;
                     owned = false;
                     cur = nullptr;
                 }
