@@ -25,6 +25,7 @@ struct HuffTable {
     uint8_t counts[16];      // the DHT spec, kept for the GPU tables (hjd_entropy.hip)
     int nsym = 0;
     uint16_t fast[512];      // (length << 8) | symbol for codes of <= 9 bits; 0 = slow path
+    int32_t fast_ac[512];    // AC: (value << 16) | (run << 5) | (code + extra bits) when those fit 9 bits, else 0
     int32_t maxcode[18];     // largest code of each length (-1: none)
     int32_t valptr[17];
     int32_t mincode[17];
@@ -85,6 +86,18 @@ int build_table(HuffTable& t, const uint8_t counts[16], const uint8_t* symbols, 
         code <<= 1;
     }
     t.maxcode[17] = 0x7fffffff;
+    // combined AC entries: symbol and its extra bits in one lookup (nonzero
+    // coefficients whose code + magnitude bits fit the 9-bit index)
+    memset(t.fast_ac, 0, sizeof(t.fast_ac));
+    for (int idx = 0; idx < 512; ++idx) {
+        const uint16_t e = t.fast[idx];
+        if (!e) continue;
+        const int len = e >> 8, rs = e & 0xFF, run = rs >> 4, size = rs & 15;
+        if (size == 0 || len + size > 9) continue;
+        const int bits = (idx >> (9 - len - size)) & ((1 << size) - 1);
+        const int value = bits < (1 << (size - 1)) ? bits - (1 << size) + 1 : bits;
+        t.fast_ac[idx] = static_cast<int32_t>((static_cast<uint32_t>(value) << 16) | (run << 5) | (len + size));
+    }
     t.defined = true;
     return 0;
 }
@@ -313,6 +326,20 @@ struct BitReader {
 
     void refill()
     {
+        // fast path: the next 8 bytes hold no 0xFF (no stuffing, no marker) --
+        // take as many whole bytes as fit in one big-endian load
+        if (!at_marker && end - p >= 8) {
+            uint64_t v;
+            memcpy(&v, p, 8);
+            const uint64_t inv = ~v;   // a 0xFF byte of v is a zero byte of inv
+            if (((inv - 0x0101010101010101ull) & ~inv & 0x8080808080808080ull) == 0) {
+                const int take = (63 - nbits) >> 3;   // bytes that fit (nbits < 64 after)
+                acc |= (__builtin_bswap64(v) >> nbits) & ~(~0ull >> (nbits + 8 * take));
+                p += take;
+                nbits += 8 * take;
+                return;
+            }
+        }
         while (nbits <= 56) {
             uint64_t b = 0;
             if (!at_marker && p < end) {
@@ -387,6 +414,15 @@ inline bool decode_block(BitReader& br, const HuffTable& dc, const HuffTable& ac
     memset(out, 0, 64 * sizeof(int16_t));
     out[0] = static_cast<int16_t>(pred);
     for (int k = 1; k < 64;) {
+        if (br.nbits < 16) br.refill();
+        const int32_t fe = ac.fast_ac[br.peek(9)];
+        if (fe) {   // run + nonzero coefficient in one lookup
+            br.skip(fe & 31);
+            k += (fe >> 5) & 15;
+            if (k > 63) return false;
+            out[k++] = static_cast<int16_t>(fe >> 16);
+            continue;
+        }
         const int rs = decode_symbol(br, ac);
         if (rs < 0) return false;
         const int r = rs >> 4, sz = rs & 15;
