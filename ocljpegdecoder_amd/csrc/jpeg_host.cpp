@@ -407,9 +407,16 @@ inline int receive_extend(BitReader& br, int s)
 // One block (src/decoder.cpp:221-260).
 inline bool decode_block(BitReader& br, const HuffTable& dc, const HuffTable& ac, int& pred, int16_t* out)
 {
-    int s = decode_symbol(br, dc);
-    if (s < 0 || s > 11) return false;
-    pred += receive_extend(br, s);
+    if (br.nbits < 16) br.refill();
+    const int32_t fd = dc.fast_ac[br.peek(9)];   // a DC table's symbols are sizes: run 0
+    if (fd) {
+        br.skip(fd & 31);
+        pred += fd >> 16;
+    } else {
+        const int s = decode_symbol(br, dc);
+        if (s < 0 || s > 11) return false;
+        pred += receive_extend(br, s);
+    }
     if (pred < -32768 || pred > 32767) return false;
     memset(out, 0, 64 * sizeof(int16_t));
     out[0] = static_cast<int16_t>(pred);
