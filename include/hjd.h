@@ -82,8 +82,9 @@ enum hjd_input_format {
  * One frame of a batch.  Blocks are MCU-major in raster MCU order; per MCU the
  * Y blocks in HxV raster order, then Cb, then Cr (src/decoder.cpp:286-344).
  * MCU grid: ceil(W/8)xceil(H/8) (4:4:4, 3 blocks; gray, 1 block),
- * ceil(W/16)xceil(H/16) (4:2:0, 6 blocks) or ceil(W/16)xceil(H/8) (4:2:2,
- * 4 blocks).
+ * ceil(W/16)xceil(H/16) (4:2:0, 6 blocks), ceil(W/16)xceil(H/8) (4:2:2,
+ * 4 blocks), ceil(W/32)xceil(H/8) (4:1:1, 6 blocks) or ceil(W/8)xceil(H/16)
+ * (4:4:0, 4 blocks).
  */
 typedef struct hjd_frame {
     uint64_t coef_offset; /* first block's offset in the coef buffer, in BLOCKS */
@@ -91,7 +92,7 @@ typedef struct hjd_frame {
     int32_t width;        /* visible pixels (output is cropped to W x H) */
     int32_t height;
     int32_t out_pitch;    /* bytes per output row, >= 4*width (BGR24: 3*width), multiple of 4 */
-    int32_t sampling;     /* HJD_YUV444, HJD_YUV420, HJD_YUV422 or HJD_GRAY */
+    int32_t sampling;     /* enum hjd_sampling (not HJD_OTHER) */
     int32_t qt_index[3];  /* per component (Y, Cb, Cr): index into the qtable set */
     int32_t out_format;   /* HJD_OUT_BGRX (0) or HJD_OUT_BGR24; the same for all frames of a plan */
 } hjd_frame;
