@@ -514,8 +514,10 @@ struct CoefLayout {
     }
     int16_t* at(int16_t* coefs, int c, int by, int bx) const
     {
-        const int64_t mcu = static_cast<int64_t>(by / vs[c]) * mcu_w + bx / hs[c];
-        return coefs + (mcu * bpm + base[c] + (by % vs[c]) * hs[c] + bx % hs[c]) * 64;
+        // sampling factors are 1, 2 or 4 in every admitted layout: shifts and masks
+        const int lh = hs[c] >> 1, lv = vs[c] >> 1;   // log2 of 1, 2, 4
+        const int64_t mcu = static_cast<int64_t>(by >> lv) * mcu_w + (bx >> lh);
+        return coefs + (mcu * bpm + base[c] + ((by & (vs[c] - 1)) << lh) + (bx & (hs[c] - 1))) * 64;
     }
 };
 
@@ -563,6 +565,17 @@ inline bool ac_first(BitReader& br, const HuffTable& ac, const ScanSpec& sc, int
         return true;
     }
     for (int k = sc.ss; k <= sc.se;) {
+        if (br.nbits < 16) br.refill();
+        const int32_t fe = ac.fast_ac[br.peek(9)];
+        if (fe) {   // run + nonzero coefficient in one lookup
+            br.skip(fe & 31);
+            k += (fe >> 5) & 15;
+            if (k > sc.se) return false;
+            const int v = (fe >> 16) * (1 << sc.al);
+            if (!fits16(v)) return false;
+            blk[k++] = static_cast<int16_t>(v);
+            continue;
+        }
         const int rs = decode_symbol(br, ac);
         if (rs < 0) return false;
         const int r = rs >> 4, s = rs & 15;
