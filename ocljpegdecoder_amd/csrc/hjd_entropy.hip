@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -1053,12 +1054,30 @@ int gdec_run(hjd_gdec* g, const uint8_t* const* datas, const size_t* sizes, int 
 
 extern "C" {
 
+// Subsequence length when the caller passes 0.  Longer subsequences mean fewer
+// guessed starts to repair but fewer workgroups.  Measured on 4K q90 4:2:0
+// batches (profiles/r01_entropy_subbits.json, sync + write kernels):
+// - 64 frames: S = 4096 is 5-8 % faster than 2048;
+// - 32 frames: S = 4096 is 6 % slower;
+// - 8 frames: S = 4096 is 34 % slower.
+// Hence 4096 for decoders sized for >= 64 frames per call.  HJD_SUB_BITS
+// overrides it (tuning hook, tools/gpu_subbits_sweep.sh).
+static int default_sub_bits(int max_frames)
+{
+    static const int env = [] {
+        const char* e = getenv("HJD_SUB_BITS");
+        return e ? atoi(e) : 0;
+    }();
+    if (env) return env;
+    return max_frames >= 64 ? 2 * kDefaultSubBits : kDefaultSubBits;
+}
+
 int hjd_gdec_create(hjd_ctx* ctx, int max_frames, int64_t max_scan_bytes, int64_t max_blocks, int sub_bits,
                     hjd_gdec** out)
 {
     if (!ctx || !out || max_frames <= 0 || max_scan_bytes <= 0 || max_blocks <= 0)
         return set_error(HJD_E_INVALID, "invalid gdec arguments");
-    if (sub_bits == 0) sub_bits = kDefaultSubBits;
+    if (sub_bits == 0) sub_bits = default_sub_bits(max_frames);
     if (sub_bits < 32 || sub_bits > (1 << 20)) return set_error(HJD_E_INVALID, "sub_bits out of range [32, 2^20]");
     *out = nullptr;
     hjd_gdec* g = new (std::nothrow) hjd_gdec;
