@@ -1060,7 +1060,8 @@ extern "C" {
 // - 64 frames: S = 4096 is 5-8 % faster than 2048;
 // - 32 frames: S = 4096 is 6 % slower;
 // - 8 frames: S = 4096 is 34 % slower.
-// Hence 4096 for decoders sized for >= 64 frames per call.  HJD_SUB_BITS
+// Hence 4096 for decoders sized for >= 48 frames per call (the stream's
+// 48-frame batches: profiles/r01_stream_batch_ab.json).  HJD_SUB_BITS
 // overrides it (tuning hook, tools/gpu_subbits_sweep.sh).
 static int default_sub_bits(int max_frames)
 {
@@ -1069,7 +1070,7 @@ static int default_sub_bits(int max_frames)
         return e ? atoi(e) : 0;
     }();
     if (env) return env;
-    return max_frames >= 64 ? 2 * kDefaultSubBits : kDefaultSubBits;
+    return max_frames >= 48 ? 2 * kDefaultSubBits : kDefaultSubBits;
 }
 
 int hjd_gdec_create(hjd_ctx* ctx, int max_frames, int64_t max_scan_bytes, int64_t max_blocks, int sub_bits,
