@@ -133,7 +133,7 @@ int hjd_gdec_set_output_format(hjd_gdec* g, int out_format);
 /* ---- GPU-entropy stream: JPEG bytes in, BGRX in HBM out -----------------
  * Like hjd_stream, but the Huffman decode runs on the GPU: worker threads only
  * parse + destuff each JPEG into the pinned staging of the open batch (up to
- * max_frames JPEGs / max_scan_bytes / max_blocks per batch); nslots (2..8)
+ * max_frames JPEGs / max_scan_bytes / max_blocks per batch); nslots (2..16)
  * batches rotate on their own HIP streams so uploads overlap kernels. */
 typedef struct hjd_gstream hjd_gstream;
 int hjd_gstream_create(hjd_ctx* ctx, int max_frames, int64_t max_scan_bytes, int64_t max_blocks, int nslots,

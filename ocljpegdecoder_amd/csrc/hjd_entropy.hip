@@ -1453,7 +1453,7 @@ extern "C" {
 int hjd_gstream_create(hjd_ctx* ctx, int max_frames, int64_t max_scan_bytes, int64_t max_blocks, int nslots,
                        int nthreads, hjd_gstream** out)
 {
-    if (!ctx || !out || nslots < 2 || nslots > 8) return set_error(HJD_E_INVALID, "invalid gstream arguments (nslots 2..8)");
+    if (!ctx || !out || nslots < 2 || nslots > 16) return set_error(HJD_E_INVALID, "invalid gstream arguments (nslots 2..16)");
     *out = nullptr;
     if (nthreads <= 0) nthreads = static_cast<int>(std::max(1u, std::thread::hardware_concurrency()));
     hjd_gstream* st = new (std::nothrow) hjd_gstream;
