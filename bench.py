@@ -186,6 +186,27 @@ def _cpu_model():
     return "unknown"
 
 
+def check_batch_vs_oracle(torch, out, pool_host, qt, wl, ofmt):
+    """Compare EVERY frame of the last timed launch's output with the oracle
+    (frame i holds pool[i % P]'s coefficients, so P oracle decodes cover the
+    whole batch); the comparison itself runs on the device.  Outside the timed
+    region.  Returns {"ok", "frames_checked", "frames_bad", ...}."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_py as O
+    w, h, s = wl["width"], wl["height"], wl["sampling"]
+    nf, npool = out.shape[0], pool_host.shape[0]
+    nbytes = 4 * w if ofmt == 0 else 3 * w
+    exp = []
+    for i in range(npool):
+        e = O.decode_q16(pool_host[i], qt, w, h, s).view(np.uint8).reshape(h, w, 4)
+        e = e.reshape(h, 4 * w) if ofmt == 0 else np.ascontiguousarray(e[..., :3]).reshape(h, 3 * w)
+        exp.append(torch.from_numpy(np.ascontiguousarray(e)).to(out.device))
+    bad = [i for i in range(nf) if not torch.equal(out[i, :, :nbytes], exp[i % npool])]
+    return {"ok": not bad, "frames_checked": nf, "frames_bad": len(bad), "first_bad": bad[:4],
+            "how": f"all {nf} frames of the last timed launch vs oracle_decode_frame_q16 of their pool frame "
+                   f"({npool} oracle decodes), compared on the device"}
+
+
 def committed_traffic(workload, frames):
     """Per-launch HBM bytes from the committed PMC summary for this workload,
     if it was profiled at this launch size (else None: the bytes of another
@@ -434,10 +455,13 @@ def main():
     except Exception:
         pass
 
+    # every frame of the timed launch's output vs the oracle (outside the timed region)
+    pool_host = coefs[:npool].cpu().numpy()
+    checked = check_batch_vs_oracle(torch, out, pool_host, qt, wl, ofmt)
+
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu:
-            pool_host = coefs[:npool].cpu().numpy()
             log("running CPU baseline leg ...")
             cpu = cpu_baseline(pool_host, qt, wl, value)
         traffic = committed_traffic(args.workload, nf)
@@ -460,6 +484,8 @@ def main():
                        "output": "BGRX 4 B/px in HBM" if ofmt == hjd.OUT_BGRX else "BGR24 3 B/px in HBM",
                        "parallelism": f"image-parallel x{world} (no collective)",
                        "tasks_per_launch": plan.tasks},
+            "output_checked_vs_oracle": checked["ok"],
+            "output_check": checked,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "traffic": traffic[0] if traffic else None,
@@ -474,6 +500,9 @@ def main():
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if not checked["ok"]:
+        log("FATAL: the timed launch's output differs from the oracle:", checked)
+        sys.exit(1)
 
 
 if __name__ == "__main__":
