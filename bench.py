@@ -124,20 +124,34 @@ def synth_frame_gpu(torch, nblk, sampling, qt, seed, device):
     return coef_nat[:, torch.tensor(ZIGZAG, device=device)].to(torch.int16).contiguous()
 
 
-def cpu_baseline(coef_pool_host, qt, wl, frames_done_gpu_rate):
-    """CPU leg (rank 0, N=1): oracle C restatement on a pthread pool over the
-    host cores, bounded sample; plus the reference's own decode_mcu_data."""
-    sys.path.insert(0, os.path.join(REPO, "tests"))
-    import oracle_py as O
-    lib = O.oracle()
-    w, h, s = wl["width"], wl["height"], wl["sampling"]
-    nthreads = int(os.environ.get("HJD_CPU_THREADS", min(16, os.cpu_count() or 1)))
-    # ~20 frames per thread: ~10-30 s of CPU work at ~0.05-0.15 s per 4K frame
-    nframes = 20 * nthreads
-    pool = np.ascontiguousarray(coef_pool_host)
+def host_cpu_share():
+    """(threads to use, logical CPUs in the affinity mask, cgroup CPU quota or None, nproc).
+
+    A one-GPU box shows all 256 logical CPUs of the node (os.cpu_count(), the
+    affinity mask) but its cgroup grants 16 CPUs of time (cpu.max 1600000/100000,
+    profiles/r02_gpu_box_host_probe.txt) and `nproc` says 16: more threads than
+    the quota only time-slice the same 16 CPUs (measured: `all_logical_cpus`)."""
+    import math
+    import subprocess
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        nproc = int(subprocess.run(["nproc"], capture_output=True, text=True, check=True).stdout)
+    except Exception:
+        nproc = None
+    share = min(aff, math.ceil(quota)) if quota else aff
+    return share, aff, quota, nproc
+
+
+def _port_rate(lib, O, pool, q, w, h, s, nframes, nthreads):
     stride = pool.shape[1] * 64
     out = np.empty((nthreads, h * w), dtype=np.uint32)
-    q = np.ascontiguousarray(qt, np.int32)
     t0 = time.perf_counter()
     rc = lib.oracle_decode_batch_q16_mt(pool.ctypes.data_as(O.i16p), stride, pool.shape[0],
                                         q[0].ctypes.data_as(O.i32p), q[1].ctypes.data_as(O.i32p),
@@ -145,10 +159,63 @@ def cpu_baseline(coef_pool_host, qt, wl, frames_done_gpu_rate):
                                         out.ctypes.data_as(O.u32p), h * w, nframes, nthreads)
     dt = time.perf_counter() - t0
     assert rc == 0
-    res = {"value": round(nframes * w * h / dt / 1e6, 2), "unit": "Mpixels/s", "cores": nthreads, "kind": "port",
+    return nframes * w * h / dt / 1e6, dt
+
+
+def host_huffman_rate(hjd, w, h, s, nthreads):
+    """Host Huffman (csrc/jpeg_host.cpp, the config-5 host bound of SURVEY s8(d)):
+    Mpx/s on 1 thread and on `nthreads` threads, q90 synthetic files of this shape."""
+    if s not in (0, 1):
+        return None
+    pool = encode_pool(w, h, s, 2, seed0=99)
+    res = {"sample": f"2 Pillow q90 {w}x{h} {SAMPLING_NAMES[s]} files (gradient + sigma-20 noise), "
+                     f"hjd_jpeg_decode_batch -> int16 coefficients in RAM", "mean_jpeg_bytes":
+           int(np.mean([len(d) for d in pool]))}
+    for key, nt, reps in (("one_thread_Mpx_s", 1, 4), ("all_threads_Mpx_s", nthreads, 4 * nthreads)):
+        datas = [pool[i % 2] for i in range(reps)]
+        hjd.decode_coefs_batch(datas[:2], nthreads=1)
+        t0 = time.perf_counter()
+        hjd.decode_coefs_batch(datas, nthreads=nt)
+        res[key] = round(reps * w * h / (time.perf_counter() - t0) / 1e6, 1)
+    res["threads"] = nthreads
+    return res
+
+
+def cpu_baseline(coef_pool_host, qt, wl, frames_done_gpu_rate):
+    """CPU leg (rank 0, N=1): oracle C restatement on a pthread pool over the
+    host CPUs this process is granted (one frame per task), bounded sample; a
+    1-thread figure; the host-Huffman rate; plus the reference's own
+    decode_mcu_data (1 thread)."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_py as O
+    import ocljpegdecoder_amd as hjd
+    lib = O.oracle()
+    w, h, s = wl["width"], wl["height"], wl["sampling"]
+    share, aff, quota, nproc = host_cpu_share()
+    nthreads = int(os.environ.get("HJD_CPU_THREADS", share))
+    pool = np.ascontiguousarray(coef_pool_host)
+    q = np.ascontiguousarray(qt, np.int32)
+    # ~20 frames per thread: ~10-30 s of CPU work at ~0.05-0.15 s per 4K frame
+    nframes = 20 * nthreads
+    rate, dt = _port_rate(lib, O, pool, q, w, h, s, nframes, nthreads)
+    rate1, dt1 = _port_rate(lib, O, pool, q, w, h, s, 12, 1)
+    res = {"value": round(rate, 2), "unit": "Mpixels/s", "cores": nthreads, "kind": "port",
            "sample": f"{nframes} frames {w}x{h} {SAMPLING_NAMES[s]} (pool of {pool.shape[0]}), "
                      f"int16 zigzag -> BGRX in RAM, {nthreads} threads, {dt:.2f} s wall",
-           "cpu_model": _cpu_model(), "nproc": os.cpu_count()}
+           "one_thread": {"value": round(rate1, 2), "unit": "Mpixels/s", "cores": 1,
+                          "sample": f"12 frames, 1 thread, {dt1:.2f} s"},
+           "cpu_model": _cpu_model(), "nproc": nproc, "logical_cpus": aff, "cgroup_cpu_quota": quota,
+           "threads_rule": "threads = the process's CPU share: min(affinity CPUs, cgroup cpu.max quota); "
+                           "equals nproc on the GPU box"}
+    if aff > nthreads and "HJD_CPU_THREADS" not in os.environ:
+        rate_all, dt_all = _port_rate(lib, O, pool, q, w, h, s, 2 * aff, aff)
+        res["all_logical_cpus"] = {"value": round(rate_all, 2), "unit": "Mpixels/s", "threads": aff,
+                                   "sample": f"{2 * aff} frames on {aff} threads, {dt_all:.2f} s (bounded by the "
+                                             f"cgroup quota, not by the thread count)"}
+    try:
+        res["host_huffman"] = host_huffman_rate(hjd, w, h, s, nthreads)
+    except Exception as e:  # pragma: no cover (Pillow missing)
+        res["host_huffman"] = {"error": str(e)}
     if O.ref_available() and s in (0, 1):   # the reference rejects other samplings
         try:
             lib_ref = O.ref()
@@ -243,16 +310,33 @@ def encode_pool(w, h, sampling, n, seed0):
         return list(ex.map(one, range(n)))
 
 
+STREAM_POOL = 64          # distinct files the global frame-id list cycles over
+CHECK_PRIME = (1 << 31) - 1
+
+
+def frame_checksum(torch, t, weights):
+    """Position-weighted checksum of one output frame (device or host tensor),
+    computed on the device: sum_k word_k * w_k mod (2^31 - 1) over its 32-bit words."""
+    x = t.reshape(-1).view(torch.int32).to(weights.device, non_blocking=True).to(torch.int64) & 0xFFFFFFFF
+    return int(((x * weights[:x.numel()]) % CHECK_PRIME).sum().item() % CHECK_PRIME)
+
+
 def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
     """Config 5: end-to-end JPEG bytes (host memory) -> BGRX in HBM, one stream
-    per GPU with its own host worker pool; frames sharded across ranks (no
-    collective).  entropy="gpu": workers only parse + destuff, the Huffman
-    decode runs on the GPU (hjd_gstream); entropy="host": host Huffman
-    workers (hjd_stream)."""
+    per GPU with its own host worker pool.  The stream is ONE global list of
+    frame ids (file = id % 64 over a shared pool of 64 encoded 4K files); step k
+    covers ids [k*G, (k+1)*G), G = frames_per_gpu * world, and rank r decodes
+    shard_round_robin(G, r, world) of them (no collective).  After timing, every
+    surviving frame of the last step gets a checksum, aggregated over ranks
+    with shard.aggregate and compared with the oracle's pixels of the same ids.
+    entropy="gpu": workers only parse + destuff, the Huffman decode runs on the
+    GPU (hjd_gstream); entropy="host": host Huffman workers (hjd_stream)."""
+    from ocljpegdecoder_amd import shard
     w, h, s, nf = wl["width"], wl["height"], wl["sampling"], wl["frames"]
-    cores = os.cpu_count() or 1
-    nthreads = int(os.environ.get("HJD_STREAM_THREADS", max(1, min(16, cores // max(1, world)))))
-    pool = encode_pool(w, h, s, 16, seed0=7919 * rank)
+    share = host_cpu_share()[0]
+    nthreads = int(os.environ.get("HJD_STREAM_THREADS", max(1, min(16, share // max(1, world)))))
+    npool = int(os.environ.get("HJD_STREAM_POOL", STREAM_POOL))
+    pool = encode_pool(w, h, s, npool, seed0=7919)       # identical on every rank: ids map to the same files
     infos = [hjd.parse(d) for d in pool]
     max_blocks = max(i.nblocks for i in infos)
     ctx = hjd.Context(dev.index)
@@ -268,9 +352,10 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
     shape, dtype = ((h, w), torch.int32) if ofmt == hjd.OUT_BGRX else ((h, pitch), torch.uint8)
     if d2h:
         # pinned host ring, one buffer per frame that can be in flight
-        ring = [torch.empty(shape, dtype=dtype).pin_memory() for _ in range(per_batch * nslots)]
+        ring = [torch.empty(shape, dtype=dtype).pin_memory() for _ in range(min(nf, per_batch * nslots))]
         outs = [ring[i % len(ring)] for i in range(nf)]
     else:
+        ring = None
         outs = [torch.empty(shape, dtype=dtype, device=dev) for _ in range(nf)]
     if gpu_entropy:
         st = hjd.GpuJpegStream(ctx, per_batch, per_batch * max(len(d) for d in pool) + (1 << 20),
@@ -283,44 +368,60 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
     # ctypes views of the pool made once: submit() then passes pointers (no per-call copy)
     from ocljpegdecoder_amd.jpeg import _buf
     pool_c = [_buf(d) for d in pool]
+    G = nf * world
+    mine = shard.shard_round_robin(G, rank, world)        # this rank's positions within every step
 
-    def step():
-        for i in range(nf):
-            st.submit(pool_c[i % len(pool_c)], outs[i])
+    def step(k):
+        base = k * G
+        for i, pos in enumerate(mine):
+            st.submit(pool_c[(base + pos) % npool], outs[i])
         return st.sync()
 
-    for _ in range(args.warmup):
-        step()
+    for k in range(args.warmup):
+        step(k)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     before = st.sync()                 # stats are cumulative
     after = before
-    for _ in range(args.steps):
-        after = step()
+    for k in range(args.warmup, args.warmup + args.steps):
+        after = step(k)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
     host_ns = after[stat_key] - before[stat_key]
-    from ocljpegdecoder_amd import shard
     wall_max = shard.aggregate({"seconds": wall})["seconds"]   # max over ranks
     px = nf * w * h * args.steps * world
-    # correctness spot check of the last step (outside the timed region)
-    ref, info = hjd.decode_coefs(pool[0])
-    ok = None
-    try:
-        sys.path.insert(0, os.path.join(REPO, "tests"))
-        import oracle_py as O
-        exp = O.decode_q16(ref, info.qt, info.width, info.height, info.sampling)
-        got = outs[0].cpu().numpy()
-        if ofmt == hjd.OUT_BGRX:
-            ok = bool((got.view(np.uint32) == exp).all())
-        else:
-            ok = bool((got[:, :3 * w] == exp.view(np.uint8).reshape(h, w, 4)[..., :3].reshape(h, -1)).all())
-    except Exception as e:  # oracle library not built
-        log("stream spot check skipped:", e)
+
+    # ---- correctness of the last step, outside the timed region ----------------
+    # expected pixels per pool file: host Huffman coefficients -> oracle (the checker)
+    last = (args.warmup + args.steps - 1) * G
+    live = range(nf - len(ring), nf) if d2h else range(nf)     # D2H ring: only the last frames survive
+    g = torch.Generator(device=dev)
+    g.manual_seed(12345)
+    nwords = outs[0].numel() * outs[0].element_size() // 4
+    weights = torch.randint(1, CHECK_PRIME, (nwords,), generator=g, device=dev, dtype=torch.int64)
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_py as O
+    exp_cs = {}
+    for i in live:
+        f = (last + mine[i]) % npool
+        if f not in exp_cs:
+            coefs, info = hjd.decode_coefs(pool[f])
+            e = O.decode_q16(coefs, info.qt, info.width, info.height, info.sampling)
+            if ofmt != hjd.OUT_BGRX:
+                e = np.zeros((h, pitch), np.uint8)
+                e[:, :3 * w] = O.decode_q16(coefs, info.qt, w, h, s).view(np.uint8).reshape(h, w, 4)[..., :3] \
+                    .reshape(h, 3 * w)
+            exp_cs[f] = frame_checksum(torch, torch.from_numpy(np.ascontiguousarray(e)), weights)
+    got = sum(frame_checksum(torch, outs[i], weights) for i in live)
+    exp = sum(exp_cs[(last + mine[i]) % npool] for i in live)
+    # sums of < 2^31 values over <= 2^21 frames are exact in float64 (shard.aggregate's dtype)
+    agg = shard.aggregate({"frames_checked": len(live), "checksum": got, "checksum_oracle": exp,
+                           "id_sum": sum(last + mine[i] for i in live)})
+    ok = agg["checksum"] == agg["checksum_oracle"]
     if rank == 0:
         jpeg_bytes = int(np.mean([len(d) for d in pool]))
         res = {
@@ -328,25 +429,36 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
             "value": round(px / wall_max / 1e6, 1), "unit": "Mpixels/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(wall_max / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "int32",
-            "data": "synthetic JPEG files (Pillow q90, gradient + sigma-20 noise), pool of 16 per rank, "
-                    f"{nf} frames per step per GPU",
+            "data": f"synthetic JPEG files (Pillow q90, gradient + sigma-20 noise), one pool of {npool} shared by all "
+                    f"ranks, cycled over a global frame-id list",
             "config": {"workload": wl["desc"], "frames_per_gpu_per_step": nf, "width": w, "height": h,
                        "sampling": SAMPLING_NAMES[s], "host_threads_per_gpu": nthreads,
                        "entropy_decode": "gpu" if gpu_entropy else "host", "mean_jpeg_bytes": jpeg_bytes,
                        "output": ("pinned host memory (D2H-on)" if d2h else "in HBM (D2H-off)") +
                                  (", BGR24" if ofmt == hjd.OUT_BGR24 else ", BGRX"),
+                       "sharding": f"global frame ids 0..{(args.warmup + args.steps) * G - 1} (file = id % {npool}); "
+                                   f"step k = ids [k*{G}, (k+1)*{G}), shard_round_robin over {world} rank(s)",
+                       "timed_frame_ids": args.steps * G,
                        "parallelism": f"image-parallel x{world} (no collective)"},
             "end_to_end": {
                 ("host_prep_Mpx_per_thread_s" if gpu_entropy else "host_huffman_Mpx_per_thread_s"):
                     round(nf * args.steps * w * h / (host_ns / 1e9) / 1e6, 1) if host_ns else None,
                 "jpeg_GBps_in": round(nf * args.steps * jpeg_bytes * world / wall_max / 1e9, 2),
-                "output_checked_vs_oracle": ok},
+                "output_checked_vs_oracle": bool(ok)},
+            "stream_check": {"frames_checked": int(agg["frames_checked"]), "checksum": int(agg["checksum"]),
+                             "checksum_oracle": int(agg["checksum_oracle"]), "id_sum": int(agg["id_sum"]),
+                             "how": "last step: per-frame position-weighted checksum of the output, summed over "
+                                    "ranks (shard.aggregate); oracle = host Huffman coefficients -> "
+                                    "oracle_decode_frame_q16 of the same ids"},
             "roofline": None, "cpu_baseline": None,
         }
         print(json.dumps(res), flush=True)
     st.close()
     if world > 1:
         dist.destroy_process_group()
+    if not ok:
+        log("FATAL: stream output differs from the oracle")
+        sys.exit(1)
 
 
 def main():

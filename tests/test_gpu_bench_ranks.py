@@ -23,12 +23,15 @@ def _free_port():
     return p
 
 
-def _run(workload, frames, extra=()):
+def _run(workload, frames, extra=(), ranks=2, steps=3):
     env = dict(os.environ, HJD_BENCH_SAME_DEVICE="1", MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="4")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
-           "--workload", workload, "--frames", str(frames), "--no-cpu", "--dist-backend", "gloo", *extra]
+    args = [os.path.join(ROOT, "bench.py"), "--gpus", str(ranks), "--steps", str(steps), "--warmup", "1",
+            "--workload", workload, "--frames", str(frames), "--no-cpu", *extra]
+    if ranks == 1:
+        cmd = [sys.executable, *args]
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(ranks),
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), *args, "--dist-backend", "gloo"]
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
@@ -54,3 +57,25 @@ def test_two_ranks_stream_bench():
     assert r["n_gpus"] == 2 and r["value"] > 0
     assert r["end_to_end"]["output_checked_vs_oracle"] is True
     assert r["config"]["entropy_decode"] == "gpu"
+
+
+@pytest.mark.gpu
+def test_stream_sharding_matches_one_rank():
+    """Config 5's shape: one global frame-id list (file = id % pool) sharded
+    round-robin over ranks.  Two ranks x 12 frames and one rank x 24 frames
+    cover the same ids in every step, so the per-frame checksums of the last
+    step, summed over ranks (shard.aggregate), must be identical -- and equal
+    to the oracle's checksum of those ids."""
+    extra_env = {"HJD_STREAM_POOL": "8"}
+    os.environ.update(extra_env)
+    try:
+        two = _run("stream4k420", 12, steps=2)
+        one = _run("stream4k420", 24, ranks=1, steps=2)
+    finally:
+        for k in extra_env:
+            os.environ.pop(k, None)
+    for r in (one, two):
+        c = r["stream_check"]
+        assert c["frames_checked"] == 24 and c["checksum"] == c["checksum_oracle"], c
+    assert two["stream_check"]["id_sum"] == one["stream_check"]["id_sum"] == sum(range(48, 72))
+    assert two["stream_check"]["checksum"] == one["stream_check"]["checksum"]
