@@ -149,6 +149,13 @@ int hjd_plan_launch(hjd_plan* plan, const void* d_coefs, void* d_out, void* stre
  * place: int32 natural-order dequantised blocks -> int32 samples [-256,255]. */
 int hjd_idct_blocks(hjd_ctx* ctx, const int32_t* d_in, int32_t* d_out, int64_t nblocks, void* stream);
 
+/* The idct.h shim (include/idct.h) keeps its context, stream, grow-only device
+ * buffers, plan cache and pinned staging alive across images: the reference
+ * caller's clidct_clean_up (src/decoder.cpp:518-521) ends one image only.
+ * This frees all of it (HJD_COMPAT_TEARDOWN=1 does so after every image, as
+ * src/oclDCT8x8.cpp:316-341 did). */
+int hjd_compat_release(void);
+
 /* ---- test / measurement hooks (same device code as the fused kernel) ---- */
 /* Colour stage alone over n (Y,U,V) triples: out[i] = BGRX.  mode 0 = the
  * kernel's exact-integer formulation, 1 = literal fp64 formulation. */

@@ -108,3 +108,43 @@ def test_reference_program_on_mi355x(name):
     assert bmp[:54] == hjd.bmp_header(w, h)    # our BMP sink writes the reference's header
     px = bmp[54:]
     assert hashlib.sha256(px).hexdigest() == rec["bgrx_sha256"]
+
+
+def _fnv1a(b: bytes) -> int:
+    h = 1469598103934665603
+    for c in np.frombuffer(b, np.uint8).tolist():
+        h = ((h ^ c) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(DROPIN), reason="oracle/_ref/ref_dropin not built")
+def test_reference_program_many_images_one_process():
+    """The reference program decodes several files per process (src/main.cpp:31-39)
+    and runs the whole idct.h lifecycle per image (src/decoder.cpp:202-216,
+    :518-521).  The shim keeps context, stream, buffers and plans across images:
+    the first image allocates, a smaller image of a new geometry only builds a
+    plan, the first geometry again allocates and builds nothing -- and every
+    image's retrieved pixels are the reference's (FNV-1a of the BGRX rows)."""
+    names = ["JPEG_example_JPG_RIP_050", "syn444_odd_41x23_q75", "JPEG_example_JPG_RIP_050", "syn420_160x48_q95_dri"]
+    tmp = tempfile.mkdtemp(prefix="hjd_dropin_multi_")
+    try:
+        files = []
+        for i, n in enumerate(names):
+            files.append(os.path.join(tmp, f"{i}.jpg"))
+            shutil.copy(os.path.join(O.GOLDEN, n + ".jpg"), files[-1])
+        env = dict(os.environ, HJD_COMPAT_STATS="1")
+        r = subprocess.run([DROPIN, *files], cwd=tmp, capture_output=True, text=True, timeout=120, env=env)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    stats = [dict(kv.split("=", 1) for kv in l.split()[1:]) for l in r.stderr.splitlines()
+             if l.startswith("[hjd-compat]")]
+    assert [int(s["image"]) for s in stats] == [1, 2, 3, 4], r.stderr[-2000:]
+    allocs = [int(s["allocs"]) for s in stats]
+    plans = [int(s["plans_built"]) for s in stats]
+    assert allocs[0] >= 2 and allocs[1:] == [0, 0, 0], allocs     # growth only: image 1 is the largest
+    assert plans == [1, 1, 0, 1], plans                              # plan cache hit for the repeated geometry
+    for n, s in zip(names, stats):
+        c = O.load_case(n)
+        assert int(s["fnv"], 16) == _fnv1a(np.ascontiguousarray(c["bgrx"]).tobytes()), n
