@@ -365,9 +365,16 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
         st = hjd.JpegStream(ctx, max_blocks, nslots=nthreads + 4, nthreads=nthreads)
         stat_key = "host_decode_ns"
 
-    # ctypes views of the pool made once: submit() then passes pointers (no per-call copy)
-    from ocljpegdecoder_amd.jpeg import _buf
-    pool_c = [_buf(d) for d in pool]
+    # the pool is held the way a loader would read files: into pinned host memory
+    # (HJD_STREAM_PINNED=1, default), so the scans go to the GPU raw and are
+    # destuffed there -- the host parses headers only; with 0, pageable ctypes
+    # buffers take the host destuff path.  Made once: submit() passes pointers.
+    pinned_pool = gpu_entropy and os.environ.get("HJD_STREAM_PINNED", "1") == "1"
+    if pinned_pool:
+        pool_c = [hjd.pinned_bytes(d) for d in pool]
+    else:
+        from ocljpegdecoder_amd.jpeg import _buf
+        pool_c = [_buf(d) for d in pool]
     G = nf * world
     mine = shard.shard_round_robin(G, rank, world)        # this rank's positions within every step
 
@@ -392,6 +399,7 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
         dist.barrier()
     wall = time.perf_counter() - t0
     host_ns = after[stat_key] - before[stat_key]
+    host_scan = after.get("host_scan_bytes", 0) - before.get("host_scan_bytes", 0)
     wall_max = shard.aggregate({"seconds": wall})["seconds"]   # max over ranks
     px = nf * w * h * args.steps * world
 
@@ -444,6 +452,9 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
                 ("host_prep_Mpx_per_thread_s" if gpu_entropy else "host_huffman_Mpx_per_thread_s"):
                     round(nf * args.steps * w * h / (host_ns / 1e9) / 1e6, 1) if host_ns else None,
                 "jpeg_GBps_in": round(nf * args.steps * jpeg_bytes * world / wall_max / 1e9, 2),
+                "destuff": ("gpu (pinned JPEG pool, raw scans DMA'd)" if pinned_pool else "host (pageable pool)")
+                           if gpu_entropy else "n/a (host Huffman)",
+                "host_scan_bytes_per_frame": round(host_scan / (nf * args.steps), 1) if gpu_entropy else None,
                 "output_checked_vs_oracle": bool(ok)},
             "stream_check": {"frames_checked": int(agg["frames_checked"]), "checksum": int(agg["checksum"]),
                              "checksum_oracle": int(agg["checksum_oracle"]), "id_sum": int(agg["id_sum"]),

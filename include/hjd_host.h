@@ -155,6 +155,18 @@ int hjd_gstream_sync(hjd_gstream* s, int64_t stats[5]);
  * 3 bytes per pixel.  Only between hjd_gstream_sync and the next submit
  * (HJD_E_STATE otherwise). */
 int hjd_gstream_set_output_format(hjd_gstream* s, int out_format);
+/* Scan bytes the host CPU has read + written so far (destuffing into pinned
+ * staging: 2 per scan byte; a frame whose bytes are pinned host memory is
+ * destuffed on the GPU and costs 0: only its header is parsed on the host). */
+int hjd_gstream_host_bytes(hjd_gstream* s, int64_t* host_scan_bytes);
+
+/* Pin (page-lock) a caller's host range so the GPU can DMA from it: JPEG bytes
+ * in pinned memory (this, or hipHostMalloc) reach the device raw and are
+ * destuffed there (HJD_DESTUFF=auto, the default; "host" / "device" force one
+ * path).  The range must stay registered while frames submitted from it are in
+ * flight (until hjd_gstream_sync / hjd_gdec_sync). */
+int hjd_host_register(void* ptr, size_t size);
+int hjd_host_unregister(void* ptr);
 
 /* The 54-byte header of the reference's output BMP (src/decoder.cpp:372-394):
  * 32 bpp, top-down; the file is this header followed by the W*H*4 BGRX bytes. */
@@ -166,6 +178,13 @@ int hjd_bmp_header_bgr24(int32_t width, int32_t height, uint8_t header[54]);
 
 /* Test hook (no GPU): runs the same parallel algorithm on the host, one frame,
  * and writes its coefficients.  Not a decode path. */
+/* Destuff step alone (test hooks): the host routine, and the device kernels on
+ * one raw scan of n bytes with nseg restart intervals expected (out: >= n+64
+ * bytes; status: kStatusCorrupt bit 2 for malformed scans). */
+int hjd_debug_destuff_host(const uint8_t* scan, size_t n, uint8_t* out, size_t cap, uint32_t* seg_end, int max_seg,
+                           int* nseg, int64_t* out_bytes);
+int hjd_debug_destuff_gpu(hjd_ctx* ctx, const uint8_t* scan, size_t n, int nseg, uint8_t* out, size_t cap,
+                          uint32_t* seg_end, int64_t* out_bytes, uint32_t* status);
 int hjd_debug_entropy_emulate(const uint8_t* data, size_t size, int sub_bits, int16_t* coefs, int64_t capacity_blocks,
                               int32_t* status);
 

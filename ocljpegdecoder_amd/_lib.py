@@ -147,6 +147,15 @@ def _bind_host(lib):
         "hjd_bmp_header": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, u8p]),
         "hjd_bmp_header_bgr24": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, u8p]),
         "hjd_gstream_set_output_format": (ctypes.c_int, [vp, ctypes.c_int]),
+        "hjd_gstream_host_bytes": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int64)]),
+        "hjd_host_register": (ctypes.c_int, [vp, ctypes.c_size_t]),
+        "hjd_host_unregister": (ctypes.c_int, [vp]),
+        "hjd_debug_destuff_host": (ctypes.c_int, [u8p, ctypes.c_size_t, u8p, ctypes.c_size_t,
+                                                  ctypes.POINTER(ctypes.c_uint32), ctypes.c_int,
+                                                  ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int64)]),
+        "hjd_debug_destuff_gpu": (ctypes.c_int, [vp, u8p, ctypes.c_size_t, ctypes.c_int, u8p, ctypes.c_size_t,
+                                                 ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int64),
+                                                 ctypes.POINTER(ctypes.c_uint32)]),
         "hjd_stream_set_output_format": (ctypes.c_int, [vp, ctypes.c_int]),
         "hjd_gstream_sync": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int64)]),
         "hjd_debug_entropy_emulate": (ctypes.c_int, [u8p, ctypes.c_size_t, ctypes.c_int,

@@ -148,9 +148,18 @@ struct Prepared {
     int32_t qt[3][64];         // zigzag
     void* d_out = nullptr;
     int32_t pitch = 0;
+    // device destuff: the raw scan goes to the device (data_bits is then the
+    // raw upper bound until destuff_scan_kernel writes the real length)
+    int destuff = 0;           // kDestuffHost / kDestuffFromCaller / kDestuffFromStaging
+    const uint8_t* raw_src = nullptr;   // caller's pinned bytes (kDestuffFromCaller)
+    uint32_t raw_len = 0;
 };
 
-int prepare(const uint8_t* data, size_t size, uint8_t* dst, size_t cap, Prepared& pf)
+constexpr int kDestuffHost = 0;          // memchr/memcpy destuff into pinned staging (destuff() above)
+constexpr int kDestuffFromCaller = 1;    // raw bytes DMA'd from the caller's pinned buffer, destuffed on the GPU
+constexpr int kDestuffFromStaging = 2;   // raw bytes memcpy'd into pinned staging, destuffed on the GPU
+
+int prepare(const uint8_t* data, size_t size, uint8_t* dst, size_t cap, Prepared& pf, int mode = kDestuffHost)
 {
     hjd_internal::ScanHeader h;
     int rc = hjd_internal::parse_scan_header(data, size, &h);
@@ -184,6 +193,26 @@ int prepare(const uint8_t* data, size_t size, uint8_t* dst, size_t cap, Prepared
     }
     size_t len = 0;
     if (h.scan_offset > size) return set_error(HJD_E_INVALID, "scan offset past the end of the file");
+    if (mode != kDestuffHost) {
+        // the header is all the host reads; the GPU finds stuffing, markers and the scan's end
+        const size_t raw = size - h.scan_offset;
+        if (raw == 0) return set_error(HJD_E_INVALID, "empty scan");
+        if (raw >= (1u << 28)) return set_error(HJD_E_INVALID, "scan too large for one frame (>= 256 MiB)");
+        if (raw > cap) return set_error(HJD_E_INVALID, "scan larger than the staging capacity");
+        if (h.nblocks >= (1ll << 31)) return set_error(HJD_E_INVALID, "frame too large");
+        const int64_t nmcu = static_cast<int64_t>(h.mcu_w) * h.mcu_h;
+        const int64_t want = h.restart_interval > 0 ? (nmcu + h.restart_interval - 1) / h.restart_interval : 1;
+        if (want > raw / 2 + 1) return set_error(HJD_E_INVALID, "%lld restart intervals cannot fit %zu scan bytes",
+                                                 static_cast<long long>(want), raw);
+        pf.seg_end.assign(static_cast<size_t>(want), 0u);   // filled on the device
+        pf.destuff = mode;
+        pf.raw_len = static_cast<uint32_t>(raw);
+        pf.raw_src = data + h.scan_offset;
+        if (mode == kDestuffFromStaging) memcpy(dst, pf.raw_src, raw);
+        pf.data_bits = static_cast<uint32_t>(raw * 8);      // upper bound (groups are laid out for it)
+        return HJD_OK;
+    }
+    pf.raw_len = static_cast<uint32_t>(std::min<size_t>(size - h.scan_offset, 0xFFFFFFFFu));   // bytes the host reads
     rc = destuff(data + h.scan_offset, data + size, dst, cap, pf.seg_end, len);
     if (rc) return rc;
     if (len == 0) return set_error(HJD_E_INVALID, "empty scan");
@@ -199,6 +228,24 @@ int prepare(const uint8_t* data, size_t size, uint8_t* dst, size_t cap, Prepared
     return HJD_OK;
 }
 
+// Device destuff ("Destuff on the GPU").  A frame whose scan
+// bytes reach the device raw (straight from the caller's pinned buffer, or
+// copied into pinned staging) is destuffed by three kernels over 16-KiB tiles:
+// count -> per-frame scan -> write.  Its destuffed bit string lands where a
+// host-destuffed frame's would, at data_off of the data area, so the entropy
+// kernels are unchanged; the host only parses the header.
+constexpr uint32_t kTileBytes = 16384;
+constexpr int kTileThreads = 256;
+constexpr uint32_t kThreadBytes = kTileBytes / kTileThreads;   // 64 contiguous bytes per thread
+constexpr uint32_t kNoEnd = 0xFFFFFFFFu;
+
+struct RawFrame {          // one per frame of a batch (16 B)
+    uint32_t raw_len;      // scan bytes from the end of the SOS header to the end of the file
+    uint32_t tile_base;    // first tile of the frame
+    uint32_t ntiles;       // 0: destuffed on the host
+    uint32_t end;          // raw offset where the scan ends (destuff_scan_kernel)
+};
+
 // ---------------------------------------------------------------------------
 // Batch layout.  The header (frames | tables | segment ends | group->frame map |
 // pixel-kernel records | natural-order qtables) is laid out compactly per batch
@@ -209,7 +256,7 @@ struct Caps {
     int max_frames;
     int64_t max_scan_bytes, max_blocks;
     int sub_bits;
-    int64_t max_subs, max_wgs, max_segs;
+    int64_t max_subs, max_wgs, max_segs, max_tiles;
     size_t hdr_cap, data;
 };
 
@@ -223,14 +270,17 @@ Caps make_caps(int max_frames, int64_t max_scan_bytes, int64_t max_blocks, int s
     c.max_subs = (max_scan_bytes * 8 + sub_bits - 1) / sub_bits + max_frames;
     c.max_wgs = (c.max_subs + kOwn - 1) / kOwn + max_frames;
     c.max_segs = max_blocks / 3 + max_frames;
-    const size_t per_frame = sizeof(EntFrame) + sizeof(HuffLut) * kMaxTables + sizeof(FrameRecord) + 192 * 4;
-    c.hdr_cap = align_up(per_frame * max_frames + 4 * static_cast<size_t>(c.max_segs + c.max_wgs) + 8 * kAlign, kAlign);
+    c.max_tiles = max_scan_bytes / kTileBytes + max_frames;
+    const size_t per_frame = sizeof(EntFrame) + sizeof(HuffLut) * kMaxTables + sizeof(FrameRecord) + 192 * 4 +
+                             sizeof(RawFrame);
+    c.hdr_cap = align_up(per_frame * max_frames + 4 * static_cast<size_t>(c.max_segs + c.max_wgs + c.max_tiles) +
+                             10 * kAlign, kAlign);
     c.data = c.hdr_cap;
     return c;
 }
 
 struct HdrOffsets {
-    size_t frames, tabs, seg, wg, recs, qt, used;
+    size_t frames, tabs, seg, wg, recs, qt, rawf, tilef, used;
 };
 
 // Device-side view of a batch (kernel argument).
@@ -248,6 +298,12 @@ struct EntBatchDev {
     uint32_t* status;
     int16_t* coefs;
     uint32_t nframes, nwg, sub_bits, ntab_max;   // ntab_max: tables of the largest frame (dynamic LDS)
+    // device destuff (ntiles == 0: every frame of the batch was destuffed on the host)
+    const uint8_t* raw;          // raw scan bytes, frame f at frames[f].data_off
+    RawFrame* rawf;              // [nframes]
+    const uint32_t* tile_frame;  // [ntiles] frame of each tile
+    uint32_t* tiles;             // [3][ntiles] scratch: emitted bytes, markers, end (then offsets)
+    uint32_t ntiles;
 };
 
 // `blocks`: the frame's block_info() records (fill_blocks), LDS on the device.
@@ -362,6 +418,8 @@ __global__ __launch_bounds__(kGroupSubs) void ent_sync_kernel(EntBatchDev b)
     const EntFrame F = b.frames[f];
     const uint32_t gl = w - F.wg_base;
     const uint32_t S = b.sub_bits;
+    // groups laid out for a device-destuffed frame's upper bound (raw bytes) past its real end
+    if (gl >= frame_groups(F.nsub)) return;
     __shared__ BlockInfo blocks[kMaxBpm];
     const RunCtx c = make_ctx(b, F, tabs, blocks);
     load_tables(tabs, blocks, b.tabs + F.tab_base, F, b.frames + f, tid, kGroupSubs);
@@ -485,7 +543,7 @@ __global__ __launch_bounds__(256) void ent_link_kernel(EntBatchDev b)
     const uint32_t f = b.wg_frame[w];
     const EntFrame F = b.frames[f];
     const uint32_t gl = w - F.wg_base;
-    if (gl == 0) {
+    if (gl == 0 || gl >= frame_groups(F.nsub)) {   // first group, or past a device-destuffed frame's end
         b.linked[w] = 1;
         return;
     }
@@ -566,6 +624,7 @@ __global__ __launch_bounds__(kGroupSubs) void ent_write_kernel(EntBatchDev b)
     const EntFrame F = b.frames[f];
     const uint32_t gl = w - F.wg_base;
     const uint32_t S = b.sub_bits;
+    if (gl >= frame_groups(F.nsub)) return;
     __shared__ BlockInfo blocks[kMaxBpm];
     load_tables(tabs, blocks, b.tabs + F.tab_base, F, b.frames + f, tid, kGroupSubs);
     // block index / DC predictors at this group's start: all previous groups of the frame
@@ -599,6 +658,315 @@ __global__ __launch_bounds__(kGroupSubs) void ent_write_kernel(EntBatchDev b)
     uint32_t bad = (st.flags & kError) ? kStatusCorrupt : 0;
     if (ku == F.nsub - 1 && excl.nblk + st.nblk < F.nblocks) bad |= kStatusCount;
     if (bad) atomicOr(&b.status[f], bad);
+}
+
+// ---------------------------------------------------------------------------
+// Device destuff kernels.  The byte rules restate destuff() above (and T.81
+// B.1.1.5 / F.1.2.3): every 0xFF is the first byte of a pair, so the fate of
+// byte i depends only on (r[i-1], r[i], r[i+1]):
+//   r[i] = FF: next 00 -> emit FF (stuffing); next FF -> drop (fill byte);
+//              next D0..D7 -> drop, restart marker; no next byte or any other
+//              next -> the scan ends here (EOI or another marker);
+//   r[i] != FF after an FF: drop (the 00 of a stuffed pair, or RSTn's code);
+//   otherwise emit r[i].
+// ---------------------------------------------------------------------------
+
+// Work split: a 256-thread group takes a 16-KiB tile in 4 passes; in pass p
+// thread t takes the 16 bytes at p*4096 + 16t (one coalesced dwordx4 per lane).
+// A lane classifies its 16 bytes with word-parallel tests: a 16-bit mask of
+// 0xFF bytes, then a loop over those bytes only (0-1 per lane at q90: a 0xFF
+// is ~1 byte in 256), giving a drop mask, a marker mask and the scan's end.
+constexpr int kPasses = static_cast<int>(kTileBytes / (16 * kTileThreads));   // 4
+
+struct Lane16 {
+    uint64_t lo, hi;          // the 16 bytes, little-endian (byte 0 = first in the stream)
+    uint32_t drop;            // bytes removed (stuffing 00, fill FF, RSTn pairs, everything from the end on)
+    uint32_t marks;           // bit k: an RSTn pair starts at byte k
+    uint32_t end;             // frame offset of the scan's end if it lies in these bytes, else kNoEnd
+};
+
+__device__ __forceinline__ uint32_t ff_mask4(uint32_t w)
+{
+    const uint32_t t = ~w;   // FF bytes -> 00; exact zero-byte test
+    const uint32_t z = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t | 0x7F7F7F7Fu);
+    return ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
+}
+
+__device__ __forceinline__ uint32_t byte_at(const Lane16& v, uint32_t k)
+{
+    return static_cast<uint32_t>((k < 8 ? v.lo >> (8 * k) : v.hi >> (8 * (k - 8))) & 0xFFu);
+}
+
+// Classify the 16 bytes at frame offset s (16-B aligned); bytes at or past
+// `lim` (the frame's raw length, or the known scan end) are dropped.
+__device__ __forceinline__ Lane16 classify16(const uint8_t* r, uint32_t s, uint32_t len, uint32_t lim)
+{
+    Lane16 v;
+    const u32x4 q = *reinterpret_cast<const u32x4*>(r + s);
+    v.lo = static_cast<uint64_t>(q.x) | (static_cast<uint64_t>(q.y) << 32);
+    v.hi = static_cast<uint64_t>(q.z) | (static_cast<uint64_t>(q.w) << 32);
+    v.marks = 0;
+    v.end = kNoEnd;
+    uint32_t drop = 0;
+    if (s >= lim) {
+        v.drop = 0xFFFFu;
+        return v;
+    }
+    if (lim - s < 16) drop = 0xFFFFu & ~((1u << (lim - s)) - 1u);
+    uint32_t ff = ff_mask4(q.x) | (ff_mask4(q.y) << 4) | (ff_mask4(q.z) << 8) | (ff_mask4(q.w) << 12);
+    const uint32_t prev = s > 0 ? r[s - 1] : 0u;
+    if (prev == 0xFFu && !(ff & 1u)) drop |= 1u;   // second byte of a pair begun in the previous 16
+    if (ff) {
+        const uint32_t next16 = s + 16 < len ? r[s + 16] : 0u;
+        while (ff) {
+            const uint32_t k = __builtin_ctz(ff);
+            ff &= ff - 1u;
+            if (s + k >= lim) break;
+            const bool has_next = s + k + 1 < len;
+            const uint32_t nb = k < 15 ? byte_at(v, k + 1) : next16;
+            const uint32_t pair = k < 15 ? 3u << k : 1u << k;   // this FF and its second byte, if in these 16
+            if (has_next && nb == 0x00u) {
+                drop |= (pair & ~(1u << k));                     // FF kept, 00 dropped
+            } else if (has_next && nb == 0xFFu) {
+                drop |= 1u << k;                                 // fill byte; the next FF leads a pair
+            } else if (has_next && nb >= 0xD0u && nb <= 0xD7u) {
+                drop |= pair;
+                v.marks |= 1u << k;
+            } else {                                             // EOI, another marker, or FF at the very end
+                v.end = s + k;
+                drop |= 0xFFFFu & ~((1u << k) - 1u);
+                break;
+            }
+        }
+    }
+    v.drop = drop;
+    return v;
+}
+
+// Pack the kept bytes of v to its low end (lowest first); returns their count.
+__device__ __forceinline__ uint32_t compact16(Lane16& v)
+{
+    const uint32_t keep = ~v.drop & 0xFFFFu;
+    const uint32_t n = __builtin_popcount(keep);
+    if (n == 16) return n;
+    // drops below the highest kept byte need a shift; process them from the top down
+    uint32_t holes = v.drop & ((keep ? (2u << (31 - __builtin_clz(keep))) : 1u) - 1u);
+    while (holes) {
+        const uint32_t k = 31 - __builtin_clz(holes);
+        holes &= ~(1u << k);
+        if (k >= 8) {
+            const uint32_t j = k - 8;
+            const uint64_t low = j ? (~0ull >> (64 - 8 * j)) : 0ull;
+            v.hi = (v.hi & low) | ((v.hi >> 8) & ~low);
+        } else {
+            const uint64_t low = k ? (~0ull >> (64 - 8 * k)) : 0ull;
+            v.lo = (v.lo & low) | ((v.lo >> 8) & ~low) | (v.hi << 56);
+            v.hi >>= 8;
+        }
+    }
+    return n;
+}
+
+// Block-wide exclusive scan of two counters (256 threads); returns the totals.
+__device__ __forceinline__ void block_scan2(uint32_t& a, uint32_t& b2, uint32_t& tot_a, uint32_t& tot_b, uint32_t* sa,
+                                            uint32_t* sb)
+{
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    uint32_t xa = a, xb = b2;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t ya = __shfl_up(xa, d), yb = __shfl_up(xb, d);
+        if (lane >= d) { xa += ya; xb += yb; }
+    }
+    if (lane == 63) { sa[wv] = xa; sb[wv] = xb; }
+    __syncthreads();
+    uint32_t ba = 0, bb = 0;
+    for (int i = 0; i < wv; ++i) { ba += sa[i]; bb += sb[i]; }
+    tot_a = sa[0] + sa[1] + sa[2] + sa[3];
+    tot_b = sb[0] + sb[1] + sb[2] + sb[3];
+    a = ba + xa - a;     // exclusive
+    b2 = bb + xb - b2;
+    __syncthreads();
+}
+
+__device__ __forceinline__ uint32_t lane_offset(uint32_t t, int p)
+{
+    return static_cast<uint32_t>(p) * (16u * kTileThreads) + 16u * t;
+}
+
+__global__ __launch_bounds__(kTileThreads) void destuff_count_kernel(EntBatchDev b)
+{
+    __shared__ uint32_t s_end, sa[4], sb[4];
+    const uint32_t t = blockIdx.x;
+    const uint32_t f = b.tile_frame[t];
+    const RawFrame R = b.rawf[f];
+    const uint8_t* r = b.raw + b.frames[f].data_off;
+    const uint32_t s0 = (t - R.tile_base) * kTileBytes;
+    if (threadIdx.x == 0) s_end = kNoEnd;
+    __syncthreads();
+    uint32_t ne[kPasses], nm[kPasses], end = kNoEnd;
+#pragma unroll
+    for (int p = 0; p < kPasses; ++p) {
+        const uint32_t s = s0 + lane_offset(threadIdx.x, p);
+        const Lane16 v = classify16(r, s, R.raw_len, R.raw_len);
+        ne[p] = __builtin_popcount(~v.drop & 0xFFFFu);
+        nm[p] = __builtin_popcount(v.marks);
+        end = min(end, v.end);
+    }
+    if (end != kNoEnd) atomicMin(&s_end, end);
+    __syncthreads();
+    const uint32_t tile_end = s_end;
+    uint32_t te = 0, tm = 0;
+#pragma unroll
+    for (int p = 0; p < kPasses; ++p)          // what lies past the scan's end does not count
+        if (s0 + lane_offset(threadIdx.x, p) <= tile_end) { te += ne[p]; tm += nm[p]; }
+    uint32_t x = te, y = tm;
+    block_scan2(x, y, te, tm, sa, sb);
+    if (threadIdx.x == 0) {
+        b.tiles[t] = te;
+        b.tiles[b.ntiles + t] = tm;
+        b.tiles[2 * b.ntiles + t] = tile_end;
+    }
+}
+
+// One group per frame: tile offsets (exclusive scans), the frame's length,
+// subsequence count, segment table tail and read-ahead pad; malformed scans
+// are flagged kStatusCorrupt (what destuff()/prepare() reject on the host).
+__global__ __launch_bounds__(kTileThreads) void destuff_scan_kernel(EntBatchDev b)
+{
+    __shared__ uint32_t sa[4], sb[4], s_stop;
+    const uint32_t f = blockIdx.x;
+    RawFrame& R = b.rawf[f];
+    if (R.ntiles == 0) return;
+    EntFrame& F = const_cast<EntFrame*>(b.frames)[f];
+    const int tid = threadIdx.x;
+    uint32_t carry_e = 0, carry_m = 0, end = kNoEnd;
+    for (uint32_t c0 = 0; c0 < R.ntiles; c0 += kTileThreads) {
+        const uint32_t j = c0 + tid;
+        const uint32_t t = R.tile_base + j;
+        uint32_t e = 0, m = 0, te = kNoEnd;
+        if (j < R.ntiles) {
+            e = b.tiles[t];
+            m = b.tiles[b.ntiles + t];
+            te = b.tiles[2 * b.ntiles + t];
+        }
+        if (tid == 0) s_stop = kNoEnd;
+        __syncthreads();
+        if (te != kNoEnd) atomicMin(&s_stop, j);     // first tile of the chunk holding the scan's end
+        __syncthreads();
+        const uint32_t stop = s_stop;
+        if (j > stop) e = m = 0;
+        uint32_t xe = e, xm = m, tot_e, tot_m;
+        block_scan2(xe, xm, tot_e, tot_m, sa, sb);
+        if (j < R.ntiles) {
+            b.tiles[t] = carry_e + xe;               // byte offset of the tile's output
+            b.tiles[b.ntiles + t] = carry_m + xm;    // index of its first marker
+        }
+        carry_e += tot_e;
+        carry_m += tot_m;
+        if (stop != kNoEnd) {
+            if (tid == 0) s_stop = b.tiles[2 * b.ntiles + R.tile_base + stop];
+            __syncthreads();
+            end = s_stop;
+            break;
+        }
+    }
+    const uint32_t total = carry_e, markers = carry_m;
+    const uint32_t bits = total * 8;
+    uint32_t* seg = const_cast<uint32_t*>(b.seg_end) + F.seg_base;
+    for (uint32_t k = min(markers, F.nseg - 1) + tid; k < F.nseg; k += kTileThreads) seg[k] = bits;
+    uint8_t* out = const_cast<uint8_t*>(b.data) + F.data_off + total;
+    if (tid < static_cast<int>(kDataPad)) out[tid] = 0xFF;
+    if (tid == 0) {
+        R.end = end == kNoEnd ? R.raw_len : end;
+        F.data_bits = bits;
+        F.nsub = (bits + b.sub_bits - 1) / b.sub_bits;
+        if (total == 0 || total >= (1u << 28) || markers != F.nseg - 1) atomicOr(&b.status[f], kStatusCorrupt);
+    }
+}
+
+__global__ __launch_bounds__(kTileThreads) void destuff_write_kernel(EntBatchDev b)
+{
+    __shared__ uint32_t sa[4], sb[4];
+    __shared__ uint32_t stage[kTileBytes / 4 + 8];      // output bytes of the tile, word-aligned to the output
+    const uint32_t t = blockIdx.x;
+    const uint32_t f = b.tile_frame[t];
+    const RawFrame R = b.rawf[f];
+    const EntFrame F = b.frames[f];
+    const uint8_t* r = b.raw + F.data_off;
+    const uint32_t s0 = (t - R.tile_base) * kTileBytes;
+    const uint32_t tile_out = b.tiles[t];
+    uint32_t mark_base = b.tiles[b.ntiles + t];
+    const uint32_t base = tile_out & ~3u;              // stage word 0 <-> output byte `base`
+    const uint32_t lo = tile_out - base;
+    for (uint32_t i = threadIdx.x; i < kTileBytes / 4 + 8; i += kTileThreads) stage[i] = 0u;
+    __syncthreads();
+    uint32_t* seg = const_cast<uint32_t*>(b.seg_end) + F.seg_base;
+    uint32_t out_pos = lo;                             // stage byte of this pass's first output
+#pragma unroll
+    for (int p = 0; p < kPasses; ++p) {
+        const uint32_t s = s0 + lane_offset(threadIdx.x, p);
+        Lane16 v = classify16(r, s, R.raw_len, R.end);
+        const uint32_t marks = v.marks;                // classify16 stops at the scan's end
+        const uint32_t kept_mask = ~v.drop & 0xFFFFu;
+        uint32_t n = __builtin_popcount(kept_mask), nm = __builtin_popcount(marks), pe, pm;
+        uint32_t xe = n, xm = nm;
+        block_scan2(xe, xm, pe, pm, sa, sb);
+        // restart markers: ordinal and the destuffed bit offset where the interval ends
+        uint32_t mm = marks, ord = mark_base + xm;
+        while (mm) {
+            const uint32_t k = __builtin_ctz(mm);
+            mm &= mm - 1u;
+            const uint32_t code = (k < 15 ? byte_at(v, k + 1) : r[s + 16]) - 0xD0u;
+            if (code != (ord & 7u)) atomicOr(b.status + f, kStatusCorrupt);   // RSTn out of order
+            if (ord + 1 < F.nseg)
+                seg[ord] = (tile_out + (out_pos - lo) + xe + __builtin_popcount(kept_mask & ((1u << k) - 1u))) * 8;
+            ++ord;
+        }
+        if (n) {   // the kept bytes, packed, OR-ed into the staged words they cover
+            compact16(v);
+            const uint32_t o = out_pos + xe;
+            const uint32_t sh = 8 * (o & 3u);
+            uint32_t w[5];
+            const uint32_t x0 = static_cast<uint32_t>(v.lo), x1 = static_cast<uint32_t>(v.lo >> 32);
+            const uint32_t x2 = static_cast<uint32_t>(v.hi), x3 = static_cast<uint32_t>(v.hi >> 32);
+            // mask off bytes past n before shifting (their content is stale)
+            uint32_t m0 = n >= 4 ? ~0u : (1u << (8 * n)) - 1u;
+            uint32_t m1 = n >= 8 ? ~0u : n <= 4 ? 0u : (1u << (8 * (n - 4))) - 1u;
+            uint32_t m2 = n >= 12 ? ~0u : n <= 8 ? 0u : (1u << (8 * (n - 8))) - 1u;
+            uint32_t m3 = n >= 16 ? ~0u : n <= 12 ? 0u : (1u << (8 * (n - 12))) - 1u;
+            const uint32_t y0 = x0 & m0, y1 = x1 & m1, y2 = x2 & m2, y3 = x3 & m3;
+            if (sh) {
+                w[0] = y0 << sh;
+                w[1] = (y1 << sh) | (y0 >> (32 - sh));
+                w[2] = (y2 << sh) | (y1 >> (32 - sh));
+                w[3] = (y3 << sh) | (y2 >> (32 - sh));
+                w[4] = y3 >> (32 - sh);
+            } else {
+                w[0] = y0; w[1] = y1; w[2] = y2; w[3] = y3; w[4] = 0u;
+            }
+            const uint32_t wbase = o >> 2, nw = (8 * n + sh + 31) / 32;
+#pragma unroll
+            for (int i = 0; i < 5; ++i)
+                if (static_cast<uint32_t>(i) < nw) atomicOr(&stage[wbase + i], w[i]);
+        }
+        out_pos += pe;
+        mark_base += pm;
+    }
+    __syncthreads();
+    // coalesced word stores; the partial words at the tile's two ends by bytes
+    uint8_t* out = const_cast<uint8_t*>(b.data) + F.data_off;
+    const uint32_t nbytes = out_pos;                   // = lo + the tile's output bytes
+    const uint32_t nwords = (nbytes + 3) / 4;
+    const uint8_t* sb8 = reinterpret_cast<const uint8_t*>(stage);
+    for (uint32_t i = threadIdx.x; i < nwords; i += kTileThreads) {
+        const uint32_t b0 = 4 * i, b1 = min(b0 + 4, nbytes);
+        if (b0 >= lo && b1 == b0 + 4) {
+            *reinterpret_cast<uint32_t*>(out + base + b0) = stage[i];
+        } else {
+            for (uint32_t k = max(b0, lo); k < b1; ++k) out[base + k] = sb8[k];
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -741,7 +1109,11 @@ struct hjd_gdec {
     uint32_t* d_status = nullptr;
     uint32_t* h_status = nullptr;       // pinned
     int16_t* d_coefs = nullptr;
+    uint8_t* d_raw = nullptr;           // raw scan bytes of device-destuffed frames (same offsets as the data area)
+    uint32_t* d_tiles = nullptr;        // destuff scratch [3][max_tiles]
     hipEvent_t staged = nullptr, done = nullptr;
+    int64_t last_h2d = 0;               // bytes the last issue moved host -> device
+    int64_t last_host_scan_bytes = 0;   // scan bytes the host CPU read + wrote for the staged frames
     bool pending = false;
     std::vector<Prepared> frames;
     size_t data_used = 0;
@@ -786,6 +1158,37 @@ int hjd_gdec::wait_staging()
     return HJD_OK;
 }
 
+namespace {
+
+// HJD_DESTUFF: "host" (always destuff on the host), "device" (always on the
+// GPU; unpinned bytes are memcpy'd raw into staging), default "auto": on the
+// GPU when the caller's bytes are pinned host memory (hipHostMalloc'd or
+// hipHostRegister'ed, e.g. hjd_host_register), so the host CPU never touches
+// the scan, on the host otherwise.
+int destuff_policy()
+{
+    const char* e = getenv("HJD_DESTUFF");   // read per frame (~100 ns): tests switch it in-process
+    if (e && !strcmp(e, "host")) return 0;
+    if (e && !strcmp(e, "device")) return 2;
+    return 1;
+}
+
+bool pinned_host(const void* p, size_t n)
+{
+    if (!p || !n) return false;
+    for (const void* q : {p, static_cast<const void*>(static_cast<const uint8_t*>(p) + n - 1)}) {
+        hipPointerAttribute_t a;
+        if (hipPointerGetAttributes(&a, q) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        if (a.type != hipMemoryTypeHost) return false;
+    }
+    return true;
+}
+
+}  // namespace
+
 int hjd_gdec::prepare_frame(int i, const uint8_t* data, size_t size, size_t data_off, size_t cap)
 {
     Prepared& p = frames[static_cast<size_t>(i)];
@@ -793,7 +1196,11 @@ int hjd_gdec::prepare_frame(int i, const uint8_t* data, size_t size, size_t data
     p.data_off = data_off;
     if (!data) return p.rc = set_error(HJD_E_INVALID, "frame %d: NULL data", i);
     if (cap <= kDataPad) return p.rc = set_error(HJD_E_INVALID, "scan bytes exceed the batch capacity");
-    int rc = prepare(data, size, data_area() + data_off, cap - kDataPad, p);
+    int mode = kDestuffHost;
+    const int pol = gpu ? destuff_policy() : 0;
+    if (pol == 2) mode = pinned_host(data, size) ? kDestuffFromCaller : kDestuffFromStaging;
+    else if (pol == 1 && pinned_host(data, size)) mode = kDestuffFromCaller;
+    int rc = prepare(data, size, data_area() + data_off, cap - kDataPad, p, mode);
     if (rc) return p.rc = rc;
     return HJD_OK;
 }
@@ -837,8 +1244,14 @@ int hjd_gdec::assemble(uint8_t* blob, int16_t* coefs, int64_t* block_offsets, vo
     o.wg = align_up(o.seg + 4 * nseg, kAlign);
     o.recs = align_up(o.wg + 4 * nwg, kAlign);
     o.qt = align_up(o.recs + (d_outs ? sizeof(FrameRecord) * n : 0), kAlign);
-    o.used = align_up(o.qt + (d_outs ? 192 * 4 * static_cast<size_t>(n) : 0), kAlign);
-    if (o.used > caps.hdr_cap) return set_error(HJD_E_INVALID, "batch header exceeds its capacity");
+    size_t ntiles = 0;
+    for (const Prepared& p : frames)
+        if (p.destuff != kDestuffHost) ntiles += (p.raw_len + kTileBytes - 1) / kTileBytes;
+    o.rawf = align_up(o.qt + (d_outs ? 192 * 4 * static_cast<size_t>(n) : 0), kAlign);
+    o.tilef = align_up(o.rawf + (ntiles ? sizeof(RawFrame) * n : 0), kAlign);
+    o.used = align_up(o.tilef + 4 * ntiles, kAlign);
+    if (o.used > caps.hdr_cap || ntiles > static_cast<size_t>(caps.max_tiles))
+        return set_error(HJD_E_INVALID, "batch header exceeds its capacity");
 
     EntFrame* ef = reinterpret_cast<EntFrame*>(h_stage + o.frames);
     HuffLut* tb = reinterpret_cast<HuffLut*>(h_stage + o.tabs);
@@ -919,6 +1332,26 @@ int hjd_gdec::assemble(uint8_t* blob, int16_t* coefs, int64_t* block_offsets, vo
         }
     }
 
+    d.ntiles = static_cast<uint32_t>(ntiles);
+    d.rawf = nullptr;
+    d.tile_frame = nullptr;
+    if (ntiles) {
+        RawFrame* rf = reinterpret_cast<RawFrame*>(h_stage + o.rawf);
+        uint32_t* tf = reinterpret_cast<uint32_t*>(h_stage + o.tilef);
+        uint32_t tbase = 0;
+        for (int i = 0; i < n; ++i) {
+            const Prepared& p = frames[i];
+            RawFrame r{p.raw_len, tbase, 0, 0};
+            if (p.destuff != kDestuffHost) {
+                r.ntiles = (p.raw_len + kTileBytes - 1) / kTileBytes;
+                for (uint32_t k = 0; k < r.ntiles; ++k) tf[tbase + k] = static_cast<uint32_t>(i);
+                tbase += r.ntiles;
+            }
+            rf[i] = r;
+        }
+        d.rawf = reinterpret_cast<RawFrame*>(blob + o.rawf);
+        d.tile_frame = reinterpret_cast<const uint32_t*>(blob + o.tilef);
+    }
     d.frames = reinterpret_cast<const EntFrame*>(blob + o.frames);
     d.tabs = reinterpret_cast<const HuffLut*>(blob + o.tabs);
     d.seg_end = reinterpret_cast<const uint32_t*>(blob + o.seg);
@@ -955,6 +1388,8 @@ int gdec_alloc(hjd_gdec* g)
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_agg), sizeof(SubStats) * static_cast<size_t>(g->caps.max_wgs)));
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_status), 4 * static_cast<size_t>(g->caps.max_frames)));
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_coefs), 128 * static_cast<size_t>(g->caps.max_blocks)));
+    HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_raw), g->data_cap()));
+    HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_tiles), 12 * static_cast<size_t>(g->caps.max_tiles)));
     HJD_HIP(hipEventCreateWithFlags(&g->staged, hipEventDisableTiming));
     HJD_HIP(hipEventCreateWithFlags(&g->done, hipEventDisableTiming));
     return HJD_OK;
@@ -965,6 +1400,14 @@ int launch_entropy(hjd_gdec* g, const EntBatchDev& b, hipStream_t s)
 {
     if (b.nwg == 0) return HJD_OK;
     HJD_HIP(hipMemsetAsync(g->d_status, 0, 4 * static_cast<size_t>(b.nframes), s));
+    if (b.ntiles) {
+        hipLaunchKernelGGL(destuff_count_kernel, dim3(b.ntiles), dim3(kTileThreads), 0, s, b);
+        HJD_HIP(hipGetLastError());
+        hipLaunchKernelGGL(destuff_scan_kernel, dim3(b.nframes), dim3(kTileThreads), 0, s, b);
+        HJD_HIP(hipGetLastError());
+        hipLaunchKernelGGL(destuff_write_kernel, dim3(b.ntiles), dim3(kTileThreads), 0, s, b);
+        HJD_HIP(hipGetLastError());
+    }
     hipLaunchKernelGGL(ent_sync_kernel, dim3(b.nwg), dim3(kGroupSubs), sync_lds_bytes(b.ntab_max), s, b);
     HJD_HIP(hipGetLastError());
     hipLaunchKernelGGL(ent_link_kernel, dim3((b.nwg + 255) / 256), dim3(256), 0, s, b);
@@ -1001,11 +1444,50 @@ int gdec_issue(hjd_gdec* g, void* const* d_outs, const int32_t* pitches, int16_t
     b.linked = g->d_linked;
     b.agg = g->d_agg;
     b.status = g->d_status;
+    b.raw = g->d_raw;
+    b.tiles = g->d_tiles;
     // the device buffers are reused: order this call after the previous one
     // (which may have been issued on another stream)
     if (g->pending) HJD_HIP(hipStreamWaitEvent(s, g->done, 0));
     HJD_HIP(hipMemcpyAsync(g->d_blob, g->h_stage, g->H.used, hipMemcpyHostToDevice, s));
-    HJD_HIP(hipMemcpyAsync(g->d_blob + g->caps.data, g->h_stage + g->caps.data, g->data_used, hipMemcpyHostToDevice, s));
+    // scan bytes: runs of consecutive frames staged the same way move in one copy
+    // (host-destuffed -> data area; raw in staging -> raw area); raw bytes in the
+    // caller's pinned memory go straight from there to the raw area.
+    int64_t moved = static_cast<int64_t>(g->H.used), host_bytes = 0;
+    std::vector<void*> bd, bs;          // caller-pinned raw scans: one batched DMA submission
+    std::vector<size_t> bn;
+    for (int i = 0; i < n;) {
+        const Prepared& p = g->frames[i];
+        const size_t len = p.destuff == kDestuffHost ? p.data_bits / 8 : p.raw_len;
+        host_bytes += p.destuff == kDestuffHost ? static_cast<int64_t>(p.raw_len) + static_cast<int64_t>(len)
+                    : p.destuff == kDestuffFromStaging ? 2 * static_cast<int64_t>(len) : 0;
+        if (p.destuff == kDestuffFromCaller) {
+            bd.push_back(g->d_raw + p.data_off);
+            bs.push_back(const_cast<uint8_t*>(p.raw_src));
+            bn.push_back(len);
+            moved += static_cast<int64_t>(len);
+            ++i;
+            continue;
+        }
+        int j = i + 1;
+        size_t hi = p.data_off + len + kDataPad;
+        while (j < n && g->frames[j].destuff == p.destuff) {
+            const Prepared& q = g->frames[j];
+            hi = q.data_off + (q.destuff == kDestuffHost ? q.data_bits / 8 : q.raw_len) + kDataPad;
+            host_bytes += q.destuff == kDestuffHost ? static_cast<int64_t>(q.raw_len) + q.data_bits / 8
+                                                    : 2 * static_cast<int64_t>(q.raw_len);
+            ++j;
+        }
+        uint8_t* dst = (p.destuff == kDestuffHost ? g->d_blob + g->caps.data : g->d_raw) + p.data_off;
+        HJD_HIP(hipMemcpyAsync(dst, g->h_stage + g->caps.data + p.data_off, hi - p.data_off, hipMemcpyHostToDevice, s));
+        moved += static_cast<int64_t>(hi - p.data_off);
+        i = j;
+    }
+    // (hipMemcpyBatchAsync would submit these at once, but the HIP runtime this
+    // library shares with PyTorch -- DESIGN.md s8 -- predates it)
+    for (size_t k = 0; k < bd.size(); ++k) HJD_HIP(hipMemcpyAsync(bd[k], bs[k], bn[k], hipMemcpyHostToDevice, s));
+    g->last_h2d = moved;
+    g->last_host_scan_bytes = host_bytes;
     HJD_HIP(hipEventRecord(g->staged, s));
     g->pending = true;
     rc = launch_entropy(g, b, s);
@@ -1108,7 +1590,8 @@ int hjd_gdec_destroy(hjd_gdec* g)
     if (g->done) (void)hipEventSynchronize(g->done);
     if (g->h_stage) (void)hipHostFree(g->h_stage);
     if (g->h_status) (void)hipHostFree(g->h_status);
-    void* dev[] = {g->d_blob, g->d_entries, g->d_stats, g->d_wentries, g->d_linked, g->d_agg, g->d_status, g->d_coefs};
+    void* dev[] = {g->d_blob, g->d_entries, g->d_stats, g->d_wentries, g->d_linked, g->d_agg, g->d_status, g->d_coefs,
+                   g->d_raw, g->d_tiles};
     for (void* p : dev)
         if (p) (void)hipFree(p);
     if (g->staged) (void)hipEventDestroy(g->staged);
@@ -1207,6 +1690,82 @@ int hjd_debug_entropy_syncstats(const uint8_t* data, size_t size, int sub_bits, 
         }
         hist[bin]++;
     }
+    return HJD_OK;
+}
+
+// Test hooks for the destuff step alone: the host routine (destuff()) and the
+// three device kernels on one raw scan, so arbitrary byte strings (stuffing,
+// fill bytes, RSTn in and out of order, truncation) can be compared directly.
+int hjd_debug_destuff_host(const uint8_t* scan, size_t n, uint8_t* out, size_t cap, uint32_t* seg_end, int max_seg,
+                           int* nseg, int64_t* out_bytes)
+{
+    if (!scan || !out || !seg_end || !nseg || !out_bytes) return set_error(HJD_E_INVALID, "NULL argument");
+    std::vector<uint32_t> seg;
+    size_t len = 0;
+    const int rc = destuff(scan, scan + n, out, cap, seg, len);
+    if (rc) return rc;
+    *nseg = static_cast<int>(seg.size());
+    for (int i = 0; i < static_cast<int>(seg.size()) && i < max_seg; ++i) seg_end[i] = seg[i];
+    *out_bytes = static_cast<int64_t>(len);
+    return HJD_OK;
+}
+
+int hjd_debug_destuff_gpu(hjd_ctx* ctx, const uint8_t* scan, size_t n, int nseg, uint8_t* out, size_t cap,
+                          uint32_t* seg_end, int64_t* out_bytes, uint32_t* status)
+{
+    if (!ctx || !scan || !out || !seg_end || !out_bytes || !status || n == 0 || nseg < 1 || cap < n + kDataPad)
+        return set_error(HJD_E_INVALID, "invalid destuff arguments");
+    HJD_HIP(hipSetDevice(hjd_ctx_device(ctx)));
+    const uint32_t ntiles = static_cast<uint32_t>((n + kTileBytes - 1) / kTileBytes);
+    const size_t area = align_up(n + kDataPad, 16);
+    EntFrame F;
+    memset(&F, 0, sizeof(F));
+    F.nseg = static_cast<uint32_t>(nseg);
+    F.data_bits = static_cast<uint32_t>(n * 8);
+    RawFrame R{static_cast<uint32_t>(n), 0, ntiles, 0};
+    std::vector<uint32_t> tf(ntiles, 0);
+    uint8_t *d_raw = nullptr, *d_out = nullptr;
+    EntFrame* d_f = nullptr;
+    RawFrame* d_r = nullptr;
+    uint32_t *d_tf = nullptr, *d_tiles = nullptr, *d_seg = nullptr, *d_status = nullptr;
+    hipError_t e = hipSuccess;
+    auto ok = [&](hipError_t x) { if (e == hipSuccess) e = x; return e == hipSuccess; };
+    if (ok(hipMalloc(&d_raw, area)) && ok(hipMalloc(&d_out, area)) && ok(hipMalloc(&d_f, sizeof(F))) &&
+        ok(hipMalloc(&d_r, sizeof(R))) && ok(hipMalloc(&d_tf, 4 * ntiles)) && ok(hipMalloc(&d_tiles, 12 * ntiles)) &&
+        ok(hipMalloc(&d_seg, 4 * static_cast<size_t>(nseg))) && ok(hipMalloc(&d_status, 4)) &&
+        ok(hipMemcpy(d_raw, scan, n, hipMemcpyHostToDevice)) && ok(hipMemcpy(d_f, &F, sizeof(F), hipMemcpyHostToDevice)) &&
+        ok(hipMemcpy(d_r, &R, sizeof(R), hipMemcpyHostToDevice)) &&
+        ok(hipMemcpy(d_tf, tf.data(), 4 * ntiles, hipMemcpyHostToDevice)) && ok(hipMemset(d_status, 0, 4)) &&
+        ok(hipMemset(d_seg, 0xEE, 4 * static_cast<size_t>(nseg))) && ok(hipMemset(d_out, 0xEE, area))) {
+        EntBatchDev b;
+        memset(&b, 0, sizeof(b));
+        b.frames = d_f;
+        b.seg_end = d_seg;
+        b.data = d_out;
+        b.status = d_status;
+        b.nframes = 1;
+        b.sub_bits = 4096;
+        b.raw = d_raw;
+        b.rawf = d_r;
+        b.tile_frame = d_tf;
+        b.tiles = d_tiles;
+        b.ntiles = ntiles;
+        hipLaunchKernelGGL(destuff_count_kernel, dim3(ntiles), dim3(kTileThreads), 0, 0, b);
+        hipLaunchKernelGGL(destuff_scan_kernel, dim3(1), dim3(kTileThreads), 0, 0, b);
+        hipLaunchKernelGGL(destuff_write_kernel, dim3(ntiles), dim3(kTileThreads), 0, 0, b);
+        EntFrame Fo;
+        if (ok(hipGetLastError()) && ok(hipDeviceSynchronize()) &&
+            ok(hipMemcpy(&Fo, d_f, sizeof(Fo), hipMemcpyDeviceToHost)) &&
+            ok(hipMemcpy(out, d_out, area, hipMemcpyDeviceToHost)) &&
+            ok(hipMemcpy(seg_end, d_seg, 4 * static_cast<size_t>(nseg), hipMemcpyDeviceToHost)) &&
+            ok(hipMemcpy(status, d_status, 4, hipMemcpyDeviceToHost)))
+            *out_bytes = Fo.data_bits / 8;
+    }
+    for (void* p : {static_cast<void*>(d_raw), static_cast<void*>(d_out), static_cast<void*>(d_f),
+                    static_cast<void*>(d_r), static_cast<void*>(d_tf), static_cast<void*>(d_tiles),
+                    static_cast<void*>(d_seg), static_cast<void*>(d_status)})
+        if (p) (void)hipFree(p);
+    if (e != hipSuccess) return set_error(HJD_E_HIP, "destuff test hook: %s", hipGetErrorString(e));
     return HJD_OK;
 }
 
@@ -1315,7 +1874,7 @@ struct hjd_gstream {
     std::vector<std::thread> workers;
     int64_t batches_in_flight = 0;     // created and not yet issued
 
-    std::atomic<int64_t> images{0}, pixels{0}, prep_ns{0}, h2d_bytes{0}, batches{0};
+    std::atomic<int64_t> images{0}, pixels{0}, prep_ns{0}, h2d_bytes{0}, batches{0}, host_scan_bytes{0};
     int first_error = HJD_OK;
     std::string first_error_msg;
     int local_cpus = 0;   // CPUs of the GPU's NUMA node the workers are bound to (0: unbound)
@@ -1414,7 +1973,8 @@ void hjd_gstream::issue_locked(GBatch* b)
     if (!g->frames.empty() && rc == HJD_OK) {
         rc = gdec_issue(g, outs.data(), pitches.data(), nullptr, nullptr, streams[b->slot], host.data());
         if (rc) record_error(rc, hjd_last_error());
-        h2d_bytes += static_cast<int64_t>(g->H.used + g->data_used);
+        h2d_bytes += g->last_h2d;
+        host_scan_bytes += g->last_host_scan_bytes;
         batches++;
     }
     b->issued = true;
@@ -1631,6 +2191,27 @@ int hjd_gstream_sync(hjd_gstream* st, int64_t stats[5])
         st->first_error = HJD_OK;
         return set_error(rc, "%s", st->first_error_msg.c_str());
     }
+    return HJD_OK;
+}
+
+int hjd_gstream_host_bytes(hjd_gstream* st, int64_t* host_scan_bytes)
+{
+    if (!st || !host_scan_bytes) return set_error(HJD_E_INVALID, "NULL argument");
+    *host_scan_bytes = st->host_scan_bytes;
+    return HJD_OK;
+}
+
+int hjd_host_register(void* ptr, size_t size)
+{
+    if (!ptr || !size) return set_error(HJD_E_INVALID, "NULL or empty host range");
+    HJD_HIP(hipHostRegister(ptr, size, hipHostRegisterDefault));
+    return HJD_OK;
+}
+
+int hjd_host_unregister(void* ptr)
+{
+    if (!ptr) return set_error(HJD_E_INVALID, "NULL host pointer");
+    HJD_HIP(hipHostUnregister(ptr));
     return HJD_OK;
 }
 

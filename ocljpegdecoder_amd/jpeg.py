@@ -167,11 +167,34 @@ class JpegStream:
             pass
 
 
-def _byte_arrays(datas: Sequence[bytes]):
-    bufs = [d if isinstance(d, ctypes.Array) else _buf(d) for d in datas]
-    arr_d = (_u8p * len(bufs))(*[ctypes.cast(b, _u8p) for b in bufs])
-    arr_s = (ctypes.c_size_t * len(bufs))(*[len(b) for b in bufs])
-    return bufs, arr_d, arr_s
+def pinned_bytes(data: bytes):
+    """The bytes in a pinned (page-locked) host tensor: JPEGs submitted from
+    pinned memory reach the GPU raw and are destuffed there (no host pass over
+    the scan; include/hjd_host.h hjd_host_register).  Keep the tensor alive
+    until the decoder's / stream's sync()."""
+    import torch
+    t = torch.empty(len(data), dtype=torch.uint8).pin_memory()
+    t.numpy()[:] = np.frombuffer(data, np.uint8)
+    return t
+
+
+def _ptr_size(d):
+    """(address, size) of bytes / ctypes array / (pinned) CPU uint8 tensor."""
+    if isinstance(d, ctypes.Array):
+        return ctypes.addressof(d), len(d), d
+    if hasattr(d, "data_ptr") and hasattr(d, "is_cuda"):
+        if d.is_cuda or not d.is_contiguous() or d.element_size() != 1:
+            raise ValueError("JPEG tensors must be contiguous uint8 host tensors")
+        return d.data_ptr(), d.numel(), d
+    b = _buf(d)
+    return ctypes.addressof(b), len(b), b
+
+
+def _byte_arrays(datas):
+    items = [_ptr_size(d) for d in datas]
+    arr_d = (_u8p * len(items))(*[ctypes.cast(a, _u8p) for a, _, _ in items])
+    arr_s = (ctypes.c_size_t * len(items))(*[n for _, n, _ in items])
+    return [k for _, _, k in items], arr_d, arr_s
 
 
 def _stream_handle(stream):
@@ -277,34 +300,37 @@ class GpuJpegStream:
     def submit(self, data: bytes, out, out_pitch: Optional[int] = None):
         """out: contiguous device tensor, or a (pinned) host tensor / numpy
         array -- then the pixels are copied back to host memory (D2H sink)."""
-        buf = _buf(data) if not isinstance(data, ctypes.Array) else data
-        self._keep.append(buf)
+        addr, size, keep = _ptr_size(data)
+        self._keep.append(keep)
+        src = ctypes.cast(addr, _u8p)
         if isinstance(out, np.ndarray):
             if not out.flags.c_contiguous:
                 raise ValueError("out must be C-contiguous")
             self._keep.append(out)
             pitch = out_pitch or out.shape[-1] * out.itemsize
-            check(self.lib.hjd_gstream_submit_host(self.handle, ctypes.cast(buf, _u8p), len(buf), out.ctypes.data,
-                                                   int(pitch)), "hjd_gstream_submit_host")
+            check(self.lib.hjd_gstream_submit_host(self.handle, src, size, out.ctypes.data, int(pitch)),
+                  "hjd_gstream_submit_host")
             return
         if not out.is_contiguous():
             raise ValueError("out must be contiguous")
         out_pitch = out_pitch or out.shape[-1] * out.element_size()
         if out.is_cuda:
-            check(self.lib.hjd_gstream_submit(self.handle, ctypes.cast(buf, _u8p), len(buf), out.data_ptr(),
-                                              int(out_pitch)), "hjd_gstream_submit")
+            check(self.lib.hjd_gstream_submit(self.handle, src, size, out.data_ptr(), int(out_pitch)),
+                  "hjd_gstream_submit")
         else:
             self._keep.append(out)
-            check(self.lib.hjd_gstream_submit_host(self.handle, ctypes.cast(buf, _u8p), len(buf), out.data_ptr(),
-                                                   int(out_pitch)), "hjd_gstream_submit_host")
+            check(self.lib.hjd_gstream_submit_host(self.handle, src, size, out.data_ptr(), int(out_pitch)),
+                  "hjd_gstream_submit_host")
 
     def sync(self) -> dict:
         stats = (ctypes.c_int64 * 5)()
         rc = self.lib.hjd_gstream_sync(self.handle, stats)
         self._keep.clear()
         check(rc, "hjd_gstream_sync")
+        hb = ctypes.c_int64(0)
+        check(self.lib.hjd_gstream_host_bytes(self.handle, ctypes.byref(hb)), "hjd_gstream_host_bytes")
         return {"images": stats[0], "pixels": stats[1], "host_prep_ns": stats[2], "h2d_bytes": stats[3],
-                "batches": stats[4]}
+                "batches": stats[4], "host_scan_bytes": hb.value}
 
     def close(self):
         if self.handle:

@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--sampling", default="420", choices=["420", "444"])
     ap.add_argument("--pool", type=int, default=8)
     ap.add_argument("--pixels", action="store_true", help="also run the fused pixel kernel (full decode)")
+    ap.add_argument("--pinned", action="store_true",
+                    help="JPEG bytes in pinned host memory (destuffed on the GPU unless HJD_DESTUFF=host)")
     ap.add_argument("--no-check", action="store_true",
                     help="timing experiments whose outputs are wrong by design (HJD_LIB variants)")
     args = ap.parse_args()
@@ -39,8 +41,12 @@ def main():
     pool = bench.encode_pool(w, h, s, args.pool, seed0=99)
     datas = [pool[i % len(pool)] for i in range(args.frames)]
     infos = [hjd.parse(d) for d in datas]
+    host_datas = datas
+    if args.pinned:
+        pinned = [hjd.pinned_bytes(d) for d in pool]
+        datas = [pinned[i % len(pool)] for i in range(args.frames)]
     nblk = sum(i.nblocks for i in infos)
-    scan = sum(len(d) for d in datas)
+    scan = sum(len(d) for d in host_datas)
     ctx = hjd.Context(0)
     dev = torch.device("cuda", 0)
     stream = torch.cuda.Stream(dev)
@@ -70,7 +76,7 @@ def main():
         gd.sync()
         got = coefs.cpu().numpy()
         for i in range(min(2, len(datas))):
-            ref, _ = hjd.decode_coefs(datas[i])
+            ref, _ = hjd.decode_coefs(host_datas[i])
             assert (got[offs[i]:offs[i] + infos[i].nblocks] == ref).all(), "GPU coefficients differ"
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
