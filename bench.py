@@ -371,7 +371,15 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
     # buffers take the host destuff path.  Made once: submit() passes pointers.
     pinned_pool = gpu_entropy and os.environ.get("HJD_STREAM_PINNED", "1") == "1"
     if pinned_pool:
-        pool_c = [hjd.pinned_bytes(d) for d in pool]
+        # one pinned arena, files back to back in id order (a loader's read-ahead ring):
+        # consecutive frames' scans then move to the GPU in one DMA per run
+        import torch as _t
+        arena = _t.empty(sum(len(d) for d in pool), dtype=_t.uint8).pin_memory()
+        pool_c, pos = [], 0
+        for d in pool:
+            arena[pos:pos + len(d)] = _t.frombuffer(bytearray(d), dtype=_t.uint8)
+            pool_c.append(arena[pos:pos + len(d)])
+            pos += len(d)
     else:
         from ocljpegdecoder_amd.jpeg import _buf
         pool_c = [_buf(d) for d in pool]

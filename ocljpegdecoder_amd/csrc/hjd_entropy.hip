@@ -153,13 +153,15 @@ struct Prepared {
     int destuff = 0;           // kDestuffHost / kDestuffFromCaller / kDestuffFromStaging
     const uint8_t* raw_src = nullptr;   // caller's pinned bytes (kDestuffFromCaller)
     uint32_t raw_len = 0;
+    uint64_t raw_off = 0;      // raw-area offset of the first scan byte (RawCursor::place)
 };
 
 constexpr int kDestuffHost = 0;          // memchr/memcpy destuff into pinned staging (destuff() above)
 constexpr int kDestuffFromCaller = 1;    // raw bytes DMA'd from the caller's pinned buffer, destuffed on the GPU
 constexpr int kDestuffFromStaging = 2;   // raw bytes memcpy'd into pinned staging, destuffed on the GPU
 
-int prepare(const uint8_t* data, size_t size, uint8_t* dst, size_t cap, Prepared& pf, int mode = kDestuffHost)
+int prepare(const uint8_t* data, size_t size, uint8_t* dst, size_t cap, Prepared& pf, int mode = kDestuffHost,
+            uint64_t raw_off = 0)
 {
     hjd_internal::ScanHeader h;
     int rc = hjd_internal::parse_scan_header(data, size, &h);
@@ -208,6 +210,7 @@ int prepare(const uint8_t* data, size_t size, uint8_t* dst, size_t cap, Prepared
         pf.destuff = mode;
         pf.raw_len = static_cast<uint32_t>(raw);
         pf.raw_src = data + h.scan_offset;
+        pf.raw_off = raw_off;
         if (mode == kDestuffFromStaging) memcpy(dst, pf.raw_src, raw);
         pf.data_bits = static_cast<uint32_t>(raw * 8);      // upper bound (groups are laid out for it)
         return HJD_OK;
@@ -239,11 +242,47 @@ constexpr int kTileThreads = 256;
 constexpr uint32_t kThreadBytes = kTileBytes / kTileThreads;   // 64 contiguous bytes per thread
 constexpr uint32_t kNoEnd = 0xFFFFFFFFu;
 
-struct RawFrame {          // one per frame of a batch (16 B)
+// The raw bytes of a frame sit at any byte offset of the raw area (so that
+// frames adjacent in the caller's memory stay adjacent there and move in one
+// DMA); the kernels address them from the 16-B aligned `raw_off - begin` in
+// "region" coordinates [0, begin + raw_len) and ignore the first `begin` bytes.
+struct RawFrame {          // one per frame of a batch (32 B)
+    uint64_t raw_off;      // raw area offset of the first scan byte
     uint32_t raw_len;      // scan bytes from the end of the SOS header to the end of the file
+    uint32_t begin;        // raw_off & 15
     uint32_t tile_base;    // first tile of the frame
     uint32_t ntiles;       // 0: destuffed on the host
-    uint32_t end;          // raw offset where the scan ends (destuff_scan_kernel)
+    uint32_t end;          // region offset where the scan ends (destuff_scan_kernel)
+    uint32_t pad;
+};
+static_assert(sizeof(RawFrame) == 32, "RawFrame layout");
+
+__host__ __device__ __forceinline__ uint32_t raw_region_len(uint32_t begin, uint32_t raw_len) { return begin + raw_len; }
+
+// Places raw scans in a batch's raw area.  A caller-pinned scan that follows
+// the previous one in the caller's memory within kMirrorGap bytes (a JPEG
+// header, typically) is placed at the same distance, so the run moves with one
+// DMA; anything else goes after the area in use, at the source's alignment mod 16.
+struct RawCursor {
+    static constexpr uint64_t kMirrorGap = 64 * 1024;
+    const uint8_t* last_src = nullptr;
+    uint64_t last_off = 0;
+    uint64_t end = 0;
+    bool place(const uint8_t* src, size_t n, bool mirror, size_t cap, uint64_t& off)
+    {
+        uint64_t o;
+        if (mirror && last_src && src > last_src && last_off + static_cast<uint64_t>(src - last_src) >= end &&
+            last_off + static_cast<uint64_t>(src - last_src) - end <= kMirrorGap)
+            o = last_off + static_cast<uint64_t>(src - last_src);
+        else
+            o = (end + 15) / 16 * 16 + (reinterpret_cast<uintptr_t>(src) & 15);
+        if (o + n + 32 > cap) return false;   // + the kernels' read-ahead inside the area
+        off = o;
+        end = o + n;
+        last_src = mirror ? src : nullptr;
+        last_off = o;
+        return true;
+    }
 };
 
 // ---------------------------------------------------------------------------
@@ -697,9 +736,10 @@ __device__ __forceinline__ uint32_t byte_at(const Lane16& v, uint32_t k)
     return static_cast<uint32_t>((k < 8 ? v.lo >> (8 * k) : v.hi >> (8 * (k - 8))) & 0xFFu);
 }
 
-// Classify the 16 bytes at frame offset s (16-B aligned); bytes at or past
-// `lim` (the frame's raw length, or the known scan end) are dropped.
-__device__ __forceinline__ Lane16 classify16(const uint8_t* r, uint32_t s, uint32_t len, uint32_t lim)
+// Classify the 16 region bytes at s (16-B aligned): bytes before `begin` (not
+// the scan's) and at or past `lim` (the region's length, or the known scan
+// end) are dropped.
+__device__ __forceinline__ Lane16 classify16(const uint8_t* r, uint32_t s, uint32_t begin, uint32_t len, uint32_t lim)
 {
     Lane16 v;
     const u32x4 q = *reinterpret_cast<const u32x4*>(r + s);
@@ -714,7 +754,12 @@ __device__ __forceinline__ Lane16 classify16(const uint8_t* r, uint32_t s, uint3
     }
     if (lim - s < 16) drop = 0xFFFFu & ~((1u << (lim - s)) - 1u);
     uint32_t ff = ff_mask4(q.x) | (ff_mask4(q.y) << 4) | (ff_mask4(q.z) << 8) | (ff_mask4(q.w) << 12);
-    const uint32_t prev = s > 0 ? r[s - 1] : 0u;
+    if (s < begin) {                                // only in a frame's first 16 bytes (begin < 16)
+        const uint32_t pre = (1u << (begin - s)) - 1u;
+        drop |= pre;
+        ff &= ~pre;
+    }
+    const uint32_t prev = s > begin ? r[s - 1] : 0u;
     if (prev == 0xFFu && !(ff & 1u)) drop |= 1u;   // second byte of a pair begun in the previous 16
     if (ff) {
         const uint32_t next16 = s + 16 < len ? r[s + 16] : 0u;
@@ -800,7 +845,8 @@ __global__ __launch_bounds__(kTileThreads) void destuff_count_kernel(EntBatchDev
     const uint32_t t = blockIdx.x;
     const uint32_t f = b.tile_frame[t];
     const RawFrame R = b.rawf[f];
-    const uint8_t* r = b.raw + b.frames[f].data_off;
+    const uint8_t* r = b.raw + (R.raw_off - R.begin);
+    const uint32_t L = raw_region_len(R.begin, R.raw_len);
     const uint32_t s0 = (t - R.tile_base) * kTileBytes;
     if (threadIdx.x == 0) s_end = kNoEnd;
     __syncthreads();
@@ -808,7 +854,7 @@ __global__ __launch_bounds__(kTileThreads) void destuff_count_kernel(EntBatchDev
 #pragma unroll
     for (int p = 0; p < kPasses; ++p) {
         const uint32_t s = s0 + lane_offset(threadIdx.x, p);
-        const Lane16 v = classify16(r, s, R.raw_len, R.raw_len);
+        const Lane16 v = classify16(r, s, R.begin, L, L);
         ne[p] = __builtin_popcount(~v.drop & 0xFFFFu);
         nm[p] = __builtin_popcount(v.marks);
         end = min(end, v.end);
@@ -878,7 +924,7 @@ __global__ __launch_bounds__(kTileThreads) void destuff_scan_kernel(EntBatchDev 
     uint8_t* out = const_cast<uint8_t*>(b.data) + F.data_off + total;
     if (tid < static_cast<int>(kDataPad)) out[tid] = 0xFF;
     if (tid == 0) {
-        R.end = end == kNoEnd ? R.raw_len : end;
+        R.end = end == kNoEnd ? raw_region_len(R.begin, R.raw_len) : end;
         F.data_bits = bits;
         F.nsub = (bits + b.sub_bits - 1) / b.sub_bits;
         if (total == 0 || total >= (1u << 28) || markers != F.nseg - 1) atomicOr(&b.status[f], kStatusCorrupt);
@@ -893,7 +939,8 @@ __global__ __launch_bounds__(kTileThreads) void destuff_write_kernel(EntBatchDev
     const uint32_t f = b.tile_frame[t];
     const RawFrame R = b.rawf[f];
     const EntFrame F = b.frames[f];
-    const uint8_t* r = b.raw + F.data_off;
+    const uint8_t* r = b.raw + (R.raw_off - R.begin);
+    const uint32_t L = raw_region_len(R.begin, R.raw_len);
     const uint32_t s0 = (t - R.tile_base) * kTileBytes;
     const uint32_t tile_out = b.tiles[t];
     uint32_t mark_base = b.tiles[b.ntiles + t];
@@ -906,7 +953,7 @@ __global__ __launch_bounds__(kTileThreads) void destuff_write_kernel(EntBatchDev
 #pragma unroll
     for (int p = 0; p < kPasses; ++p) {
         const uint32_t s = s0 + lane_offset(threadIdx.x, p);
-        Lane16 v = classify16(r, s, R.raw_len, R.end);
+        Lane16 v = classify16(r, s, R.begin, L, R.end);
         const uint32_t marks = v.marks;                // classify16 stops at the scan's end
         const uint32_t kept_mask = ~v.drop & 0xFFFFu;
         uint32_t n = __builtin_popcount(kept_mask), nm = __builtin_popcount(marks), pe, pm;
@@ -1134,7 +1181,10 @@ struct hjd_gdec {
     int stage_frames(const uint8_t* const* datas, const size_t* sizes, int n);
     // Parse + destuff one JPEG into frames[i] / the data area at data_off
     // (thread-safe for distinct i and disjoint data ranges).
-    int prepare_frame(int i, const uint8_t* data, size_t size, size_t data_off, size_t cap);
+    int prepare_frame(int i, const uint8_t* data, size_t size, size_t data_off, size_t cap, int mode,
+                      uint64_t raw_off);
+    // destuff mode of a JPEG and, for the device modes, its place in the raw area
+    int plan_raw(const uint8_t* data, size_t size, RawCursor& cur, int& mode, uint64_t& raw_off, bool& fits);
     // Lays out and fills the header for the staged frames (pixel records too
     // when d_outs is given); returns the device view (pointers into `blob`).
     int assemble(uint8_t* blob, int16_t* coefs, int64_t* block_offsets, void* const* d_outs, const int32_t* pitches,
@@ -1189,18 +1239,34 @@ bool pinned_host(const void* p, size_t n)
 
 }  // namespace
 
-int hjd_gdec::prepare_frame(int i, const uint8_t* data, size_t size, size_t data_off, size_t cap)
+int hjd_gdec::plan_raw(const uint8_t* data, size_t size, RawCursor& cur, int& mode, uint64_t& raw_off, bool& fits)
+{
+    mode = kDestuffHost;
+    raw_off = 0;
+    fits = true;
+    const int pol = gpu ? destuff_policy() : 0;
+    if (pol == 0 || !data) return HJD_OK;
+    const bool pinned = pinned_host(data, size);
+    if (pol == 2) mode = pinned ? kDestuffFromCaller : kDestuffFromStaging;
+    else if (pinned) mode = kDestuffFromCaller;
+    if (mode == kDestuffHost) return HJD_OK;
+    hjd_internal::ScanHeader h;
+    const int rc = hjd_internal::parse_scan_header(data, size, &h);
+    if (rc) return rc;
+    if (h.scan_offset >= size) return set_error(HJD_E_INVALID, "empty scan");
+    fits = cur.place(data + h.scan_offset, size - h.scan_offset, mode == kDestuffFromCaller, data_cap(), raw_off);
+    return HJD_OK;
+}
+
+int hjd_gdec::prepare_frame(int i, const uint8_t* data, size_t size, size_t data_off, size_t cap, int mode,
+                            uint64_t raw_off)
 {
     Prepared& p = frames[static_cast<size_t>(i)];
     p = Prepared();
     p.data_off = data_off;
     if (!data) return p.rc = set_error(HJD_E_INVALID, "frame %d: NULL data", i);
     if (cap <= kDataPad) return p.rc = set_error(HJD_E_INVALID, "scan bytes exceed the batch capacity");
-    int mode = kDestuffHost;
-    const int pol = gpu ? destuff_policy() : 0;
-    if (pol == 2) mode = pinned_host(data, size) ? kDestuffFromCaller : kDestuffFromStaging;
-    else if (pol == 1 && pinned_host(data, size)) mode = kDestuffFromCaller;
-    int rc = prepare(data, size, data_area() + data_off, cap - kDataPad, p, mode);
+    int rc = prepare(data, size, data_area() + data_off, cap - kDataPad, p, mode, raw_off);
     if (rc) return p.rc = rc;
     return HJD_OK;
 }
@@ -1212,9 +1278,16 @@ int hjd_gdec::stage_frames(const uint8_t* const* datas, const size_t* sizes, int
     frames.assign(static_cast<size_t>(n), Prepared());
     data_used = 0;
     int64_t blocks = 0;
+    RawCursor cur;
     for (int i = 0; i < n; ++i) {
         if (data_used >= data_cap()) return set_error(HJD_E_INVALID, "scan bytes exceed the batch capacity");
-        int rc = prepare_frame(i, datas[i], sizes[i], data_used, data_cap() - data_used);
+        int mode;
+        uint64_t raw_off;
+        bool fits;
+        int rc = plan_raw(datas[i], sizes[i], cur, mode, raw_off, fits);
+        if (rc) return set_error(rc, "frame %d: %s", i, hjd_last_error());
+        if (!fits) return set_error(HJD_E_INVALID, "scan bytes exceed the batch capacity");
+        rc = prepare_frame(i, datas[i], sizes[i], data_used, data_cap() - data_used, mode, raw_off);
         if (rc) return set_error(rc, "frame %d: %s", i, hjd_last_error());
         data_used = align_up(data_used + frames[i].data_bits / 8 + kDataPad, 16);
         blocks += frames[i].nblocks;
@@ -1246,7 +1319,8 @@ int hjd_gdec::assemble(uint8_t* blob, int16_t* coefs, int64_t* block_offsets, vo
     o.qt = align_up(o.recs + (d_outs ? sizeof(FrameRecord) * n : 0), kAlign);
     size_t ntiles = 0;
     for (const Prepared& p : frames)
-        if (p.destuff != kDestuffHost) ntiles += (p.raw_len + kTileBytes - 1) / kTileBytes;
+        if (p.destuff != kDestuffHost)
+            ntiles += (raw_region_len(static_cast<uint32_t>(p.raw_off & 15), p.raw_len) + kTileBytes - 1) / kTileBytes;
     o.rawf = align_up(o.qt + (d_outs ? 192 * 4 * static_cast<size_t>(n) : 0), kAlign);
     o.tilef = align_up(o.rawf + (ntiles ? sizeof(RawFrame) * n : 0), kAlign);
     o.used = align_up(o.tilef + 4 * ntiles, kAlign);
@@ -1341,9 +1415,9 @@ int hjd_gdec::assemble(uint8_t* blob, int16_t* coefs, int64_t* block_offsets, vo
         uint32_t tbase = 0;
         for (int i = 0; i < n; ++i) {
             const Prepared& p = frames[i];
-            RawFrame r{p.raw_len, tbase, 0, 0};
+            RawFrame r{p.raw_off, p.raw_len, static_cast<uint32_t>(p.raw_off & 15), tbase, 0, 0, 0};
             if (p.destuff != kDestuffHost) {
-                r.ntiles = (p.raw_len + kTileBytes - 1) / kTileBytes;
+                r.ntiles = (raw_region_len(r.begin, p.raw_len) + kTileBytes - 1) / kTileBytes;
                 for (uint32_t k = 0; k < r.ntiles; ++k) tf[tbase + k] = static_cast<uint32_t>(i);
                 tbase += r.ntiles;
             }
@@ -1462,23 +1536,37 @@ int gdec_issue(hjd_gdec* g, void* const* d_outs, const int32_t* pitches, int16_t
         host_bytes += p.destuff == kDestuffHost ? static_cast<int64_t>(p.raw_len) + static_cast<int64_t>(len)
                     : p.destuff == kDestuffFromStaging ? 2 * static_cast<int64_t>(len) : 0;
         if (p.destuff == kDestuffFromCaller) {
-            bd.push_back(g->d_raw + p.data_off);
+            // a run of scans placed at their distance in the caller's memory moves in one DMA
+            int j = i + 1;
+            size_t span = len;
+            while (j < n && g->frames[j].destuff == kDestuffFromCaller && g->frames[j].raw_src > p.raw_src &&
+                   g->frames[j].raw_off - p.raw_off == static_cast<uint64_t>(g->frames[j].raw_src - p.raw_src)) {
+                span = static_cast<size_t>(g->frames[j].raw_src - p.raw_src) + g->frames[j].raw_len;
+                ++j;
+            }
+            bd.push_back(g->d_raw + p.raw_off);
             bs.push_back(const_cast<uint8_t*>(p.raw_src));
-            bn.push_back(len);
+            bn.push_back(span);
+            moved += static_cast<int64_t>(span);
+            i = j;
+            continue;
+        }
+        if (p.destuff == kDestuffFromStaging) {
+            HJD_HIP(hipMemcpyAsync(g->d_raw + p.raw_off, g->h_stage + g->caps.data + p.data_off, len,
+                                   hipMemcpyHostToDevice, s));
             moved += static_cast<int64_t>(len);
             ++i;
             continue;
         }
-        int j = i + 1;
+        int j = i + 1;                   // host-destuffed: one copy per run of frames
         size_t hi = p.data_off + len + kDataPad;
-        while (j < n && g->frames[j].destuff == p.destuff) {
+        while (j < n && g->frames[j].destuff == kDestuffHost) {
             const Prepared& q = g->frames[j];
-            hi = q.data_off + (q.destuff == kDestuffHost ? q.data_bits / 8 : q.raw_len) + kDataPad;
-            host_bytes += q.destuff == kDestuffHost ? static_cast<int64_t>(q.raw_len) + q.data_bits / 8
-                                                    : 2 * static_cast<int64_t>(q.raw_len);
+            hi = q.data_off + q.data_bits / 8 + kDataPad;
+            host_bytes += static_cast<int64_t>(q.raw_len) + q.data_bits / 8;
             ++j;
         }
-        uint8_t* dst = (p.destuff == kDestuffHost ? g->d_blob + g->caps.data : g->d_raw) + p.data_off;
+        uint8_t* dst = g->d_blob + g->caps.data + p.data_off;
         HJD_HIP(hipMemcpyAsync(dst, g->h_stage + g->caps.data + p.data_off, hi - p.data_off, hipMemcpyHostToDevice, s));
         moved += static_cast<int64_t>(hi - p.data_off);
         i = j;
@@ -1722,7 +1810,7 @@ int hjd_debug_destuff_gpu(hjd_ctx* ctx, const uint8_t* scan, size_t n, int nseg,
     memset(&F, 0, sizeof(F));
     F.nseg = static_cast<uint32_t>(nseg);
     F.data_bits = static_cast<uint32_t>(n * 8);
-    RawFrame R{static_cast<uint32_t>(n), 0, ntiles, 0};
+    RawFrame R{0, static_cast<uint32_t>(n), 0, 0, ntiles, 0, 0};
     std::vector<uint32_t> tf(ntiles, 0);
     uint8_t *d_raw = nullptr, *d_out = nullptr;
     EntFrame* d_f = nullptr;
@@ -1842,6 +1930,7 @@ struct GBatch {
     std::vector<void*> outs;         // device destination, or null for a host-output frame
     std::vector<int32_t> pitches;
     std::vector<void*> host_outs;    // host destination (D2H sink), or null
+    RawCursor raw;                   // raw-area placement of device-destuffed scans
 };
 
 struct GJob {
@@ -1851,6 +1940,8 @@ struct GJob {
     size_t size;
     size_t data_off;
     size_t cap;
+    int mode;                        // kDestuff*
+    uint64_t raw_off;
 };
 
 }  // namespace
@@ -1996,7 +2087,7 @@ void hjd_gstream::worker()
         }
         hjd_gdec* g = slots[job.batch->slot];
         const auto t0 = std::chrono::steady_clock::now();
-        const int rc = g->prepare_frame(job.index, job.data, job.size, job.data_off, job.cap);
+        const int rc = g->prepare_frame(job.index, job.data, job.size, job.data_off, job.cap, job.mode, job.raw_off);
         prep_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
         const std::string msg = rc ? hjd_last_error() : "";
         std::unique_lock<std::mutex> lk(mu);
@@ -2066,23 +2157,36 @@ static int gstream_submit(hjd_gstream* st, const uint8_t* data, size_t size, voi
     hjd_gdec* g0 = st->slots[0];
     if (need > g0->data_cap() || h.nblocks > g0->caps.max_blocks)
         return set_error(HJD_E_INVALID, "JPEG larger than one batch's capacity");
+    int mode = kDestuffHost;
+    uint64_t raw_off = 0;
+    bool fits = true;
     if (st->open) {
         GBatch* b = st->open;
         hjd_gdec* g = st->slots[b->slot];
-        if (b->nframes == g->caps.max_frames || b->bytes + need > g->data_cap() || b->blocks + h.nblocks > g->caps.max_blocks) {
+        RawCursor cur = b->raw;
+        rc = g->plan_raw(data, size, cur, mode, raw_off, fits);
+        if (rc) return rc;
+        if (!fits || b->nframes == g->caps.max_frames || b->bytes + need > g->data_cap() ||
+            b->blocks + h.nblocks > g->caps.max_blocks) {
             b->closed = true;
             st->open = nullptr;
             if (b->prepared == b->nframes) st->issue_locked(b);
+        } else {
+            b->raw = cur;
         }
     }
     if (!st->open) {
         rc = st->open_batch(lk);
         if (rc) return rc;
+        GBatch* b = st->open;
+        rc = st->slots[b->slot]->plan_raw(data, size, b->raw, mode, raw_off, fits);
+        if (rc) return rc;
+        if (!fits) return set_error(HJD_E_INVALID, "JPEG larger than one batch's capacity");
     }
     GBatch* b = st->open;
     hjd_gdec* g = st->slots[b->slot];
     if (b->nframes == 0) g->frames.assign(static_cast<size_t>(g->caps.max_frames), Prepared());
-    GJob job{b, b->nframes, data, size, b->bytes, need};
+    GJob job{b, b->nframes, data, size, b->bytes, need, mode, raw_off};
     b->outs.push_back(d_out);
     b->host_outs.push_back(h_out);
     b->pitches.push_back(out_pitch);

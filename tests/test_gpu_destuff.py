@@ -195,3 +195,61 @@ def test_pinned_inputs_stream_no_host_scan_bytes(hjd, ctx, monkeypatch):
         ref, info = hjd.decode_coefs(d)
         exp = O.decode_q16(ref, info.qt, info.width, info.height, info.sampling)
         np.testing.assert_array_equal(o.cpu().numpy().view(np.uint32), exp)
+
+
+def _arena(hjd, datas, seed):
+    """JPEG files back to back in ONE pinned buffer, at odd offsets (as a loader
+    reading files into a pinned ring would leave them): views into it."""
+    import torch
+    rng = np.random.default_rng(seed)
+    gaps = rng.integers(0, 40, len(datas))
+    total = int(sum(len(d) for d in datas) + gaps.sum() + 64)
+    arena = torch.zeros(total, dtype=torch.uint8).pin_memory()
+    views, pos = [], int(rng.integers(1, 16))
+    for d, g in zip(datas, gaps):
+        arena[pos:pos + len(d)] = torch.frombuffer(bytearray(d), dtype=torch.uint8)
+        views.append(arena[pos:pos + len(d)])
+        pos += len(d) + int(g)
+    return arena, views
+
+
+def test_pinned_arena_runs_gpu_decoder(hjd, ctx, monkeypatch):
+    """Adjacent files in one pinned arena: their scans are placed at the same
+    distance in the raw area (unaligned starts) and move in one DMA per run."""
+    import torch
+    monkeypatch.setenv("HJD_DESTUFF", "auto")
+    datas = _pil_files()
+    arena, views = _arena(hjd, datas, seed=5)
+    infos = [hjd.parse(d) for d in datas]
+    total = sum(i.nblocks for i in infos)
+    coefs = torch.full((total, 64), 0x5A5A, dtype=torch.int16, device="cuda")
+    with hjd.GpuDecoder(ctx, len(datas), sum(map(len, datas)) + 4096, total) as gd:
+        for _ in range(2):
+            offs = gd.decode_coefs(views, coefs)
+            status = gd.sync()
+            host = coefs.cpu().numpy()
+            for d, o, i, s in zip(datas, offs, infos, status):
+                ref, _ = hjd.decode_coefs(d)
+                np.testing.assert_array_equal(host[o:o + i.nblocks], ref)
+                assert s & ~1 == 0
+    del arena
+
+
+def test_pinned_arena_stream(hjd, ctx, monkeypatch):
+    import torch
+    monkeypatch.setenv("HJD_DESTUFF", "auto")
+    datas = _pil_files() * 3
+    arena, views = _arena(hjd, datas, seed=9)
+    infos = [hjd.parse(d) for d in datas]
+    outs = [torch.full((i.height, i.width), -1, dtype=torch.int32, device="cuda") for i in infos]
+    with hjd.GpuJpegStream(ctx, 5, 5 * max(map(len, datas)) + (1 << 16), 5 * max(i.nblocks for i in infos),
+                           nslots=3, nthreads=3) as st:
+        for v, o in zip(views, outs):
+            st.submit(v, o)
+        stats = st.sync()
+    assert stats["host_scan_bytes"] == 0
+    for d, o, i in zip(datas, outs, infos):
+        ref, info = hjd.decode_coefs(d)
+        exp = O.decode_q16(ref, info.qt, info.width, info.height, info.sampling)
+        np.testing.assert_array_equal(o.cpu().numpy().view(np.uint32), exp)
+    del arena
