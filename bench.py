@@ -480,6 +480,77 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
         sys.exit(1)
 
 
+def numa_nodes():
+    try:
+        return sorted(int(d[4:]) for d in os.listdir("/sys/devices/system/node") if d.startswith("node") and
+                      d[4:].isdigit())
+    except OSError:
+        return []
+
+
+def run_host_prep(args):
+    """--host-prep-only: the host side of the config-5 stream with no GPU, as N
+    concurrent per-GPU worker pools (pool p on NUMA node p % nodes), to state
+    the host ceiling of the 8-GPU stream.  Modes: host destuff
+    (parse + tables + destuff into staging: what a pageable JPEG costs), header
+    only (the GPU-destuff path for pinned JPEGs), plain memcpy (DRAM reference).
+    Per configuration: wall-clock JPEG GB/s and implied Gpx/s (4K 4:2:0 q90),
+    and the rate per thread from thread CPU clocks, which stays meaningful when
+    pools x threads exceed the box's CPU quota (then wall-clock is the quota's)."""
+    import threading
+    import ocljpegdecoder_amd as hjd
+    from ocljpegdecoder_amd import _lib
+    lib = _lib.load()
+    w, h = 3840, 2160
+    files = encode_pool(w, h, 1, 16, seed0=7919)
+    mean_bytes = float(np.mean([len(d) for d in files]))
+    bufs = [(ctypes.c_uint8 * len(d)).from_buffer_copy(d) for d in files]
+    arr_d = (ctypes.POINTER(ctypes.c_uint8) * len(bufs))(*[ctypes.cast(b, ctypes.POINTER(ctypes.c_uint8)) for b in bufs])
+    arr_s = (ctypes.c_size_t * len(bufs))(*[len(d) for d in files])
+    nodes = numa_nodes() or [-1]
+    share, aff, quota, nproc = host_cpu_share()
+    pools_list = [int(x) for x in args.pools.split(",")]
+    tpp_list = [int(x) for x in args.threads_per_pool.split(",")] if args.threads_per_pool else None
+    rows = []
+    for npools in pools_list:
+        for tpp in (tpp_list or sorted({max(1, share // npools), 16})):
+            for mode, name in ((0, "host_destuff"), (1, "header_only"), (2, "memcpy")):
+                per = 400 * tpp if mode != 1 else 4000 * tpp
+                outs = [(ctypes.c_int64 * 4)() for _ in range(npools)]
+                rcs = [0] * npools
+                barrier = ctypes.c_int32(0)
+
+                def one(p):
+                    rcs[p] = lib.hjd_debug_host_prep(arr_d, arr_s, len(bufs), mode, tpp, nodes[p % len(nodes)],
+                                                     per, args.arena_mb << 20, args.ring_mb << 20,
+                                                     ctypes.byref(barrier), npools, outs[p])
+                th = [threading.Thread(target=one, args=(p,)) for p in range(npools)]
+                for t in th:
+                    t.start()
+                for t in th:
+                    t.join()
+                wall = max(o[0] for o in outs) / 1e9      # timed phases start together (barrier)
+                if any(rcs):
+                    raise RuntimeError(f"host prep failed: {_lib.error_string()}")
+                nbytes = sum(o[2] for o in outs)
+                cpu_s = sum(o[1] for o in outs) / 1e9
+                frames = sum(o[3] for o in outs)
+                rows.append({"pools": npools, "threads_per_pool": tpp, "mode": name,
+                             "wall_GBps": round(nbytes / wall / 1e9, 2),
+                             "wall_Gpx_s": round(frames * w * h / wall / 1e9, 1),
+                             "per_thread_GBps_cpu_clock": round(nbytes / cpu_s / 1e9, 2) if cpu_s else None,
+                             "per_pool_Gpx_s_cpu_clock": round(frames / npools * w * h / (cpu_s / (npools * tpp))
+                                                               / 1e9, 1) if cpu_s else None,
+                             "oversubscribed": npools * tpp > share})
+                log(json.dumps(rows[-1]))
+    print(json.dumps({"what": "config-5 host preparation ceiling (no GPU)", "cpu_model": _cpu_model(),
+                      "arena_MB_per_pool": args.arena_mb, "staging_ring_MB_per_pool": args.ring_mb,
+                      "logical_cpus": aff, "cgroup_cpu_quota": quota, "nproc": nproc, "numa_nodes": len(nodes),
+                      "frame": f"{w}x{h} 4:2:0 q90, mean {mean_bytes / 1e6:.2f} MB",
+                      "gpu_demand_GBps_per_gpu_at_100Gpx_s": round(100e9 / (w * h) * mean_bytes / 1e9, 1),
+                      "rows": rows}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -489,9 +560,17 @@ def main():
     ap.add_argument("--frames", type=int, default=0, help="override batch size")
     ap.add_argument("--grid", type=int, default=0, help="persistent grid (workgroups), 0 = default")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--host-prep-only", action="store_true",
+                    help="config-5 host side only, no GPU: per-GPU worker pools (see run_host_prep)")
+    ap.add_argument("--pools", default="1,2,4,8", help="--host-prep-only: pool counts")
+    ap.add_argument("--threads-per-pool", default="", help="--host-prep-only: threads per pool (default: share/N and 16)")
+    ap.add_argument("--arena-mb", type=int, default=1024, help="--host-prep-only: JPEG source arena per pool")
+    ap.add_argument("--ring-mb", type=int, default=512, help="--host-prep-only: pinned-staging ring per pool")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for the barrier/timing reduction (no data-path collective)")
     args = ap.parse_args()
+    if args.host_prep_only:
+        return run_host_prep(args)
 
     import torch
     import torch.distributed as dist

@@ -166,6 +166,16 @@ int hjd_gstream_host_bytes(hjd_gstream* s, int64_t* host_scan_bytes);
  * path).  The range must stay registered while frames submitted from it are in
  * flight (until hjd_gstream_sync / hjd_gdec_sync). */
 int hjd_host_register(void* ptr, size_t size);
+/* Host-side stream preparation alone, no GPU (measurement hook for the
+ * multi-GPU host ceiling, one call = one per-GPU pool): nthreads threads on
+ * NUMA node `node` (-1: unbound) prepare `frames` JPEGs read in order from an
+ * arena of arena_bytes (datas replicated) into a staging ring of ring_bytes.
+ * mode 0 host destuff, 1 header + tables only (the GPU-destuff path), 2 plain
+ * memcpy of each file.  Calls sharing `barrier` (parties > 1) start their timed
+ * phase together.  out: wall ns, summed thread CPU ns, JPEG bytes, frames. */
+int hjd_debug_host_prep(const uint8_t* const* datas, const size_t* sizes, int n, int mode, int nthreads, int node,
+                        int64_t frames, int64_t arena_bytes, int64_t ring_bytes, int32_t* barrier, int parties,
+                        int64_t out[4]);
 int hjd_host_unregister(void* ptr);
 
 /* The 54-byte header of the reference's output BMP (src/decoder.cpp:372-394):

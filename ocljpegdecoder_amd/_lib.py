@@ -150,6 +150,10 @@ def _bind_host(lib):
         "hjd_gstream_host_bytes": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int64)]),
         "hjd_host_register": (ctypes.c_int, [vp, ctypes.c_size_t]),
         "hjd_host_unregister": (ctypes.c_int, [vp]),
+        "hjd_debug_host_prep": (ctypes.c_int, [ctypes.POINTER(u8p), ctypes.POINTER(ctypes.c_size_t), ctypes.c_int,
+                                               ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int64,
+                                               ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(ctypes.c_int32),
+                                               ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]),
         "hjd_debug_destuff_host": (ctypes.c_int, [u8p, ctypes.c_size_t, u8p, ctypes.c_size_t,
                                                   ctypes.POINTER(ctypes.c_uint32), ctypes.c_int,
                                                   ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int64)]),

@@ -2298,6 +2298,102 @@ int hjd_gstream_sync(hjd_gstream* st, int64_t stats[5])
     return HJD_OK;
 }
 
+// Host-side stream preparation alone, no GPU (bench.py --host-prep-only: the
+// host ceiling of the multi-GPU config-5 stream).  One call =
+// one per-GPU worker pool: nthreads threads bound to NUMA node `node` (-1:
+// unbound) prepare `frames` JPEGs.  The sources are an arena of `arena_bytes`
+// (the pool's files replicated back to back, first-touched on that node, read
+// in order) and each frame lands in the next slot of a staging ring of
+// `ring_bytes`: with both larger than the node's L3 the traffic is DRAM's, as
+// for a loader streaming fresh files.
+//   mode 0: the host-destuff path (header, tables, destuff into staging);
+//   mode 1: the GPU-destuff path (header and tables only);
+//   mode 2: a plain memcpy of each file into staging (the DRAM reference).
+// out[0] wall ns, out[1] summed thread CPU ns, out[2] JPEG bytes, out[3] frames.
+int hjd_debug_host_prep(const uint8_t* const* datas, const size_t* sizes, int n, int mode, int nthreads, int node,
+                        int64_t frames, int64_t arena_bytes, int64_t ring_bytes, int32_t* barrier, int parties,
+                        int64_t out[4])
+{
+    if (!datas || !sizes || n <= 0 || nthreads <= 0 || frames <= 0 || !out || mode < 0 || mode > 2)
+        return set_error(HJD_E_INVALID, "invalid host-prep arguments");
+    const hjd_internal::CpuSet cpus = hjd_internal::node_cpus(node);
+    size_t maxsz = 0, total = 0;
+    for (int i = 0; i < n; ++i) {
+        maxsz = std::max(maxsz, sizes[i]);
+        total += sizes[i];
+    }
+    const size_t reps = std::max<size_t>(1, static_cast<size_t>(arena_bytes) / std::max<size_t>(total, 1));
+    const size_t slot = align_up(maxsz + 4 * kDataPad, 4096);
+    const size_t nslot = std::max<size_t>(static_cast<size_t>(nthreads),
+                                          static_cast<size_t>(ring_bytes) / slot);
+    std::vector<const uint8_t*> src;
+    std::vector<size_t> src_size;
+    uint8_t* arena = nullptr;
+    uint8_t* ring = nullptr;
+    {   // arena and ring first-touched by a thread on the pool's node
+        std::thread t([&] {
+            hjd_internal::bind_current_thread(cpus);
+            arena = static_cast<uint8_t*>(malloc(total * reps));
+            ring = static_cast<uint8_t*>(malloc(slot * nslot));
+            if (!arena || !ring) return;
+            size_t pos = 0;
+            for (size_t r = 0; r < reps; ++r)
+                for (int i = 0; i < n; ++i) {
+                    memcpy(arena + pos, datas[i], sizes[i]);
+                    src.push_back(arena + pos);
+                    src_size.push_back(sizes[i]);
+                    pos += sizes[i];
+                }
+            memset(ring, 0, slot * nslot);
+        });
+        t.join();
+    }
+    if (!arena || !ring) {
+        free(arena);
+        free(ring);
+        return set_error(HJD_E_NOMEM, "host-prep arena");
+    }
+    if (barrier && parties > 1) {   // concurrent pools start their timed phase together
+        __atomic_add_fetch(barrier, 1, __ATOMIC_SEQ_CST);
+        while (__atomic_load_n(barrier, __ATOMIC_SEQ_CST) < parties) std::this_thread::yield();
+    }
+    std::atomic<int64_t> next{0}, cpu_ns{0}, bytes{0};
+    std::atomic<int> err{HJD_OK};
+    auto worker = [&] {
+        hjd_internal::bind_current_thread(cpus);
+        timespec c0, c1;
+        clock_gettime(CLOCK_THREAD_CPUTIME_ID, &c0);
+        int64_t my_bytes = 0;
+        Prepared pf;
+        for (;;) {
+            const int64_t k = next.fetch_add(1);
+            if (k >= frames) break;
+            const size_t i = static_cast<size_t>(k) % src.size();
+            uint8_t* dst = ring + slot * (static_cast<size_t>(k) % nslot);
+            int rc = HJD_OK;
+            if (mode == 2) memcpy(dst, src[i], src_size[i]);
+            else rc = prepare(src[i], src_size[i], dst, slot - kDataPad, pf,
+                              mode == 0 ? kDestuffHost : kDestuffFromCaller, 0);
+            if (rc) err = rc;
+            my_bytes += static_cast<int64_t>(src_size[i]);
+        }
+        clock_gettime(CLOCK_THREAD_CPUTIME_ID, &c1);
+        cpu_ns += (c1.tv_sec - c0.tv_sec) * 1000000000ll + (c1.tv_nsec - c0.tv_nsec);
+        bytes += my_bytes;
+    };
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> th;
+    for (int t = 0; t < nthreads; ++t) th.emplace_back(worker);
+    for (auto& t : th) t.join();
+    out[0] = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+    out[1] = cpu_ns;
+    out[2] = bytes;
+    out[3] = frames;
+    free(arena);
+    free(ring);
+    return err == HJD_OK ? HJD_OK : set_error(err, "host prep failed: %s", hjd_last_error());
+}
+
 int hjd_gstream_host_bytes(hjd_gstream* st, int64_t* host_scan_bytes)
 {
     if (!st || !host_scan_bytes) return set_error(HJD_E_INVALID, "NULL argument");

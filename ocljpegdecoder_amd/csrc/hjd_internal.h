@@ -90,6 +90,7 @@ struct CpuSet {
     std::vector<int> cpus;
 };
 CpuSet device_local_cpus(int device);
+CpuSet node_cpus(int node);   // CPUs of NUMA node `node` this process may use (empty: unknown)
 std::vector<int> bind_current_thread(const CpuSet& s);
 void restore_current_thread(const std::vector<int>& prev);
 

@@ -102,3 +102,21 @@ void hjd_internal::restore_current_thread(const std::vector<int>& prev)
     for (int c : prev) CPU_SET(c, &set);
     (void)pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
 }
+
+hjd_internal::CpuSet hjd_internal::node_cpus(int node)
+{
+    CpuSet s;
+    if (node < 0) return s;
+    std::vector<int> cpus =
+        parse_cpulist(read_file("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist"));
+    cpu_set_t allowed;
+    CPU_ZERO(&allowed);
+    if (sched_getaffinity(0, sizeof(allowed), &allowed) == 0) {
+        std::vector<int> keep;
+        for (int c : cpus)
+            if (CPU_ISSET(c, &allowed)) keep.push_back(c);
+        cpus.swap(keep);
+    }
+    s.cpus = cpus;
+    return s;
+}
