@@ -331,6 +331,8 @@ struct EntBatchDev {
     const uint8_t* data;
     uint64_t* entries;
     SubStats* stats;
+    uint64_t* mids;       // [sub] verified state at the first unit boundary >= k*S + S/2
+    SubStats* stats1;     // [sub] statistics of the first half (entry -> mid)
     uint64_t* wentries;   // [group][kWarm] warm-up entries
     uint32_t* linked;     // [group] 1 if joined to the previous group's chain
     SubStats* agg;
@@ -408,11 +410,12 @@ __device__ __forceinline__ SubStats shfl_down_stats(const SubStats& s, int d)
 }
 
 // Ordered inclusive scan of one value per thread over the workgroup (LDS).
+template <int N = kGroupSubs>
 __device__ __forceinline__ SubStats block_scan_inclusive(SubStats v, SubStats* buf, int tid)
 {
     buf[tid] = v;
     __syncthreads();
-    for (int d = 1; d < kGroupSubs; d <<= 1) {
+    for (int d = 1; d < N; d <<= 1) {
         SubStats o = v;
         if (tid >= d) o = stats_combine(buf[tid - d], v);
         __syncthreads();
@@ -475,8 +478,16 @@ __global__ __launch_bounds__(kGroupSubs) void ent_sync_kernel(EntBatchDev b)
     uint64_t used = valid ? guess_entry(c, ku * S) : 0;
     SubStats st = stats_identity(), suf = stats_identity();
     uint64_t cp = used, x = used;
+    // the write kernel decodes each subsequence as two halves, from the entry and
+    // from the mid-state: every run that produces a subsequence's final entry
+    // records its mid-state and first-half statistics (the last such run wins)
+    const bool rec = valid && tid >= kWarm;
     if (valid) {
         cp = run<false>(c, used, mid, st, nullptr);
+        if (rec) {
+            b.mids[F.sub_base + ku] = cp;
+            b.stats1[F.sub_base + ku] = st;
+        }
         x = run<false>(c, cp, (ku + 1) * S, suf, nullptr);
         st = stats_combine(st, suf);
     }
@@ -496,6 +507,10 @@ __global__ __launch_bounds__(kGroupSubs) void ent_sync_kernel(EntBatchDev b)
         if (!same_state(e, used)) {
             SubStats s2 = stats_identity();
             resume = run<false>(c, e, mid, s2, nullptr);
+            if (rec) {
+                b.mids[F.sub_base + ku] = resume;
+                b.stats1[F.sub_base + ku] = s2;
+            }
             used = e;
             if (same_state(resume, cp)) {
                 st = stats_combine(s2, suf);
@@ -539,8 +554,18 @@ __global__ __launch_bounds__(kGroupSubs) void ent_sync_kernel(EntBatchDev b)
             item = L.list[r][tid];
             e = L.x[item - 1];
             const uint32_t kk = static_cast<uint32_t>(k0 + item);
-            if (!same_state(e, L.used[item])) x2 = run<false>(c, e, (kk + 1) * S, s2, nullptr);
-            else item = -1;
+            if (!same_state(e, L.used[item])) {
+                const uint64_t m2 = run<false>(c, e, kk * S + S / 2, s2, nullptr);
+                if (item >= kWarm) {
+                    b.mids[F.sub_base + kk] = m2;
+                    b.stats1[F.sub_base + kk] = s2;
+                }
+                SubStats s3 = stats_identity();
+                x2 = run<false>(c, m2, (kk + 1) * S, s3, nullptr);
+                s2 = stats_combine(s2, s3);
+            } else {
+                item = -1;
+            }
         }
         if (tid == 0) L.nlist[r ^ 1] = 0;
         __syncthreads();   // all reads of L.x done; the next list is empty
@@ -614,8 +639,14 @@ __host__ __device__ __forceinline__ void repair_frame(const EntBatchDev& b, uint
         uint32_t k = first - 1;
         uint64_t cur = b.entries[F.sub_base + k];
         for (;;) {
-            SubStats st = stats_identity();
-            const uint64_t x = run<false>(c, cur, (k + 1) * b.sub_bits, st, nullptr);
+            SubStats st = stats_identity(), st2 = stats_identity();
+            const uint64_t m = run<false>(c, cur, k * b.sub_bits + b.sub_bits / 2, st, nullptr);
+            if (k >= first) {
+                b.mids[F.sub_base + k] = m;
+                b.stats1[F.sub_base + k] = st;
+            }
+            const uint64_t x = run<false>(c, m, (k + 1) * b.sub_bits, st2, nullptr);
+            st = stats_combine(st, st2);
             if (k >= first) {
                 b.entries[F.sub_base + k] = cur;
                 b.stats[F.sub_base + k] = st;
@@ -650,14 +681,26 @@ __global__ __launch_bounds__(64) void ent_fallback_kernel(EntBatchDev b)
     if (lane == 0) repair_frame(b, f, tabs, blocks);
 }
 
-__global__ __launch_bounds__(kGroupSubs) void ent_write_kernel(EntBatchDev b)
+// Two threads per subsequence: thread t decodes the first half of group
+// subsequence t (entry -> the recorded mid-state), thread t + 256 the second
+// (mid-state -> end), so each serial chain is S/2 bits long while the sync
+// kernel keeps its S (the sync kernel is fastest at S = 4096,
+// writing at 2048).  A run that starts inside a block skips to the next DC unit
+// and a run finishes the block it started past its stop, so the halves write
+// disjoint blocks; the second half's block index and DC predictors are the
+// subsequence's prefix combined with the first half's statistics.
+constexpr int kWriteThreads = 2 * kGroupSubs;
+
+__global__ __launch_bounds__(kWriteThreads) void ent_write_kernel(EntBatchDev b)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    int16_t* stage = reinterpret_cast<int16_t*>(smem);                                  // [256][kStageStride]
-    HuffLut* tabs = reinterpret_cast<HuffLut*>(smem + sizeof(int16_t) * kGroupSubs * kStageStride);
+    int16_t* stage = reinterpret_cast<int16_t*>(smem);                                  // [512][kStageStride]
+    HuffLut* tabs = reinterpret_cast<HuffLut*>(smem + sizeof(int16_t) * kWriteThreads * kStageStride);
     SubStats* buf = reinterpret_cast<SubStats*>(stage);   // scan scratch before any block is staged
-    static_assert(sizeof(SubStats) * kGroupSubs <= sizeof(int16_t) * kGroupSubs * kStageStride, "scratch");
+    static_assert(sizeof(SubStats) * kWriteThreads <= sizeof(int16_t) * kWriteThreads * kStageStride, "scratch");
     const int tid = threadIdx.x;
+    const int t = tid & (kGroupSubs - 1);
+    const bool second = tid >= kGroupSubs;
     const uint32_t w = blockIdx.x;
     const uint32_t f = b.wg_frame[w];
     const EntFrame F = b.frames[f];
@@ -665,24 +708,32 @@ __global__ __launch_bounds__(kGroupSubs) void ent_write_kernel(EntBatchDev b)
     const uint32_t S = b.sub_bits;
     if (gl >= frame_groups(F.nsub)) return;
     __shared__ BlockInfo blocks[kMaxBpm];
-    load_tables(tabs, blocks, b.tabs + F.tab_base, F, b.frames + f, tid, kGroupSubs);
+    load_tables(tabs, blocks, b.tabs + F.tab_base, F, b.frames + f, tid, kWriteThreads);
     // block index / DC predictors at this group's start: all previous groups of the frame
     SubStats pre = stats_identity();
-    for (uint32_t base = 0; base < gl; base += kGroupSubs) {
+    for (uint32_t base = 0; base < gl; base += kWriteThreads) {
         const SubStats v = base + tid < gl ? b.agg[F.wg_base + base + tid] : stats_identity();
-        block_scan_inclusive(v, buf, tid);
-        const SubStats total = buf[kGroupSubs - 1];
+        block_scan_inclusive<kWriteThreads>(v, buf, tid);
+        const SubStats total = buf[kWriteThreads - 1];
         __syncthreads();
         pre = stats_combine(pre, total);
     }
-    const int64_t k = group_sub(gl, tid);
-    const bool own = tid >= kWarm && k < static_cast<int64_t>(F.nsub);
+    const int64_t k = group_sub(gl, t);
+    const bool own = t >= kWarm && k < static_cast<int64_t>(F.nsub);
     const uint32_t ku = static_cast<uint32_t>(k);
-    const SubStats mine = own ? b.stats[F.sub_base + ku] : stats_identity();
-    block_scan_inclusive(mine, buf, tid);
-    const SubStats excl = stats_combine(pre, tid > 0 ? buf[tid - 1] : stats_identity());
+    // subsequence prefixes (the upper 256 entries are identities and do not disturb them)
+    const SubStats mine = own && !second ? b.stats[F.sub_base + ku] : stats_identity();
+    block_scan_inclusive<kWriteThreads>(mine, buf, tid);
+    SubStats excl = stats_combine(pre, t > 0 ? buf[t - 1] : stats_identity());
     __syncthreads();   // scratch reads done before blocks are staged
     if (!own) return;
+    uint64_t entry = b.entries[F.sub_base + ku];
+    uint32_t stop = ku * S + S / 2;
+    if (second) {
+        excl = stats_combine(excl, b.stats1[F.sub_base + ku]);
+        entry = b.mids[F.sub_base + ku];
+        stop = (ku + 1) * S;
+    }
     const RunCtx c = make_ctx(b, F, tabs, blocks);
     RunOut o;
     o.coefs = b.coefs + F.coef_off * 64;
@@ -693,9 +744,9 @@ __global__ __launch_bounds__(kGroupSubs) void ent_write_kernel(EntBatchDev b)
     o.pred[1] = excl.dc[1];
     o.pred[2] = excl.dc[2];
     SubStats st = stats_identity();
-    run<true>(c, b.entries[F.sub_base + ku], (ku + 1) * S, st, &o);
+    run<true>(c, entry, stop, st, &o);
     uint32_t bad = (st.flags & kError) ? kStatusCorrupt : 0;
-    if (ku == F.nsub - 1 && excl.nblk + st.nblk < F.nblocks) bad |= kStatusCount;
+    if (second && ku == F.nsub - 1 && excl.nblk + st.nblk < F.nblocks) bad |= kStatusCount;
     if (bad) atomicOr(&b.status[f], bad);
 }
 
@@ -1034,11 +1085,18 @@ void emulate(const EntBatchDev& b)
         std::vector<SubStats> st(kGroupSubs, stats_identity()), suf(kGroupSubs, stats_identity());
         std::vector<uint64_t> cp(kGroupSubs, 0);
         auto valid = [&](int t) { const int64_t k = group_sub(gl, t); return k >= 0 && k < int64_t(F.nsub); };
+        auto record = [&](int t, uint64_t m, const SubStats& s1) {   // as the device: owned subsequences
+            if (t < kWarm) return;
+            const uint32_t k = static_cast<uint32_t>(group_sub(gl, t));
+            b.mids[F.sub_base + k] = m;
+            b.stats1[F.sub_base + k] = s1;
+        };
         for (int t = 0; t < kGroupSubs; ++t) {   // phase 1, split at the checkpoint
             if (!valid(t)) continue;
             const uint32_t k = static_cast<uint32_t>(group_sub(gl, t));
             used[t] = guess_entry(c, k * S);
             cp[t] = run<false>(c, used[t], k * S + S / 2, st[t], nullptr);
+            record(t, cp[t], st[t]);
             x[t] = run<false>(c, cp[t], (k + 1) * S, suf[t], nullptr);
             st[t] = stats_combine(st[t], suf[t]);
             xs0[t] = x[t];
@@ -1055,6 +1113,7 @@ void emulate(const EntBatchDev& b)
                     uint64_t x2;
                     if (round == 0) {   // round 0: to the checkpoint, on if phase 1 is not joined there
                         const uint64_t r = run<false>(c, (*cur)[t - 1], ku * S + S / 2, s2, nullptr);
+                        record(t, r, s2);
                         if (same_state(r, cp[t])) {
                             x2 = x[t];
                             s2 = stats_combine(s2, suf[t]);
@@ -1064,7 +1123,11 @@ void emulate(const EntBatchDev& b)
                             s2 = stats_combine(s2, s3);
                         }
                     } else {
-                        x2 = run<false>(c, (*cur)[t - 1], (ku + 1) * S, s2, nullptr);
+                        const uint64_t m2 = run<false>(c, (*cur)[t - 1], ku * S + S / 2, s2, nullptr);
+                        record(t, m2, s2);
+                        SubStats s3 = stats_identity();
+                        x2 = run<false>(c, m2, (ku + 1) * S, s3, nullptr);
+                        s2 = stats_combine(s2, s3);
                     }
                     changed |= !same_state(x2, x[t]);
                     used[t] = (*cur)[t - 1];
@@ -1118,18 +1181,22 @@ void emulate(const EntBatchDev& b)
         const RunCtx c = make_ctx(b, F, b.tabs + F.tab_base, blocks);
         SubStats pre = stats_identity();
         for (uint32_t i = 0; i < F.nsub; ++i) {
-            RunOut o;
-            o.coefs = b.coefs + F.coef_off * 64;
-            o.stage = stage;
-            o.blk = pre.nblk;
-            o.nblocks = F.nblocks;
-            o.pred[0] = pre.dc[0];
-            o.pred[1] = pre.dc[1];
-            o.pred[2] = pre.dc[2];
-            SubStats s = stats_identity();
-            run<true>(c, b.entries[F.sub_base + i], (i + 1) * S, s, &o);
-            if (s.flags & kError) b.status[f] |= kStatusCorrupt;
-            if (i == F.nsub - 1 && pre.nblk + s.nblk < F.nblocks) b.status[f] |= kStatusCount;
+            for (int half = 0; half < 2; ++half) {   // as ent_write_kernel: entry -> mid, mid -> end
+                const SubStats p = half ? stats_combine(pre, b.stats1[F.sub_base + i]) : pre;
+                RunOut o;
+                o.coefs = b.coefs + F.coef_off * 64;
+                o.stage = stage;
+                o.blk = p.nblk;
+                o.nblocks = F.nblocks;
+                o.pred[0] = p.dc[0];
+                o.pred[1] = p.dc[1];
+                o.pred[2] = p.dc[2];
+                SubStats s = stats_identity();
+                run<true>(c, half ? b.mids[F.sub_base + i] : b.entries[F.sub_base + i],
+                          half ? (i + 1) * S : i * S + S / 2, s, &o);
+                if (s.flags & kError) b.status[f] |= kStatusCorrupt;
+                if (half && i == F.nsub - 1 && p.nblk + s.nblk < F.nblocks) b.status[f] |= kStatusCount;
+            }
             pre = stats_combine(pre, b.stats[F.sub_base + i]);
         }
     }
@@ -1150,6 +1217,8 @@ struct hjd_gdec {
     uint8_t* d_blob = nullptr;
     uint64_t* d_entries = nullptr;
     SubStats* d_stats = nullptr;
+    uint64_t* d_mids = nullptr;
+    SubStats* d_stats1 = nullptr;
     uint64_t* d_wentries = nullptr;
     uint32_t* d_linked = nullptr;
     SubStats* d_agg = nullptr;
@@ -1168,9 +1237,9 @@ struct hjd_gdec {
     int first_error = HJD_OK;
 
     // host-side work arrays for emulation
-    std::vector<uint64_t> e_entries, e_wentries;
+    std::vector<uint64_t> e_entries, e_wentries, e_mids;
     std::vector<uint32_t> e_linked;
-    std::vector<SubStats> e_stats, e_agg;
+    std::vector<SubStats> e_stats, e_agg, e_stats1;
     std::vector<uint32_t> e_status;
 
     uint8_t* data_area() { return h_stage + caps.data; }
@@ -1457,6 +1526,8 @@ int gdec_alloc(hjd_gdec* g)
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_blob), total));
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_entries), 8 * static_cast<size_t>(g->caps.max_subs)));
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_stats), sizeof(SubStats) * static_cast<size_t>(g->caps.max_subs)));
+    HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_mids), 8 * static_cast<size_t>(g->caps.max_subs)));
+    HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_stats1), sizeof(SubStats) * static_cast<size_t>(g->caps.max_subs)));
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_wentries), 8 * kWarm * static_cast<size_t>(g->caps.max_wgs)));
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_linked), 4 * static_cast<size_t>(g->caps.max_wgs)));
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_agg), sizeof(SubStats) * static_cast<size_t>(g->caps.max_wgs)));
@@ -1488,9 +1559,9 @@ int launch_entropy(hjd_gdec* g, const EntBatchDev& b, hipStream_t s)
     HJD_HIP(hipGetLastError());
     hipLaunchKernelGGL(ent_fallback_kernel, dim3(b.nframes), dim3(64), 0, s, b);
     HJD_HIP(hipGetLastError());
-    constexpr size_t kStageBytes = sizeof(int16_t) * kGroupSubs * kStageStride;
-    hipLaunchKernelGGL(ent_write_kernel, dim3(b.nwg), dim3(kGroupSubs), kStageBytes + sizeof(HuffLut) * b.ntab_max, s,
-                       b);
+    constexpr size_t kStageBytes = sizeof(int16_t) * kWriteThreads * kStageStride;
+    hipLaunchKernelGGL(ent_write_kernel, dim3(b.nwg), dim3(kWriteThreads), kStageBytes + sizeof(HuffLut) * b.ntab_max,
+                       s, b);
     HJD_HIP(hipGetLastError());
     return HJD_OK;
 }
@@ -1514,6 +1585,8 @@ int gdec_issue(hjd_gdec* g, void* const* d_outs, const int32_t* pitches, int16_t
     if (rc) return rc;
     b.entries = g->d_entries;
     b.stats = g->d_stats;
+    b.mids = g->d_mids;
+    b.stats1 = g->d_stats1;
     b.wentries = g->d_wentries;
     b.linked = g->d_linked;
     b.agg = g->d_agg;
@@ -1678,8 +1751,8 @@ int hjd_gdec_destroy(hjd_gdec* g)
     if (g->done) (void)hipEventSynchronize(g->done);
     if (g->h_stage) (void)hipHostFree(g->h_stage);
     if (g->h_status) (void)hipHostFree(g->h_status);
-    void* dev[] = {g->d_blob, g->d_entries, g->d_stats, g->d_wentries, g->d_linked, g->d_agg, g->d_status, g->d_coefs,
-                   g->d_raw, g->d_tiles};
+    void* dev[] = {g->d_blob, g->d_entries, g->d_stats, g->d_mids, g->d_stats1, g->d_wentries, g->d_linked, g->d_agg,
+                   g->d_status, g->d_coefs, g->d_raw, g->d_tiles};
     for (void* p : dev)
         if (p) (void)hipFree(p);
     if (g->staged) (void)hipEventDestroy(g->staged);
@@ -1885,12 +1958,16 @@ int hjd_debug_entropy_emulate(const uint8_t* data, size_t size, int sub_bits, in
     const int64_t total = g.frames[0].nblocks;
     g.e_entries.assign(static_cast<size_t>(g.caps.max_subs), 0);
     g.e_stats.assign(static_cast<size_t>(g.caps.max_subs), stats_identity());
+    g.e_mids.assign(static_cast<size_t>(g.caps.max_subs), 0);
+    g.e_stats1.assign(static_cast<size_t>(g.caps.max_subs), stats_identity());
     g.e_wentries.assign(static_cast<size_t>(g.caps.max_wgs) * kWarm, 0);
     g.e_linked.assign(static_cast<size_t>(g.caps.max_wgs), 0);
     g.e_agg.assign(static_cast<size_t>(g.caps.max_wgs), stats_identity());
     g.e_status.assign(1, 0);
     b.entries = g.e_entries.data();
     b.stats = g.e_stats.data();
+    b.mids = g.e_mids.data();
+    b.stats1 = g.e_stats1.data();
     b.wentries = g.e_wentries.data();
     b.linked = g.e_linked.data();
     b.agg = g.e_agg.data();
