@@ -25,10 +25,26 @@ constexpr int kTaskBlocks = 48;      // blocks per task (6 rounds x 8 lane group
 constexpr int kSlotBytes = 144;      // LDS bytes per block slot (128 + 16 pad: bank spread)
 constexpr int kRowStride = 48;       // transpose buffer: bytes per row (b128 row writes conflict-free)
 constexpr int kRowBufBlock = 416;    // transpose buffer: bytes per block (104 dwords = 8 mod 32 banks)
-constexpr int kWaveLds = kTaskBlocks * kSlotBytes + 8 * kRowBufBlock;  // 10240
 constexpr int kWavesPerGroup = 4;
 constexpr int kGroupThreads = 64 * kWavesPerGroup;
-static_assert(kWavesPerGroup * kWaveLds * 4 <= 160 * 1024, "4 groups per CU must fit the 160 KiB LDS");
+#ifndef HJD_T2
+#define HJD_T2 0
+#endif
+
+// Per-wave LDS layout of the fused kernel.  Default: 48 block slots plus a
+// transpose buffer (10240 B, 4 waves per SIMD).  t2 (HJD_T2, 4:4:4): the
+// row->column transpose goes through the round's own block slot (its
+// coefficients are already gathered) in two halves, and the lane rows of the
+// three dequant tables live in LDS (384 B) instead of 12 VGPRs, so a wave needs
+// 7296 B and <= 96 VGPRs: 5 waves per SIMD.
+template <int kSampling>
+struct KLayout {
+    static constexpr bool t2 = HJD_T2 != 0 && kSampling == 0;
+    static constexpr int q_lds = 3 * 8 * 16;
+    static constexpr int wave_lds = kTaskBlocks * kSlotBytes + (t2 ? q_lds : 8 * kRowBufBlock);
+    static constexpr int min_waves = t2 ? 5 : 4;
+    static_assert(kWavesPerGroup * wave_lds * min_waves <= 160 * 1024, "the groups per CU must fit the 160 KiB LDS");
+};
 
 // Device-side frame record built by hjd_plan_create.
 struct FrameDev {
@@ -531,17 +547,21 @@ __device__ __forceinline__ bool round_is_luma(int i)
 // the pairs (q0,q4), (q1,q7), (q3,q5), (q2,q6) (load_qrow_pk).
 template <int kSampling>
 __device__ __forceinline__ RowPk load_round_pk(const char* __restrict__ slots, int lane, int i, const int (&zoff)[8],
-                                               const uint32_t (&q)[3][4])
+                                               const uint32_t (&q)[3][4], const char* __restrict__ qlds)
 {
     const int g = lane >> 3;
     const int b = round_block<kSampling>(i, g);
     const int comp = round_component<kSampling>(i);
     const char* blk = slots + b * kSlotBytes;
+    uint4 ql = make_uint4(0, 0, 0, 0);
+    if constexpr (KLayout<kSampling>::t2)   // this lane's table row pairs from the wave's LDS copy
+        ql = *reinterpret_cast<const uint4*>(qlds + (comp >= 0 ? comp : (g < 4 ? 1 : 2)) * 128 + (lane & 7) * 16);
     auto pair = [&](int ca, int cb, int k) {
         const s16x2 c = {*reinterpret_cast<const short*>(blk + zoff[ca]),
                          *reinterpret_cast<const short*>(blk + zoff[cb])};
         // a mixed round (4:2:2 round 4) selects the table per lane
-        const uint32_t qq = comp >= 0 ? q[comp < 0 ? 0 : comp][k] : (g < 4 ? q[1][k] : q[2][k]);
+        const uint32_t qq = KLayout<kSampling>::t2 ? (k == 0 ? ql.x : k == 1 ? ql.y : k == 2 ? ql.z : ql.w)
+                          : comp >= 0 ? q[comp < 0 ? 0 : comp][k] : (g < 4 ? q[1][k] : q[2][k]);
         return c * __builtin_bit_cast(s16x2, qq);   // dequant (src/decoder.cpp:340)
     };
     RowPk p;
@@ -587,14 +607,14 @@ __device__ __forceinline__ void load_qrow_pk(const int* __restrict__ qt_pool, in
 // LDS latency overlaps it.
 template <int kSampling, int kFmt>
 __device__ __forceinline__ void idct_stage(char* __restrict__ slots, char* __restrict__ rowbuf, int lane,
-                                           const int (&zoff)[8], const uint32_t (&q)[3][4],
+                                           const int (&zoff)[8], const uint32_t (&q)[3][4], const char* __restrict__ qlds,
                                            const int* __restrict__ src32, int nblk)
 {
     const int g = lane >> 3, r = lane & 7;
     RowPk pk;
     int v[8];
     if constexpr (kFmt == 0)
-        pk = load_round_pk<kSampling>(slots, lane, 0, zoff, q);
+        pk = load_round_pk<kSampling>(slots, lane, 0, zoff, q, qlds);
     else
         load_round_i32<kSampling>(lane, 0, src32, nblk, v);
 #pragma unroll
@@ -604,21 +624,39 @@ __device__ __forceinline__ void idct_stage(char* __restrict__ slots, char* __res
             idct8_row_pk(pk, v);
         else
             idct8<false>(v);
-        {
+        int c8[8];
+        if constexpr (KLayout<kSampling>::t2) {
+            // Transpose through block b's own slot, whose coefficients the
+            // previous gather already read (DS ops of a wave run in order):
+            // row halves 0-3 (128 B) serve columns 0-3, then halves 4-7 serve
+            // columns 4-7.
+            char* tb = slots + b * kSlotBytes;
+            const char* col = tb + (r & 3) * 4;
+            *reinterpret_cast<int4*>(tb + r * 16) = make_int4(v[0], v[1], v[2], v[3]);
+            wave_lds_sync();
+            if (r < 4) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) c8[k] = *reinterpret_cast<const int*>(col + k * 16);
+            }
+            wave_lds_sync();
+            *reinterpret_cast<int4*>(tb + r * 16) = make_int4(v[4], v[5], v[6], v[7]);
+            wave_lds_sync();
+            if (r >= 4) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) c8[k] = *reinterpret_cast<const int*>(col + k * 16);
+            }
+        } else {
             int4* dst = reinterpret_cast<int4*>(rowbuf + g * kRowBufBlock + r * kRowStride);
             dst[0] = make_int4(v[0], v[1], v[2], v[3]);
             dst[1] = make_int4(v[4], v[5], v[6], v[7]);
-        }
-        wave_lds_sync();
-        int c8[8];
-        {
+            wave_lds_sync();
             const char* col = rowbuf + g * kRowBufBlock + r * 4;
 #pragma unroll
             for (int k = 0; k < 8; ++k) c8[k] = *reinterpret_cast<const int*>(col + k * kRowStride);
         }
         if (i + 1 < 6) {
             if constexpr (kFmt == 0)
-                pk = load_round_pk<kSampling>(slots, lane, i + 1, zoff, q);
+                pk = load_round_pk<kSampling>(slots, lane, i + 1, zoff, q, qlds);
             else
                 load_round_i32<kSampling>(lane, i + 1, src32, nblk, v);
         }
@@ -640,16 +678,18 @@ __device__ __forceinline__ void idct_stage(char* __restrict__ slots, char* __res
 // SGPRs; the next task's coefficients are prefetched into VGPRs while the
 // current one is transformed.
 template <int kSampling, int kFmt, int kVariant>
-__global__ __launch_bounds__(kGroupThreads, 4) void decode_kernel(const void* __restrict__ coefs,
+__global__ __launch_bounds__(kGroupThreads, KLayout<kSampling>::min_waves) void decode_kernel(const void* __restrict__ coefs,
                                                               const int* __restrict__ qt_pool,
                                                               const FrameDev* __restrict__ frames, int nframes,
                                                               int64_t total_tasks, uint8_t* __restrict__ out)
 {
-    __shared__ __attribute__((aligned(16))) char lds[kWavesPerGroup * kWaveLds];
+    using L = KLayout<kSampling>;
+    __shared__ __attribute__((aligned(16))) char lds[kWavesPerGroup * L::wave_lds];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    char* slots = lds + wave * kWaveLds;
-    char* rowbuf = slots + kTaskBlocks * kSlotBytes;
+    char* slots = lds + wave * L::wave_lds;
+    char* rowbuf = slots + kTaskBlocks * kSlotBytes;   // transpose buffer (default) or table rows (t2)
+    char* qlds = rowbuf;
     const int r = lane & 7;
 
     // this wave's task sequence: t_begin, t_begin + t_step, ... (< t_end)
@@ -711,8 +751,19 @@ __global__ __launch_bounds__(kGroupThreads, 4) void decode_kernel(const void* __
         if constexpr (kFmt == 0) {
             if (cc.qt0 != q_tables[0] || cc.qt1 != q_tables[1] || cc.qt2 != q_tables[2]) {
                 q_tables[0] = cc.qt0; q_tables[1] = cc.qt1; q_tables[2] = cc.qt2;
+                if constexpr (L::t2) {
+                    // lane group c < 3 writes component c's row r into the wave's
+                    // table copy (read by later DS ops of this wave, in order)
+                    const int c = lane >> 3;
+                    if (c < 3) {
+                        uint32_t qq[4];
+                        load_qrow_pk(qt_pool, c == 0 ? q_tables[0] : c == 1 ? q_tables[1] : q_tables[2], r, qq);
+                        *reinterpret_cast<uint4*>(qlds + c * 128 + r * 16) = make_uint4(qq[0], qq[1], qq[2], qq[3]);
+                    }
+                } else {
 #pragma unroll
-                for (int c = 0; c < 3; ++c) load_qrow_pk(qt_pool, q_tables[c], r, q[c]);
+                    for (int c = 0; c < 3; ++c) load_qrow_pk(qt_pool, q_tables[c], r, q[c]);
+                }
             }
 #pragma unroll
             for (int k = 0; k < 6; ++k) {
@@ -730,7 +781,7 @@ __global__ __launch_bounds__(kGroupThreads, 4) void decode_kernel(const void* __
         }
 
         if constexpr ((kVariant & kAblNoIdct) == 0)
-            idct_stage<kSampling, kFmt>(slots, rowbuf, lane, zoff, q,
+            idct_stage<kSampling, kFmt>(slots, rowbuf, lane, zoff, q, qlds,
                                         static_cast<const int*>(coefs) + tg.blk0 * 64, tg.nblk);
 
         constexpr int kRows = KGeom<kSampling>::kMcuH;

@@ -8,8 +8,10 @@ idct.h compatibility shim (include/idct.h) and the host JPEG front end
 """
 from __future__ import annotations
 
+import json
 import os
 import subprocess
+import time
 import sys
 from concurrent.futures import ThreadPoolExecutor
 
@@ -51,7 +53,7 @@ def _headers():
 
 
 def build(verbose: bool = False, force: bool = False, ablation: bool = False, variant: str = "",
-          defines=()) -> str:
+          defines=(), record: bool = False) -> str:
     """ablation=True builds the TUNING-ONLY library build/ablation/libhjd.so with
     -DHJD_ABLATION (stage-skipping kernel variants for tools/tune.py; wrong
     outputs by design).  Load it with HJD_LIB=build/ablation/libhjd.so.
@@ -90,6 +92,11 @@ def build(verbose: bool = False, force: bool = False, ablation: bool = False, va
         if force or _needs(o, [s] + headers):
             # host-only C++ (no device code): compiled by hipcc's clang as plain C++
             jobs.append([HIPCC, *COMMON, "-x", "c++", "-pthread", "-c", s, "-o", o])
+    t0 = time.time()
+    if force:   # a forced build starts from an empty object directory
+        for f in os.listdir(OBJDIR):
+            if f.endswith(".o"):
+                os.remove(os.path.join(OBJDIR, f))
     with ThreadPoolExecutor(max_workers=min(8, max(1, len(jobs)))) as ex:
         for out in ex.map(_run, jobs):
             if verbose and out.strip():
@@ -98,6 +105,14 @@ def build(verbose: bool = False, force: bool = False, ablation: bool = False, va
         out = _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", "-o", LIB, *objs])
         if verbose and out.strip():
             print(out)
+    if record:
+        rec = {"build_mode": "full" if force else "incremental", "objects_compiled": len(jobs),
+               "objects_linked": len(objs), "sources": [os.path.relpath(j[-3], REPO) for j in jobs], "arch": ARCH,
+               "library": os.path.relpath(LIB, REPO), "library_bytes": os.path.getsize(LIB),
+               "seconds": round(time.time() - t0, 1), "utc": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())}
+        with open(os.path.join(REPO, "build", "build_record.json"), "w") as f:
+            json.dump(rec, f, indent=1)
+        print("build_record:", json.dumps(rec))
     return LIB
 
 
