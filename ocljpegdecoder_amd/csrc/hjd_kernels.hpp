@@ -673,6 +673,34 @@ __device__ __forceinline__ void idct_stage(char* __restrict__ slots, char* __res
     }
 }
 
+#ifndef HJD_XCD
+#define HJD_XCD 1
+#endif
+#ifndef HJD_XCD_CHUNK
+#define HJD_XCD_CHUNK 0
+#endif
+// Logical position of workgroup `bid` in the task order.  The hardware deals
+// consecutive workgroups to the 8 XCDs in turn, so in launch order adjacent
+// strips land in 8 different L2s.  With HJD_XCD (default on) each XCD's
+// groups cover contiguous task ranges instead: XCD x = bid % 8 takes runs of
+// HJD_XCD_CHUNK consecutive positions (0: one contiguous eighth of the grid,
+// x*q + min(x, rem) + bid/8), the tail that does not fill 8 runs keeps launch
+// order.
+__device__ __forceinline__ uint32_t group_order(uint32_t bid, uint32_t ngroups)
+{
+    if constexpr (HJD_XCD == 0) {
+        return bid;
+    } else if constexpr (HJD_XCD_CHUNK == 0) {
+        const uint32_t x = bid & 7, k = bid >> 3, q = ngroups >> 3, rem = ngroups & 7;
+        return x * q + min(x, rem) + k;
+    } else {
+        constexpr uint32_t C = HJD_XCD_CHUNK;
+        if (bid >= ngroups / (8 * C) * (8 * C)) return bid;
+        const uint32_t x = bid & 7, k = bid >> 3;
+        return ((k / C) * 8 + x) * C + k % C;
+    }
+}
+
 // The fused kernel.  Persistent grid; wave w owns the contiguous task range
 // [w*T/W, (w+1)*T/W) so its frame changes rarely and the frame record stays in
 // SGPRs; the next task's coefficients are prefetched into VGPRs while the
@@ -704,7 +732,7 @@ __global__ __launch_bounds__(kGroupThreads, KLayout<kSampling>::min_waves) void 
         t_step = kWavesPerGroup;
     } else {
         const int64_t nwaves = static_cast<int64_t>(gridDim.x) * kWavesPerGroup;
-        const int64_t gw = static_cast<int64_t>(blockIdx.x) * kWavesPerGroup + wave;
+        const int64_t gw = static_cast<int64_t>(group_order(blockIdx.x, gridDim.x)) * kWavesPerGroup + wave;
         const int64_t chunk = total_tasks / nwaves, rem = total_tasks % nwaves;
         t_begin = gw * chunk + min(gw, rem);
         t_end = t_begin + chunk + (gw < rem ? 1 : 0);

@@ -407,14 +407,20 @@ int64_t hjd_plan_coef_bytes(const hjd_plan* plan) { return plan ? plan->coef_byt
 // r01_tune_grid_*.json): the hardware dispatches groups in order, so the
 // resident waves always work inside a narrow window of the batch and HBM sees
 // far better locality than with 4096 persistent waves spread over the whole
-// batch (4:2:0 +12 %, 4:4:4 +13 % over one persistent wave per slot).  The
-// heavier 4:4:4 tasks still profit from the one-task-ahead prefetch, so their
-// waves take ~8 tasks; 4:2:0 waves take one (4:2:2 and gray: 8, like 4:4:4).
+// batch (4:2:0 +12 %, 4:4:4 +13 % over one persistent wave per slot).  With
+// the XCD-contiguous group order (hjd_kernels.hpp group_order) the best chunk
+// is 2 tasks per wave at 4:2:0 (+3.9 % over 1 on 1024-frame batches) and 16 at
+// the heavier samplings (+1.3 % over 8; profiles/r02_tune_tasks_per_wave.json).
+// HJD_TASKS_PER_WAVE overrides it (tuning).
 static int decode_grid(int sampling, int fmt, int64_t tasks)
 {
+    static const int64_t env = [] {
+        const char* e = getenv("HJD_TASKS_PER_WAVE");
+        return e ? static_cast<int64_t>(atoll(e)) : int64_t(0);
+    }();
     // ... but never fewer than ~4 waves per SIMD (256 CUs x 4 SIMDs): a single
-    // 4:4:4 frame at 8 tasks per wave would leave most of the chip idle.
-    int64_t per_wave = (sampling == HJD_YUV420 && fmt == 0) ? 1 : 8;
+    // 4:4:4 frame at 16 tasks per wave would leave most of the chip idle.
+    int64_t per_wave = env > 0 ? env : (sampling == HJD_YUV420 && fmt == 0) ? 2 : 16;
     per_wave = std::max<int64_t>(1, std::min<int64_t>(per_wave, tasks / (4 * 1024)));
     const int64_t waves = (tasks + per_wave - 1) / per_wave;
     const int64_t groups = (waves + hjd::kWavesPerGroup - 1) / hjd::kWavesPerGroup;
