@@ -673,6 +673,9 @@ __device__ __forceinline__ void idct_stage(char* __restrict__ slots, char* __res
     }
 }
 
+#ifndef HJD_NT_LOAD
+#define HJD_NT_LOAD 1   // non-temporal coefficient loads (read once; +2.5 % 4:2:0, +1.2 % 4:4:4 same-box)
+#endif
 #ifndef HJD_XCD
 #define HJD_XCD 1
 #endif
@@ -759,7 +762,15 @@ __global__ __launch_bounds__(kGroupThreads, KLayout<kSampling>::min_waves) void 
         const int4* src = reinterpret_cast<const int4*>(static_cast<const short*>(coefs) + g.blk0 * 64);
         if (g.nblk == kTaskBlocks) {
 #pragma unroll
-            for (int k = 0; k < 6; ++k) pre[k] = src[lane + 64 * k];
+            for (int k = 0; k < 6; ++k) {
+#if HJD_NT_LOAD
+                typedef int i32x4 __attribute__((ext_vector_type(4)));
+                const i32x4 t = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(src) + lane + 64 * k);
+                pre[k] = make_int4(t.x, t.y, t.z, t.w);
+#else
+                pre[k] = src[lane + 64 * k];
+#endif
+            }
         } else {
 #pragma unroll
             for (int k = 0; k < 6; ++k) {
