@@ -342,9 +342,9 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
     ctx = hjd.Context(dev.index)
     gpu_entropy = wl.get("entropy") == "gpu"
     d2h = bool(wl.get("d2h"))
-    # 48-frame batches take S = 4096 in the entropy kernels (hjd_entropy.hip
-    # default_sub_bits); 8 slots keep several batches on the GPU at once:
-    # 100-102 Gpx/s against 89-97 for 32 x S = 2048 x 6 slots (profiles/r01_stream_batch_ab.json)
+    # 48-frame batches x 8 slots keep several batches on the GPU at once; the
+    # stream's decoders take S = 8192 in the entropy kernels (hjd_entropy.hip
+    # stream_sub_bits): 97-99 Gpx/s against 91-94 at S = 4096 (profiles/r02_stream_subbits.json)
     per_batch = int(os.environ.get("HJD_STREAM_BATCH", 16 if d2h else 48))
     nslots = int(os.environ.get("HJD_STREAM_SLOTS", 4 if d2h else 8))
     ofmt = wl.get("out_format", hjd.OUT_BGRX)

@@ -1716,6 +1716,19 @@ static int default_sub_bits(int max_frames)
     return max_frames >= 48 ? 2 * kDefaultSubBits : kDefaultSubBits;
 }
 
+// The stream's decoders: batches of several slots overlap on the GPU, so the
+// parallelism a single batch lacks at long subsequences comes from the other
+// slots, and fewer guessed starts to repair wins.  Measured end to end on the
+// config-5 stream (profiles/r02_stream_subbits.json): S = 8192 at 32-48
+// frames per batch x 8 slots gives 97-101 Gpx/s against 91-94 at S = 4096;
+// 16384 and 64-96-frame batches are slower.
+static int stream_sub_bits(int max_frames)
+{
+    const char* e = getenv("HJD_SUB_BITS");
+    if (e) return atoi(e);
+    return max_frames >= 24 ? 4 * kDefaultSubBits : default_sub_bits(max_frames);
+}
+
 int hjd_gdec_create(hjd_ctx* ctx, int max_frames, int64_t max_scan_bytes, int64_t max_blocks, int sub_bits,
                     hjd_gdec** out)
 {
@@ -2200,7 +2213,8 @@ int hjd_gstream_create(hjd_ctx* ctx, int max_frames, int64_t max_scan_bytes, int
                                                                        : hjd_internal::device_local_cpus(st->device);
     const std::vector<int> prev = hjd_internal::bind_current_thread(local);
     for (int s = 0; s < nslots; ++s) {
-        int rc = hjd_gdec_create(ctx, max_frames, max_scan_bytes, max_blocks, 0, &st->slots[s]);
+        int rc = hjd_gdec_create(ctx, max_frames, max_scan_bytes, max_blocks, stream_sub_bits(max_frames),
+                                 &st->slots[s]);
         if (rc == HJD_OK && hipStreamCreateWithFlags(&st->streams[s], hipStreamNonBlocking) != hipSuccess)
             rc = set_error(HJD_E_HIP, "hipStreamCreate");
         if (rc) {

@@ -29,7 +29,7 @@ def _pil(w, h, q, sub, seed, noise=20.0, gray=False, **kw):
     return b.getvalue()
 
 
-@pytest.mark.parametrize("sub_bits", [32, 64, 100, 1024, 4096])
+@pytest.mark.parametrize("sub_bits", [32, 64, 100, 1024, 4096, 8192, 16384])
 def test_golden_files(hjd, sub_bits):
     for name in O.golden_cases():
         data = open(os.path.join(O.GOLDEN, name + ".jpg"), "rb").read()

@@ -30,7 +30,7 @@ def _coefs_gpu(hjd, ctx, datas, sub_bits=0):
     return [host[o:o + i.nblocks] for o, i in zip(offs, infos)], status
 
 
-@pytest.mark.parametrize("sub_bits", [32, 256, 1024])
+@pytest.mark.parametrize("sub_bits", [32, 256, 1024, 8192])
 def test_golden_coefficients(hjd, ctx, sub_bits):
     cases = _golden_bytes()
     got, status = _coefs_gpu(hjd, ctx, [d for _, d in cases], sub_bits)
@@ -98,10 +98,12 @@ def test_mixed_batch_pixels_match_oracle(hjd, ctx):
         np.testing.assert_array_equal(o.cpu().numpy().view(np.uint32), exp)
 
 
-def test_4k_frames(hjd, ctx):
-    """Full-size 4K frames (BASELINE configs[4] input), both samplings."""
+@pytest.mark.parametrize("sub_bits", [0, 8192])
+def test_4k_frames(hjd, ctx, sub_bits):
+    """Full-size 4K frames (BASELINE configs[4] input), both samplings; S = 8192
+    is the stream's subsequence length."""
     datas = [_pil(3840, 2160, 90, 2, seed=7), _pil(3840, 2160, 90, 0, seed=8)]
-    got, status = _coefs_gpu(hjd, ctx, datas)
+    got, status = _coefs_gpu(hjd, ctx, datas, sub_bits)
     for d, g in zip(datas, got):
         ref, _ = hjd.decode_coefs(d)
         np.testing.assert_array_equal(g, ref)
@@ -155,7 +157,7 @@ def test_capacity_errors(hjd, ctx):
             gd.decode_coefs([d], coefs)              # too many scan bytes
 
 
-@pytest.mark.parametrize("max_frames,nslots,nthreads", [(3, 2, 1), (5, 3, 4), (16, 4, 16)])
+@pytest.mark.parametrize("max_frames,nslots,nthreads", [(3, 2, 1), (5, 3, 4), (16, 4, 16), (32, 3, 8)])
 def test_gstream_many_images(hjd, ctx, max_frames, nslots, nthreads):
     """GPU-entropy stream: many files of mixed geometry through rotating batches;
     pixels equal the reference's (golden) or the oracle on the host-decoded
