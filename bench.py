@@ -560,6 +560,9 @@ def main():
     ap.add_argument("--frames", type=int, default=0, help="override batch size")
     ap.add_argument("--grid", type=int, default=0, help="persistent grid (workgroups), 0 = default")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-stream", action="store_true",
+                    help="N=1 pixel workloads: skip the config-5 stream leg (a child bench.py run, reported "
+                         "under config5_stream)")
     ap.add_argument("--host-prep-only", action="store_true",
                     help="config-5 host side only, no GPU: per-GPU worker pools (see run_host_prep)")
     ap.add_argument("--pools", default="1,2,4,8", help="--host-prep-only: pool counts")
@@ -674,6 +677,12 @@ def main():
         if world == 1 and not args.no_cpu:
             log("running CPU baseline leg ...")
             cpu = cpu_baseline(pool_host, qt, wl, value)
+        stream5 = None
+        if world == 1 and not args.no_stream and args.workload == "4k420":
+            del coefs, out
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+            stream5 = config5_stream_leg()
         traffic = committed_traffic(args.workload, nf)
         res = {
             "metric": "Mpixels/s decoded (dequant+IDCT+colour) at 1/2/4/8 GPUs; % HBM roofline",
@@ -704,6 +713,7 @@ def main():
                          "kernel_ms_per_launch": round(kernel_ms, 4)},
             "cpu_baseline": cpu,
             "device_copy_GBps": copy_gbps,
+            "config5_stream": stream5,
         }
         if cpu and "reference" in cpu:
             res["cpu_reference"] = cpu.pop("reference")
@@ -713,6 +723,31 @@ def main():
     if not checked["ok"]:
         log("FATAL: the timed launch's output differs from the oracle:", checked)
         sys.exit(1)
+
+
+def config5_stream_leg():
+    """BASELINE configs[4] on this GPU, measured in the same default run: a child
+    `bench.py --workload stream4k420` (its own process and HIP context; started
+    as a child, never exec'd), whose line is summarised here.  Its Mpx/s is a
+    separate end-to-end figure (JPEG bytes in pinned host memory -> BGRX in
+    HBM), not the headline `value`."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--workload", "stream4k420", "--steps", "3", "--warmup", "1",
+           "--no-cpu"]
+    log("running config-5 stream leg:", " ".join(cmd[1:]))
+    try:
+        r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=420)
+    except subprocess.TimeoutExpired:
+        return {"error": "timeout after 420 s"}
+    line = next((l for l in reversed(r.stdout.splitlines()) if l.startswith("{")), None)
+    if r.returncode != 0 or line is None:
+        return {"error": f"rc {r.returncode}", "stderr_tail": r.stderr[-400:]}
+    d = json.loads(line)
+    return {"value": d["value"], "unit": d["unit"], "ms_per_step": d["ms_per_step"], "steps": d["steps"],
+            "frames_per_step": d["config"]["frames_per_gpu_per_step"], "workload": d["config"]["workload"],
+            "jpeg_GBps_in": d["end_to_end"]["jpeg_GBps_in"], "destuff": d["end_to_end"]["destuff"],
+            "output_checked_vs_oracle": d["end_to_end"]["output_checked_vs_oracle"],
+            "command": "python " + " ".join(["bench.py"] + cmd[2:])}
 
 
 if __name__ == "__main__":

@@ -12,7 +12,7 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.
 tail -1 $O/smoke.log
 timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err || { echo BENCH FAILED; tail $O/bench.err; exit 1; }
 cat $O/bench.json
-timeout -k 10 600 python bench.py --workload 4k444 --no-cpu > $O/bench444.json 2> $O/bench444.err || { echo BENCH444 FAILED; exit 1; }
+timeout -k 10 600 python bench.py --workload 4k444 --no-cpu --no-stream > $O/bench444.json 2> $O/bench444.err || { echo BENCH444 FAILED; exit 1; }
 timeout -k 10 600 python bench.py --workload stream4k420 --steps 3 --warmup 1 > $O/stream.json 2> $O/stream.err || { echo STREAM FAILED; exit 1; }
 python3 -c "
 import json

@@ -10,6 +10,6 @@ tail -1 $O/tests.log
 timeout -k 10 600 python tools/latency_sweep.py > $O/sweep.json 2> $O/sweep.err || { echo SWEEP FAILED; tail $O/sweep.err; exit 1; }
 cat $O/sweep.json
 for k in 200; do
-  timeout -k 10 300 python bench.py --workload fhd420 --steps $k --warmup 20 --no-cpu > $O/fhd_$k.json 2> $O/fhd_$k.err || { echo BENCH FAILED; tail $O/fhd_$k.err; exit 1; }
+  timeout -k 10 300 python bench.py --workload fhd420 --steps $k --warmup 20 --no-cpu --no-stream > $O/fhd_$k.json 2> $O/fhd_$k.err || { echo BENCH FAILED; tail $O/fhd_$k.err; exit 1; }
   python3 -c "import json; d=json.load(open('$O/fhd_$k.json')); print('fhd steps', $k, d['value'], d['ms_per_step'], d['roofline']['kernel_ms_per_launch'])"
 done

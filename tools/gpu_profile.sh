@@ -14,8 +14,8 @@ mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 for wl in $WLS; do
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/ktrace_$wl -o bench -- \
-      python3 $R/bench.py --workload $wl --steps 10 --warmup 2 --no-cpu > $OUT/ktrace_$wl.json 2> $OUT/ktrace_$wl.err || exit 1
+      python3 $R/bench.py --workload $wl --steps 10 --warmup 2 --no-cpu --no-stream > $OUT/ktrace_$wl.json 2> $OUT/ktrace_$wl.err || exit 1
   timeout -k 10 900 rocprofv3 -i $R/tools/pmc_traffic.txt --output-format csv -d $OUT/pmc_$wl -o pmc -- \
-      python3 $R/bench.py --workload $wl --steps 3 --warmup 1 --no-cpu > $OUT/pmc_$wl.json 2> $OUT/pmc_$wl.err || exit 1
+      python3 $R/bench.py --workload $wl --steps 3 --warmup 1 --no-cpu --no-stream > $OUT/pmc_$wl.json 2> $OUT/pmc_$wl.err || exit 1
 done
 echo "profile $TAG done"

@@ -16,13 +16,13 @@ cd /tmp && export TMPDIR=/tmp
 if [ "${2:-}" != "skip-pixel" ]; then
 for wl in 4k420 4k444; do
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ktrace_$wl -o bench -- \
-      python3 $R/bench.py --workload $wl --steps 10 --warmup 2 --no-cpu > $O/ktrace_$wl.json 2> $O/ktrace_$wl.err || { echo KTRACE $wl FAILED; tail $O/ktrace_$wl.err; exit 1; }
+      python3 $R/bench.py --workload $wl --steps 10 --warmup 2 --no-cpu --no-stream > $O/ktrace_$wl.json 2> $O/ktrace_$wl.err || { echo KTRACE $wl FAILED; tail $O/ktrace_$wl.err; exit 1; }
   echo "ktrace $wl ok"
   timeout -k 10 900 rocprofv3 -i $R/tools/pmc_traffic.txt --output-format csv -d $O/pmc_$wl -o pmc -- \
-      python3 $R/bench.py --workload $wl --steps 3 --warmup 1 --no-cpu > $O/pmc_$wl.json 2> $O/pmc_$wl.err || { echo PMC $wl FAILED; tail $O/pmc_$wl.err; exit 1; }
+      python3 $R/bench.py --workload $wl --steps 3 --warmup 1 --no-cpu --no-stream > $O/pmc_$wl.json 2> $O/pmc_$wl.err || { echo PMC $wl FAILED; tail $O/pmc_$wl.err; exit 1; }
   echo "pmc $wl ok"
   timeout -k 10 600 rocprofv3 -i $R/tools/pmc_pixel.txt --output-format csv -d $O/sq_$wl -o px -- \
-      python3 $R/bench.py --workload $wl --frames 256 --steps 2 --warmup 1 --no-cpu > $O/sq_$wl.json 2> $O/sq_$wl.err || { echo SQ $wl FAILED; tail $O/sq_$wl.err; exit 1; }
+      python3 $R/bench.py --workload $wl --frames 256 --steps 2 --warmup 1 --no-cpu --no-stream > $O/sq_$wl.json 2> $O/sq_$wl.err || { echo SQ $wl FAILED; tail $O/sq_$wl.err; exit 1; }
   python3 $R/tools/pmc_pixel_summary.py $O/sq_$wl > $O/sq_$wl.txt; cat $O/sq_$wl.txt
 done
 fi
@@ -33,5 +33,5 @@ timeout -k 10 600 rocprofv3 -i $R/tools/pmc_entropy.txt --output-format csv -d $
     python3 $R/tools/entropy_bench.py --frames 48 --reps 1 --pinned > $O/ent_pmc.json 2> $O/ent_pmc.err || { echo ENT PMC FAILED; tail -20 $O/ent_pmc.err; exit 1; }
 python3 $R/tools/pmc_entropy_summary.py $O/ent_pmc > $O/ent_pmc.txt; cat $O/ent_pmc.txt
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stream_kt -o stream -- \
-    python3 $R/bench.py --workload stream4k420 --steps 3 --warmup 1 --no-cpu > $O/stream_kt.json 2> $O/stream_kt.err || { echo STREAM KT FAILED; tail $O/stream_kt.err; exit 1; }
+    python3 $R/bench.py --workload stream4k420 --steps 3 --warmup 1 --no-cpu --no-stream > $O/stream_kt.json 2> $O/stream_kt.err || { echo STREAM KT FAILED; tail $O/stream_kt.err; exit 1; }
 echo "profile $TAG done"
