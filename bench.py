@@ -59,8 +59,9 @@ WORKLOADS = {
     "fhd420": dict(width=1920, height=1080, sampling=1, frames=1,
                    desc="BASELINE configs[1]: single 1920x1080 4:2:0 frame, one launch (cache/launch bound)"),
     "stream4k420": dict(width=3840, height=2160, sampling=1, frames=1024, entropy="gpu",
-                        desc="BASELINE configs[4] per GPU: stream of 4K 4:2:0 JPEGs (pool of 16 distinct q90 "
-                             "files); host parse+destuff workers || pinned H2D || GPU Huffman decode + fused kernel"),
+                        desc="BASELINE configs[4] per GPU: stream of 4K 4:2:0 JPEGs (pool of 64 distinct q90 "
+                             "files in pinned memory); host header parse || raw-scan DMA || GPU destuff + Huffman "
+                             "decode + fused kernel"),
     "stream4k420_d2h": dict(width=3840, height=2160, sampling=1, frames=256, entropy="gpu", d2h=True,
                             desc="BASELINE configs[4] per GPU, D2H-on (SURVEY s8(e)): as stream4k420, and every "
                                  "frame's BGRX copied back to pinned host memory"),
