@@ -40,6 +40,11 @@ import numpy as np
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
+# JPEG zigzag: natural index of zigzag position k (src/zigzag.h)
+ZIGZAG_NAT = [0, 1, 8, 16, 9, 2, 3, 10, 17, 24, 32, 25, 18, 11, 4, 5, 12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,
+              7, 14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51, 58, 59, 52, 45, 38, 31,
+              39, 46, 53, 60, 61, 54, 47, 55, 62, 63]
+
 WORKLOADS = {
     "4k420": dict(width=3840, height=2160, sampling=1, frames=1024,
                   desc="BASELINE configs[2]: batch of 1024 synthetic 3840x2160 4:2:0 frames, persistent kernel"),
@@ -56,6 +61,12 @@ WORKLOADS = {
     "4k420_bgr24": dict(width=3840, height=2160, sampling=1, frames=1024, out_format=1,
                         desc="extension (SURVEY s8(f) rank 4): configs[2] with 3-byte BGR24 output (24-bpp BMP "
                              "rows) instead of BGRX"),
+    "4k420_i32": dict(width=3840, height=2160, sampling=1, frames=1024, input="i32",
+                      desc="configs[2] in the idct.h-compat input format (SURVEY s8(d)): int32 natural-order "
+                           "dequantised blocks (jpg.mcu_data, src/jpeg.h:76), 10 B/px"),
+    "4k444_i32": dict(width=3840, height=2160, sampling=0, frames=1024, input="i32",
+                      desc="configs[3] in the idct.h-compat input format: int32 natural-order dequantised "
+                           "blocks, 16 B/px"),
     "fhd420": dict(width=1920, height=1080, sampling=1, frames=1,
                    desc="BASELINE configs[1]: single 1920x1080 4:2:0 frame, one launch (cache/launch bound)"),
     "stream4k420": dict(width=3840, height=2160, sampling=1, frames=1024, entropy="gpu",
@@ -610,9 +621,26 @@ def main():
 
     # ---- inputs resident in HBM --------------------------------------------------
     npool = min(POOL, nf)
-    coefs = torch.empty((nf, nblk, 64), dtype=torch.int16, device=dev)
+    i32 = wl.get("input") == "i32"
+    pool16 = torch.empty((npool, nblk, 64), dtype=torch.int16, device=dev)
     for i in range(npool):
-        coefs[i] = synth_frame_gpu(torch, nblk, s, qt, seed=1000 * rank + i, device=dev)
+        pool16[i] = synth_frame_gpu(torch, nblk, s, qt, seed=1000 * rank + i, device=dev)
+    if i32:
+        # the idct.h format: dequantised (src/decoder.cpp:338-342) int32 in natural order
+        inv = [0] * 64
+        for k, n in enumerate(ZIGZAG_NAT):
+            inv[n] = k
+        comp = torch.from_numpy(hjd.block_components(s, nblk)).to(dev)
+        qz = torch.from_numpy(np.asarray(qt, dtype=np.int32)).to(dev)[comp]          # [nblk, 64] file order
+        src = (pool16.to(torch.int32) * qz)[:, :, torch.tensor(inv, device=dev)]     # natural order
+        coefs = torch.empty((nf, nblk, 64), dtype=torch.int32, device=dev)
+        for i in range(npool):
+            coefs[i] = src[i]
+        del src
+    else:
+        coefs = torch.empty((nf, nblk, 64), dtype=torch.int16, device=dev)
+        for i in range(npool):
+            coefs[i] = pool16[i]
     for i in range(npool, nf):
         coefs[i].copy_(coefs[i % npool])
     ofmt = wl.get("out_format", hjd.OUT_BGRX)
@@ -621,7 +649,7 @@ def main():
     specs = [hjd.FrameSpec(w, h, s, coef_offset=i * nblk, out_offset=i * h * pitch, out_pitch=pitch,
                            qt_index=(0, 1, 2), out_format=ofmt) for i in range(nf)]
     ctx = hjd.Context(dev.index)
-    plan = hjd.Plan(ctx, specs, hjd.IN_Q16_ZIGZAG, qtables=qt)
+    plan = hjd.Plan(ctx, specs, hjd.IN_I32_NATURAL if i32 else hjd.IN_Q16_ZIGZAG, qtables=None if i32 else qt)
     torch.cuda.synchronize()
 
     stream = torch.cuda.current_stream()
@@ -670,7 +698,7 @@ def main():
         pass
 
     # every frame of the timed launch's output vs the oracle (outside the timed region)
-    pool_host = coefs[:npool].cpu().numpy()
+    pool_host = pool16.cpu().numpy()
     checked = check_batch_vs_oracle(torch, out, pool_host, qt, wl, ofmt)
 
     if rank == 0:
@@ -700,7 +728,9 @@ def main():
             "data": "synthetic (device-generated FDCT+quantised smooth+noise blocks, pool of "
                     f"{npool} distinct frames replicated to {nf}); inputs resident in HBM",
             "config": {"workload": wl["desc"], "frames_per_gpu": nf, "width": w, "height": h,
-                       "sampling": SAMPLING_NAMES[s], "input": "int16 quantised zigzag + qtables",
+                       "sampling": SAMPLING_NAMES[s],
+                       "input": "int32 natural-order dequantised (idct.h format)" if i32
+                                else "int16 quantised zigzag + qtables",
                        "output": "BGRX 4 B/px in HBM" if ofmt == hjd.OUT_BGRX else "BGR24 3 B/px in HBM",
                        "parallelism": f"image-parallel x{world} (no collective)",
                        "tasks_per_launch": plan.tasks},
