@@ -707,11 +707,11 @@ def main():
             log("running CPU baseline leg ...")
             cpu = cpu_baseline(pool_host, qt, wl, value)
         stream5 = None
-        if world == 1 and not args.no_stream and args.workload == "4k420":
+        if not args.no_stream and args.workload == "4k420":
             del coefs, out
             torch.cuda.synchronize()
             torch.cuda.empty_cache()
-            stream5 = config5_stream_leg()
+            stream5 = config5_stream_leg(world, args.dist_backend)
         traffic = committed_traffic(args.workload, nf)
         res = {
             "metric": "Mpixels/s decoded (dequant+IDCT+colour) at 1/2/4/8 GPUs; % HBM roofline",
@@ -756,29 +756,56 @@ def main():
         sys.exit(1)
 
 
-def config5_stream_leg():
-    """BASELINE configs[4] on this GPU, measured in the same default run: a child
-    `bench.py --workload stream4k420` (its own process and HIP context; started
-    as a child, never exec'd), whose line is summarised here.  Its Mpx/s is a
-    separate end-to-end figure (JPEG bytes in pinned host memory -> BGRX in
-    HBM), not the headline `value`."""
+def config5_stream_leg(world, dist_backend):
+    """BASELINE configs[4] on the same GPUs, measured in the same default run:
+    rank 0 starts a child `bench.py --workload stream4k420` (N=1: plain python;
+    N>1: torch.distributed.run over the same N GPUs on a fresh port, the frame
+    ids sharded round-robin, no data-path collective) and summarises its line.
+    The child has its own processes and HIP contexts (started as children,
+    never exec'd; the torchrun variables of this rank are not passed on).  Its
+    Mpx/s is the whole-job end-to-end figure (JPEG bytes in pinned host memory
+    -> BGRX in HBM), not the headline `value`."""
+    import signal
+    import socket
     import subprocess
-    cmd = [sys.executable, os.path.abspath(__file__), "--workload", "stream4k420", "--steps", "3", "--warmup", "1",
-           "--no-cpu"]
+    args = [os.path.abspath(__file__), "--gpus", str(world), "--workload", "stream4k420", "--steps", "3",
+            "--warmup", "1", "--no-cpu", "--dist-backend", dist_backend]
+    if os.environ.get("HJD_BENCH_STREAM_FRAMES"):   # tests: smaller steps
+        args += ["--frames", os.environ["HJD_BENCH_STREAM_FRAMES"]]
+    if world == 1:
+        cmd = [sys.executable] + args
+    else:
+        sk = socket.socket()
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+        sk.close()
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+               "--master-addr", "127.0.0.1", "--master-port", str(port)] + args
+    drop = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE", "ROLE_RANK",
+            "ROLE_NAME", "ROLE_WORLD_SIZE", "MASTER_PORT", "TORCHELASTIC_RUN_ID", "TORCHELASTIC_RESTART_COUNT",
+            "TORCHELASTIC_MAX_RESTARTS", "TORCHELASTIC_USE_AGENT_STORE", "TORCHELASTIC_ERROR_FILE",
+            "TORCHELASTIC_ENABLED")
+    env = {k: v for k, v in os.environ.items() if k not in drop}
     log("running config-5 stream leg:", " ".join(cmd[1:]))
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env,
+                         start_new_session=True)
     try:
-        r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=420)
+        out, err = p.communicate(timeout=600)
     except subprocess.TimeoutExpired:
-        return {"error": "timeout after 420 s"}
-    line = next((l for l in reversed(r.stdout.splitlines()) if l.startswith("{")), None)
-    if r.returncode != 0 or line is None:
-        return {"error": f"rc {r.returncode}", "stderr_tail": r.stderr[-400:]}
+        os.killpg(p.pid, signal.SIGKILL)   # the child's own process group (its torchrun workers included)
+        p.communicate()
+        return {"error": "timeout after 600 s"}
+    line = next((l for l in reversed(out.splitlines()) if l.startswith("{")), None)
+    if p.returncode != 0 or line is None:
+        return {"error": f"rc {p.returncode}", "stderr_tail": err[-400:]}
     d = json.loads(line)
-    return {"value": d["value"], "unit": d["unit"], "ms_per_step": d["ms_per_step"], "steps": d["steps"],
-            "frames_per_step": d["config"]["frames_per_gpu_per_step"], "workload": d["config"]["workload"],
+    return {"value": d["value"], "unit": d["unit"], "n_gpus": d["n_gpus"], "ms_per_step": d["ms_per_step"],
+            "steps": d["steps"], "frames_per_gpu_per_step": d["config"]["frames_per_gpu_per_step"],
+            "workload": d["config"]["workload"], "sharding": d["config"]["sharding"],
             "jpeg_GBps_in": d["end_to_end"]["jpeg_GBps_in"], "destuff": d["end_to_end"]["destuff"],
             "output_checked_vs_oracle": d["end_to_end"]["output_checked_vs_oracle"],
-            "command": "python " + " ".join(["bench.py"] + cmd[2:])}
+            "command": " ".join(["python"] + [os.path.basename(c) if c.endswith("bench.py") else c
+                                              for c in cmd[1:]])}
 
 
 if __name__ == "__main__":

@@ -23,7 +23,7 @@ def _free_port():
     return p
 
 
-def _run(workload, frames, extra=(), ranks=2, steps=3):
+def _run(workload, frames, extra=(), ranks=2, steps=3, timeout=110):
     env = dict(os.environ, HJD_BENCH_SAME_DEVICE="1", MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="4")
     args = [os.path.join(ROOT, "bench.py"), "--gpus", str(ranks), "--steps", str(steps), "--warmup", "1",
             "--workload", workload, "--frames", str(frames), "--no-cpu", *extra]
@@ -32,7 +32,7 @@ def _run(workload, frames, extra=(), ranks=2, steps=3):
     else:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(ranks),
                "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), *args, "--dist-backend", "gloo"]
-    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, p.stdout[-3000:]           # rank 0 only, one line
@@ -41,7 +41,16 @@ def _run(workload, frames, extra=(), ranks=2, steps=3):
 
 @pytest.mark.gpu
 def test_two_ranks_pixel_bench():
-    r = _run("4k420", 8)
+    """The driver's N>1 command line: the pixel line, and the config-5 stream leg
+    that rank 0 runs as a child torch.distributed.run over the same ranks
+    (HJD_BENCH_STREAM_FRAMES keeps its steps small here)."""
+    extra_env = {"HJD_BENCH_STREAM_FRAMES": "12", "HJD_STREAM_POOL": "8"}
+    os.environ.update(extra_env)
+    try:
+        r = _run("4k420", 8, timeout=240)
+    finally:
+        for k in extra_env:
+            os.environ.pop(k, None)
     assert r["n_gpus"] == 2 and r["steps"] == 3 and r["warmup"] == 1
     assert r["scaling"] == "weak" and r["higher_is_better"] is True
     assert r["value"] > 0 and r["ms_per_step"] > 0
@@ -49,6 +58,10 @@ def test_two_ranks_pixel_bench():
     px = 2 * 3 * 8 * 3840 * 2160
     assert abs(r["value"] - px / (r["ms_per_step"] * 3 / 1e3) / 1e6) / r["value"] < 0.02
     assert "no collective" in r["config"]["parallelism"] or "x2" in r["config"]["parallelism"]
+    s5 = r["config5_stream"]
+    assert "error" not in s5, s5
+    assert s5["n_gpus"] == 2 and s5["value"] > 0 and s5["output_checked_vs_oracle"] is True
+    assert s5["frames_per_gpu_per_step"] == 12 and "shard_round_robin over 2 rank(s)" in s5["sharding"]
 
 
 @pytest.mark.gpu
