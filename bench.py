@@ -711,6 +711,8 @@ def main():
             del coefs, out
             torch.cuda.synchronize()
             torch.cuda.empty_cache()
+            if world > 1:
+                dist.destroy_process_group()   # the other ranks are leaving; the child run has its own group
             stream5 = config5_stream_leg(world, args.dist_backend)
         traffic = committed_traffic(args.workload, nf)
         res = {
@@ -749,11 +751,34 @@ def main():
         if cpu and "reference" in cpu:
             res["cpu_reference"] = cpu.pop("reference")
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if world > 1 and dist.is_initialized():
         dist.destroy_process_group()
     if not checked["ok"]:
         log("FATAL: the timed launch's output differs from the oracle:", checked)
         sys.exit(1)
+
+
+def _wait_sibling_ranks_exit(timeout_s=60.0):
+    """Best effort, N>1: before rank 0 starts the child ranks, let the other
+    ranks of this run (children of the same torchrun agent) exit, so the GPUs
+    never carry both generations of processes."""
+    agent, me = os.getppid(), os.getpid()
+    deadline = time.time() + timeout_s
+    while time.time() < deadline:
+        alive = 0
+        for d in os.listdir("/proc"):
+            if not d.isdigit() or int(d) == me:
+                continue
+            try:
+                with open(f"/proc/{d}/stat") as f:
+                    fields = f.read().rsplit(")", 1)[1].split()
+            except OSError:
+                continue
+            if int(fields[1]) == agent and fields[0] not in ("Z", "X"):
+                alive += 1
+        if alive == 0:
+            return
+        time.sleep(0.5)
 
 
 def config5_stream_leg(world, dist_backend):
@@ -786,6 +811,8 @@ def config5_stream_leg(world, dist_backend):
             "TORCHELASTIC_MAX_RESTARTS", "TORCHELASTIC_USE_AGENT_STORE", "TORCHELASTIC_ERROR_FILE",
             "TORCHELASTIC_ENABLED")
     env = {k: v for k, v in os.environ.items() if k not in drop}
+    if world > 1:
+        _wait_sibling_ranks_exit()
     log("running config-5 stream leg:", " ".join(cmd[1:]))
     p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env,
                          start_new_session=True)
