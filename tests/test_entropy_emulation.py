@@ -130,3 +130,21 @@ def test_corrupt_inputs_rejected(hjd):
     cut = data[: info.scan_offset + 40] + b"\xff\xd9"
     with pytest.raises(hjd._lib.HjdError):
         hjd.emulate_entropy(cut)
+
+
+def test_emulation_asan_fuzz():
+    """The GPU entropy decoder's algorithm (host build of the same destuff,
+    sync/link/repair and write code) under AddressSanitizer + UBSan, fed
+    damaged single-scan JPEGs of several sizes at random S
+    (tools/fuzz/run_entropy.sh): no read past a frame's padded bit string, no
+    write past its blocks, corrupt data flagged rather than decoded."""
+    import os
+    import shutil
+    import subprocess
+    if shutil.which("g++") is None or not os.path.exists("/opt/rocm/bin/hipcc"):
+        pytest.skip("no toolchain")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run(["bash", os.path.join(root, "tools", "fuzz", "run_entropy.sh"), "150"], capture_output=True,
+                       text=True, timeout=900)
+    assert p.returncode == 0, (p.stdout + p.stderr)[-3000:]
+    assert "entropy mutants" in p.stdout
