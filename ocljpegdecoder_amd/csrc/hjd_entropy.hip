@@ -142,6 +142,7 @@ struct Prepared {
     uint32_t data_bits = 0;
     size_t data_off = 0;       // in the batch data area
     int ntab = 0;
+    int restart_mcus = 0;      // DRI (0: none)
     HuffLut tabs[kMaxTables];
     uint16_t jinfo[6] = {0, 0, 0, 0, 0, 0};
     std::vector<uint32_t> seg_end;
@@ -171,6 +172,7 @@ int prepare(const uint8_t* data, size_t size, uint8_t* dst, size_t cap, Prepared
     pf.sampling = h.sampling;
     pf.bpm = h.bpm;
     pf.nblocks = h.nblocks;
+    pf.restart_mcus = h.restart_interval;
     memcpy(pf.qt, h.qt, sizeof(pf.qt));
     // tables referenced by the scan, deduplicated into slots
     int slot_of[2][4];
@@ -359,6 +361,7 @@ __host__ __device__ __forceinline__ RunCtx make_ctx(const EntBatchDev& b, const 
     c.nseg = F.nseg;
     c.data_bits = F.data_bits;
     c.bpm = F.bpm;
+    c.seg_blocks = F.seg_blocks;
     return c;
 }
 
@@ -746,7 +749,7 @@ __global__ __launch_bounds__(kWriteThreads) void ent_write_kernel(EntBatchDev b)
     SubStats st = stats_identity();
     run<true>(c, entry, stop, st, &o);
     uint32_t bad = (st.flags & kError) ? kStatusCorrupt : 0;
-    if (second && ku == F.nsub - 1 && excl.nblk + st.nblk < F.nblocks) bad |= kStatusCount;
+    if (second && ku == F.nsub - 1 && excl.nblk + st.nblk != F.nblocks) bad |= kStatusCount;
     if (bad) atomicOr(&b.status[f], bad);
 }
 
@@ -1195,7 +1198,7 @@ void emulate(const EntBatchDev& b)
                 run<true>(c, half ? b.mids[F.sub_base + i] : b.entries[F.sub_base + i],
                           half ? (i + 1) * S : i * S + S / 2, s, &o);
                 if (s.flags & kError) b.status[f] |= kStatusCorrupt;
-                if (half && i == F.nsub - 1 && p.nblk + s.nblk < F.nblocks) b.status[f] |= kStatusCount;
+                if (half && i == F.nsub - 1 && p.nblk + s.nblk != F.nblocks) b.status[f] |= kStatusCount;
             }
             pre = stats_combine(pre, b.stats[F.sub_base + i]);
         }
@@ -1420,6 +1423,7 @@ int hjd_gdec::assemble(uint8_t* blob, int16_t* coefs, int64_t* block_offsets, vo
         F.bpm = static_cast<uint8_t>(p.bpm);
         F.sampling = static_cast<uint8_t>(p.sampling);
         memcpy(F.jinfo, p.jinfo, sizeof(F.jinfo));
+        F.seg_blocks = F.nseg > 1 ? static_cast<uint32_t>(p.restart_mcus * p.bpm) : 0u;
         ef[i] = F;
         memcpy(tb + tab_base, p.tabs, sizeof(HuffLut) * p.ntab);
         memcpy(seg + seg_base, p.seg_end.data(), 4 * p.seg_end.size());

@@ -76,7 +76,7 @@ struct HuffLut {
 };
 static_assert(sizeof(HuffLut) == 2448, "HuffLut layout");
 
-// Per-frame record of an entropy batch (device, 64 B).
+// Per-frame record of an entropy batch (device, 80 B).
 struct EntFrame {
     uint64_t data_off;    // byte offset of the destuffed bit string in the batch data area (16-B aligned)
     uint64_t coef_off;    // first output block in the coefficient buffer
@@ -90,8 +90,10 @@ struct EntFrame {
     uint32_t tab_base;    // first HuffLut of this frame
     uint8_t ntab, bpm, sampling, pad0;
     uint16_t jinfo[6];    // per bitstream block j of an MCU: dc slot | ac slot << 3 | comp << 6 | out slot << 8
+    uint32_t seg_blocks;  // blocks of a full restart interval (DRI MCUs x bpm); 0 without restarts
+    uint32_t pad1[3];
 };
-static_assert(sizeof(EntFrame) == 64, "EntFrame layout");
+static_assert(sizeof(EntFrame) == 80, "EntFrame layout");
 
 // Per-subsequence statistics of a run; combined with an ordered, segmented
 // operator to get each subsequence's block index and DC predictors.
@@ -219,6 +221,7 @@ struct RunCtx {
     const BlockInfo* blocks;   // [bpm]
     uint32_t nseg, data_bits;
     int bpm;
+    uint32_t seg_blocks;       // EntFrame::seg_blocks
 };
 
 // The record of bitstream block j.
@@ -399,6 +402,9 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
             flags |= kReset;
             d0 = d1 = d2 = 0;
             p0 = p1 = p2 = 0;
+            // write mode: a restart interval starts with block seg * seg_blocks
+            // (T.81 B.2.1: every interval but the last holds DRI MCUs)
+            if (kWrite && c.seg_blocks && blk != seg * c.seg_blocks) flags |= kError;
         }
         uint32_t seg_end = c.seg_end[seg];
         if (seg_end < pos) flags |= kError;   // consumed before the window loads are issued
@@ -429,6 +435,10 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
                     if (left < 0 || (kWrite && owned)) flags |= kError;   // overrun / block cut by the pad
                     pos = seg_end;
                     ++seg;
+                    // write mode: the interval just closed must have held
+                    // exactly DRI MCUs (the host decoder counts them and resyncs
+                    // at the marker; a count that differs is corrupt data)
+                    if (kWrite && c.seg_blocks && seg < c.nseg && blk != seg * c.seg_blocks) flags |= kError;
                     j = 0;
                     z = 0;
                     bi = block_of(c, 0);

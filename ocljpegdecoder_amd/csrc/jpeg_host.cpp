@@ -316,7 +316,8 @@ void fill_info(const Frame& f, hjd_jpeg_info* info)
 }
 
 // Entropy-coded segment reader: 64-bit MSB-first accumulator, FF00 de-stuffing,
-// stops feeding (zeros) at the first marker.
+// fill bytes (FF FF) skipped as the reference's read_more_data does
+// (src/decoder.cpp:94-159), stops feeding (zeros) at the first marker.
 struct BitReader {
     const uint8_t* p;
     const uint8_t* end;
@@ -348,6 +349,9 @@ struct BitReader {
                 } else if (p + 1 < end && p[1] == 0x00) {
                     b = 0xFF;
                     p += 2;
+                } else if (p + 1 < end && p[1] == 0xFF) {
+                    ++p;                // a fill byte: the pair starts at the next 0xFF
+                    continue;           // (src/decoder.cpp:121-134, FF FF -> look at the next byte)
                 } else {
                     at_marker = true;   // leave p on the marker
                 }

@@ -332,3 +332,82 @@ def test_progressive_rejected_loudly(hjd, ctx):
     with hjd.GpuDecoder(ctx, 1, len(prog), info.nblocks) as gd:
         with pytest.raises(hjd._lib.HjdError, match="host decoder"):
             gd.decode_coefs([prog], coefs)
+
+
+def _mutants(seeds, n, seed):
+    """Damaged copies of single-scan JPEGs (byte flips, 0xFF / RSTn insertions,
+    truncation) that still parse as single-scan files."""
+    import ocljpegdecoder_amd as hjd
+    rng = np.random.default_rng(seed)
+    out = []
+    while len(out) < n:
+        d = bytearray(seeds[int(rng.integers(len(seeds)))])
+        for _ in range(int(rng.integers(1, 9))):
+            at = int(rng.integers(len(d)))
+            kind = int(rng.integers(4))
+            if kind == 0:
+                d[at] = 0xFF
+            elif kind == 1 and at + 1 < len(d):
+                d[at], d[at + 1] = 0xFF, 0xD0 + int(rng.integers(8))
+            else:
+                d[at] = int(rng.integers(256))
+        if rng.integers(4) == 0:
+            d = d[: int(rng.integers(1, len(d) + 1))]
+        try:
+            info = hjd.parse(bytes(d))
+        except Exception:
+            continue
+        if info.single_scan and 0 < info.nblocks <= 4096:
+            out.append(bytes(d))
+    return out
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_damaged_files_on_device(hjd, ctx, pinned):
+    """Damaged JPEGs through the device decoder (host destuff for pageable
+    bytes, the device destuff kernels for pinned ones) in batches of 8: no
+    fault, no write outside the batch's coefficient blocks (guard blocks keep
+    their sentinel), and every frame reported clean decodes to exactly the
+    host decoder's coefficients (the host emulation of the same code is
+    ASan-fuzzed on the CPU, tests/test_entropy_emulation.py)."""
+    import torch
+    seeds = [_pil(256, 128, 90, 2, seed=31), _pil(160, 96, 95, 0, seed=32, restart_marker_blocks=5),
+             _pil(200, 100, 75, 1, seed=33)]
+    muts = _mutants(seeds, 96, seed=5 + int(pinned))
+    guard = 64
+    checked = flagged = staged_out = 0
+    # every batch also holds two undamaged files, which must come out clean and
+    # exact next to their damaged neighbours
+    batches = [[seeds[k % 3], seeds[(k + 1) % 3]] + muts[b0:b0 + 6] for k, b0 in enumerate(range(0, len(muts), 6))]
+    while batches:
+        datas = batches.pop(0)
+        infos = [hjd.parse(d) for d in datas]
+        total = sum(i.nblocks for i in infos)
+        coefs = torch.full((total + guard, 64), 0x5A5A, dtype=torch.int16, device="cuda")
+        inputs = [hjd.pinned_bytes(d) for d in datas] if pinned else datas
+        with hjd.GpuDecoder(ctx, len(datas), sum(len(d) for d in datas), total, 64) as gd:
+            try:
+                offs = gd.decode_coefs(inputs, coefs)
+            except hjd._lib.HjdError:
+                # rejected while staging (e.g. RSTn out of order on the host
+                # destuff path): the whole call fails; retry its frames alone
+                if len(datas) > 1:
+                    batches += [[d] for d in datas]
+                else:
+                    staged_out += 1
+                continue
+            status = gd.sync(raise_on_error=False)
+        host = coefs.cpu().numpy()
+        assert (host[total:] == 0x5A5A).all(), "write past the batch's blocks"
+        for d, o, info, st in zip(datas, offs, infos, status):
+            if st & ~1:
+                assert d not in seeds, "an undamaged file was flagged"
+                flagged += 1
+                continue
+            try:
+                ref, _ = hjd.decode_coefs(d)
+            except Exception:
+                continue
+            np.testing.assert_array_equal(host[o:o + info.nblocks], ref)
+            checked += 1
+    assert flagged + staged_out > 0 and checked >= 2 * 16, (flagged, staged_out, checked)
