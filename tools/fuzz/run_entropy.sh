@@ -10,10 +10,11 @@ SAN="-Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host
 FLAGS="-std=c++17 -O1 -g -fno-omit-frame-pointer -I$R/include -I$R/ocljpegdecoder_amd/csrc"
 C=$R/ocljpegdecoder_amd/csrc
 pids=()
+newest_hdr=$(ls -t $C/*.hpp $C/*.h $R/include/*.h | head -1)
 for f in hjd_entropy hjd_runtime idct_compat stream_pipeline numa_affinity; do
-  [ $O/$f.o -nt $C/$f.hip ] || { /opt/rocm/bin/hipcc --offload-arch=gfx950 $FLAGS $SAN -c $C/$f.hip -o $O/$f.o & pids+=($!); }
+  [ $O/$f.o -nt $C/$f.hip ] && [ $O/$f.o -nt $newest_hdr ] || { /opt/rocm/bin/hipcc --offload-arch=gfx950 $FLAGS $SAN -c $C/$f.hip -o $O/$f.o & pids+=($!); }
 done
-[ $O/jpeg_host.o -nt $C/jpeg_host.cpp ] || { /opt/rocm/bin/hipcc -x c++ $FLAGS $SAN -c $C/jpeg_host.cpp -o $O/jpeg_host.o & pids+=($!); }
+[ $O/jpeg_host.o -nt $C/jpeg_host.cpp ] && [ $O/jpeg_host.o -nt $newest_hdr ] || { /opt/rocm/bin/hipcc -x c++ $FLAGS $SAN -c $C/jpeg_host.cpp -o $O/jpeg_host.o & pids+=($!); }
 for p in ${pids[@]+"${pids[@]}"}; do wait $p; done
 /opt/rocm/bin/hipcc -x c++ $FLAGS $SAN -c $R/tools/fuzz/entropy_emulate_fuzz.cpp -o $O/main.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -fsanitize=address,undefined -fno-gpu-sanitize $O/*.o -o $O/efuzz -lpthread
