@@ -291,9 +291,12 @@ __device__ __forceinline__ uint32_t perm(uint32_t s0, uint32_t s1, uint32_t sel)
 constexpr uint32_t kSelLoLo = 0x05040100u;   // (s1.lo16) | (s0.lo16 << 16)
 constexpr uint32_t kSelHiHi = 0x07060302u;   // (s1.hi16) | (s0.hi16 << 16)
 
-// The chroma terms of two pixels as int16 pairs (low half = first pixel).
+// The chroma terms of two pixels as int16 pairs: r = (r0, r1) (low half =
+// first pixel), bg0 = (b0, g0) and bg1 = (b1, g1) -- the B and G terms of one
+// pixel share a word, so each pixel's saturated B,G bytes come out of one
+// v_sat_pk_u8_i16 already in BGRX order.
 struct ChromaPair {
-    uint32_t r, g, b;
+    uint32_t r, bg0, bg1;
     int flagged;      // either pixel's G term needs the corrected path
 };
 
@@ -301,10 +304,25 @@ __device__ __forceinline__ ChromaPair pair_of(const ChromaTerms& c0, const Chrom
 {
     ChromaPair p;
     p.r = perm(c1.r, c0.r, kSelHiHi);
-    p.g = perm(c1.g, c0.g, kSelHiHi);
-    p.b = perm(c1.b, c0.b, kSelHiHi);
+    p.bg0 = perm(c0.g, c0.b, kSelHiHi);
+    p.bg1 = perm(c1.g, c1.b, kSelHiHi);
     p.flagged = static_cast<int>(g_flagged(c0)) | static_cast<int>(g_flagged(c1));
     return p;
+}
+
+// (ys.lo + c.lo, ys.lo + c.hi) and (ys.hi + c.lo, ys.hi + c.hi): one packed add
+// whose op_sel broadcasts one luma half to both lanes.
+__device__ __forceinline__ uint32_t pk_add16_ylo(uint32_t ys, uint32_t c)
+{
+    uint32_t r;
+    asm("v_pk_add_u16 %0, %1, %2 op_sel:[0,0] op_sel_hi:[0,1]" : "=v"(r) : "v"(ys), "v"(c));
+    return r;
+}
+__device__ __forceinline__ uint32_t pk_add16_yhi(uint32_t ys, uint32_t c)
+{
+    uint32_t r;
+    asm("v_pk_add_u16 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1]" : "=v"(r) : "v"(ys), "v"(c));
+    return r;
 }
 
 // G-term correction of one flagged pixel (see the block comment above).
@@ -317,23 +335,22 @@ __device__ __forceinline__ short g_fix(const ChromaTerms& c, int ys)
 
 // Two BGRX pixels from an int16 pair of level-shifted luma samples Ys = Y+128
 // (low half first) and their chroma pair.  kCheck applies g_fix; callers take
-// that path only when some lane of the wave has a flagged pixel.
+// that path only when some lane of the wave has a flagged pixel.  3 packed
+// adds, 3 saturating packs and 2 byte permutes per two pixels.
 template <bool kCheck>
 __device__ __forceinline__ void pixels2(uint32_t yspair, const ChromaPair& c, const ChromaTerms* c0,
                                         const ChromaTerms* c1, uint32_t& px0, uint32_t& px1)
 {
     const uint32_t R = sat_pk_u8(pk_add16(yspair, c.r));   // bytes r0 r1
-    uint32_t graw = pk_add16(yspair, c.g);
-    if constexpr (kCheck) {
-        const short d0 = g_fix(*c0, static_cast<short>(yspair));
-        const short d1 = g_fix(*c1, static_cast<int>(yspair) >> 16);
-        graw = __builtin_bit_cast(uint32_t, __builtin_bit_cast(s16x2, graw) + (s16x2){d0, d1});
+    uint32_t bg0 = pk_add16_ylo(yspair, c.bg0);            // (Ys0 + b0, Ys0 + g0)
+    uint32_t bg1 = pk_add16_yhi(yspair, c.bg1);            // (Ys1 + b1, Ys1 + g1)
+    if constexpr (kCheck) {   // +1 on the G lane (the high int16; a carry out of bit 31 is dropped)
+        bg0 += static_cast<uint32_t>(g_fix(*c0, static_cast<short>(yspair))) << 16;
+        bg1 += static_cast<uint32_t>(g_fix(*c1, static_cast<int>(yspair) >> 16)) << 16;
     }
-    const uint32_t G = sat_pk_u8(graw);                   // bytes g0 g1
-    const uint32_t B = sat_pk_u8(pk_add16(yspair, c.b));   // bytes b0 b1
-    const uint32_t T = perm(G, B, 0x05010400u);           // b0 g0 b1 g1
-    px0 = perm(R, T, 0x0c040100u);                        // b0 g0 r0 0
-    px1 = perm(R, T, 0x0c050302u);                        // b1 g1 r1 0
+    const uint32_t BG0 = sat_pk_u8(bg0), BG1 = sat_pk_u8(bg1);   // bytes b g
+    px0 = perm(R, BG0, 0x0c040100u);                      // b0 g0 r0 0
+    px1 = perm(R, BG1, 0x0c050100u);                      // b1 g1 r1 0
 }
 
 // Scalar form (one pixel, raw Y/U/V) on top of the same code, for the colour test hooks.
