@@ -38,11 +38,12 @@ from .backend import (  # noqa: E402
 )
 
 from .jpeg import (GpuDecoder, GpuJpegStream, JpegInfo, JpegStream, bmp_bytes, bmp_header,  # noqa: E402
-                   decode_coefs, decode_coefs_batch, decode_jpeg, emulate_entropy, parse, pinned_bytes)
+                   decode_coefs, decode_coefs_batch, decode_coefs_into, decode_jpeg, emulate_entropy, parse,
+                   pinned_bytes)
 
 __all__ = [
     "GpuDecoder", "GpuJpegStream", "JpegInfo", "JpegStream", "bmp_bytes", "bmp_header", "decode_coefs",
-    "decode_coefs_batch", "decode_jpeg", "emulate_entropy",
+    "decode_coefs_batch", "decode_coefs_into", "decode_jpeg", "emulate_entropy",
     "parse", "pinned_bytes",
     "Context", "FrameSpec", "Plan", "decode_frame", "device_count", "frame_blocks", "mcu_geometry",
     "YUV444", "YUV420", "YUV422", "GRAY", "YUV411_H4V1", "YUV440", "OTHER", "block_components", "KERNEL_AUTO", "KERNEL_PERSISTENT", "KERNEL_LATENCY", "OUT_BGRX", "OUT_BGR24", "OUT_BYTES", "default_pitch", "IN_Q16_ZIGZAG", "IN_I32_NATURAL",

@@ -1708,8 +1708,12 @@ extern "C" {
 // - 32 frames: S = 4096 is 6 % slower;
 // - 8 frames: S = 4096 is 34 % slower.
 // Hence 4096 for decoders sized for >= 48 frames per call (the stream's
-// 48-frame batches: profiles/r01_stream_batch_ab.json).  HJD_SUB_BITS
-// overrides it (tuning hook, tools/gpu_subbits_sweep.sh).
+// 48-frame batches: profiles/r01_stream_batch_ab.json).  A decoder for one or
+// two images is latency-bound by the serial chain of a subsequence: one FHD
+// q90 JPEG, end to end, takes 1.16 ms at S = 1024 against 1.35 ms at 2048
+// (512: 1.04 ms, but its 4096-bit warm-up overlap fails to link often enough
+// at 256 to fall back; profiles/r02_fhd_jpeg_subbits.json), so 1024 there.
+// HJD_SUB_BITS overrides it (tuning hook, tools/gpu_subbits_sweep.sh).
 static int default_sub_bits(int max_frames)
 {
     static const int env = [] {
@@ -1717,7 +1721,7 @@ static int default_sub_bits(int max_frames)
         return e ? atoi(e) : 0;
     }();
     if (env) return env;
-    return max_frames >= 48 ? 2 * kDefaultSubBits : kDefaultSubBits;
+    return max_frames >= 48 ? 2 * kDefaultSubBits : max_frames <= 2 ? kDefaultSubBits / 2 : kDefaultSubBits;
 }
 
 // The stream's decoders: batches of several slots overlap on the GPU, so the

@@ -70,6 +70,20 @@ def decode_coefs(data: bytes):
     return coefs, JpegInfo.from_c(info)
 
 
+def decode_coefs_into(data: bytes, out: np.ndarray) -> JpegInfo:
+    """Host Huffman decode into a caller-provided int16 [>= nblocks][64] array
+    (e.g. a pinned host tensor's numpy view, for an H2D copy straight after)."""
+    lib = _lib.load()
+    buf = _buf(data)
+    info = HjdJpegInfo()
+    check(lib.hjd_jpeg_parse(buf, len(data), ctypes.byref(info)), "hjd_jpeg_parse")
+    if out.dtype != np.int16 or out.ndim != 2 or out.shape[1] != 64 or not out.flags.c_contiguous:
+        raise ValueError("out must be a C-contiguous int16 [blocks][64] array")
+    check(lib.hjd_jpeg_decode_coefs(buf, len(data), ctypes.byref(info), out.ctypes.data_as(_i16p), out.shape[0]),
+          "hjd_jpeg_decode_coefs")
+    return JpegInfo.from_c(info)
+
+
 def decode_coefs_batch(datas: Sequence[bytes], nthreads: int = 0) -> List[np.ndarray]:
     """Decode many files on a host thread pool."""
     lib = _lib.load()
