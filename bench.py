@@ -439,11 +439,12 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
     ctx = hjd.Context(dev.index)
     gpu_entropy = wl.get("entropy") == "gpu"
     d2h = bool(wl.get("d2h"))
-    # 48-frame batches x 8 slots keep several batches on the GPU at once; the
+    # 32-frame batches x 10 slots keep several batches on the GPU at once; the
     # stream's decoders take S = 8192 in the entropy kernels (hjd_entropy.hip
-    # stream_sub_bits): 97-99 Gpx/s against 91-94 at S = 4096 (profiles/r02_stream_subbits.json)
-    per_batch = int(os.environ.get("HJD_STREAM_BATCH", 16 if d2h else 48))
-    nslots = int(os.environ.get("HJD_STREAM_SLOTS", 4 if d2h else 8))
+    # stream_sub_bits): 102-104 Gpx/s against 95-97 for 48 x 8 and 91-94 at
+    # S = 4096 on the same boxes (profiles/r02_stream_subbits.json)
+    per_batch = int(os.environ.get("HJD_STREAM_BATCH", 16 if d2h else 32))
+    nslots = int(os.environ.get("HJD_STREAM_SLOTS", 4 if d2h else 10))
     ofmt = wl.get("out_format", hjd.OUT_BGRX)
     pitch = hjd.default_pitch(w, ofmt)
     shape, dtype = ((h, w), torch.int32) if ofmt == hjd.OUT_BGRX else ((h, pitch), torch.uint8)
