@@ -351,7 +351,7 @@ struct EntBatchDev {
 
 // `blocks`: the frame's block_info() records (fill_blocks), LDS on the device.
 __host__ __device__ __forceinline__ RunCtx make_ctx(const EntBatchDev& b, const EntFrame& F, const HuffLut* tabs,
-                                                    const BlockInfo* blocks)
+                                                    const BlockInfo* blocks, const uint8_t* steps = nullptr)
 {
     RunCtx c;
     c.data = b.data + F.data_off;
@@ -362,7 +362,16 @@ __host__ __device__ __forceinline__ RunCtx make_ctx(const EntBatchDev& b, const 
     c.data_bits = F.data_bits;
     c.bpm = F.bpm;
     c.seg_blocks = F.seg_blocks;
+    c.steps = steps;
     return c;
+}
+
+// The frame's AC step tables (step_entry) from its LUTs: [table][1 << kLutBits].
+__host__ __device__ __forceinline__ void fill_steps(uint8_t* steps, const HuffLut* tabs, int ntab, int tid,
+                                                    int nthreads)
+{
+    for (int i = tid; i < (ntab << kLutBits); i += nthreads)
+        steps[i] = step_entry(tabs[i >> kLutBits], static_cast<uint32_t>(i) & ((1u << kLutBits) - 1));
 }
 
 // Host side of the block records (the kernels fill their LDS copy per thread).
@@ -440,6 +449,10 @@ __device__ __forceinline__ SubStats wave_reduce_ordered(SubStats v, int lane)
     return v;
 }
 
+#ifndef HJD_STEPS
+#define HJD_STEPS 1   // sync runs take the AC step tables (A/B hook: 0 = one unit per step)
+#endif
+
 // LDS layout of the sync kernel after the group's tables (dynamic shared memory).
 struct SyncLds {
     uint64_t x[kGroupSubs];      // current exit of each subsequence
@@ -450,13 +463,17 @@ struct SyncLds {
     SubStats wsum[kGroupSubs / 64];
 };
 
-__host__ __device__ constexpr size_t sync_lds_bytes(uint32_t ntab) { return sizeof(HuffLut) * ntab + sizeof(SyncLds); }
+__host__ __device__ constexpr size_t sync_lds_bytes(uint32_t ntab)
+{
+    return (sizeof(HuffLut) + (1u << kLutBits)) * ntab + sizeof(SyncLds);
+}
 
 __global__ __launch_bounds__(kGroupSubs) void ent_sync_kernel(EntBatchDev b)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     HuffLut* tabs = reinterpret_cast<HuffLut*>(smem);
-    SyncLds& L = *reinterpret_cast<SyncLds*>(smem + sizeof(HuffLut) * b.ntab_max);
+    uint8_t* steps = smem + sizeof(HuffLut) * b.ntab_max;
+    SyncLds& L = *reinterpret_cast<SyncLds*>(smem + (sizeof(HuffLut) + (1u << kLutBits)) * b.ntab_max);
     const int tid = threadIdx.x;
     const uint32_t w = blockIdx.x;
     const uint32_t f = b.wg_frame[w];
@@ -466,9 +483,11 @@ __global__ __launch_bounds__(kGroupSubs) void ent_sync_kernel(EntBatchDev b)
     // groups laid out for a device-destuffed frame's upper bound (raw bytes) past its real end
     if (gl >= frame_groups(F.nsub)) return;
     __shared__ BlockInfo blocks[kMaxBpm];
-    const RunCtx c = make_ctx(b, F, tabs, blocks);
+    const RunCtx c = make_ctx(b, F, tabs, blocks, HJD_STEPS ? steps : nullptr);
     load_tables(tabs, blocks, b.tabs + F.tab_base, F, b.frames + f, tid, kGroupSubs);
     if (tid < 2) L.nlist[tid] = 0;
+    __syncthreads();
+    fill_steps(steps, tabs, F.ntab, tid, kGroupSubs);
     __syncthreads();
     const int64_t k0 = group_sub(gl, 0);
     const int64_t k = k0 + tid;
@@ -1082,7 +1101,9 @@ void emulate(const EntBatchDev& b)
         const EntFrame& F = b.frames[b.wg_frame[w]];
         BlockInfo blocks[kMaxBpm];
         fill_blocks(blocks, F);
-        const RunCtx c = make_ctx(b, F, b.tabs + F.tab_base, blocks);
+        std::vector<uint8_t> steps(static_cast<size_t>(F.ntab) << kLutBits);
+        fill_steps(steps.data(), b.tabs + F.tab_base, F.ntab, 0, 1);
+        const RunCtx c = make_ctx(b, F, b.tabs + F.tab_base, blocks, steps.data());
         const uint32_t gl = w - F.wg_base;
         std::vector<uint64_t> used(kGroupSubs, 0), x(kGroupSubs, 0), xs0(kGroupSubs, 0), xs1(kGroupSubs, 0);
         std::vector<SubStats> st(kGroupSubs, stats_identity()), suf(kGroupSubs, stats_identity());

@@ -191,7 +191,8 @@ struct alignas(16) BlockInfo {
     uint32_t tdc, tac;
     int32_t m0, m1, m2;
     uint32_t ji;
-    uint32_t pad[2];
+    uint32_t sac;   // first entry of the AC table's step table (RunCtx::steps)
+    uint32_t pad;
 };
 static_assert(sizeof(BlockInfo) == 32, "BlockInfo layout");
 
@@ -205,7 +206,8 @@ __host__ __device__ __forceinline__ BlockInfo block_info(uint32_t ji)
     b.m1 = comp == 1;
     b.m2 = comp == 2;
     b.ji = ji;
-    b.pad[0] = b.pad[1] = 0;
+    b.sac = ((ji >> 3) & 7) << kLutBits;
+    b.pad = 0;
     return b;
 }
 
@@ -222,7 +224,41 @@ struct RunCtx {
     uint32_t nseg, data_bits;
     int bpm;
     uint32_t seg_blocks;       // EntFrame::seg_blocks
+    const uint8_t* steps;      // [table][1 << kLutBits] AC step entries (LDS), or null: one unit per step
 };
+
+// AC step entry (sync mode): the AC units that a 10-bit peek decodes
+// completely, taken in one step, since a sync run needs no AC values --
+// only how far they move pos and z.  One byte: [3:0] bits consumed, [7:4] 15
+// if the last unit is an EOB (the block ends), else how far the units move z
+// (<= 14; the units before an EOB also move it by <= 14).  0: the first
+// unit's code or extra bits reach past the peek (or it moves z by 15 or more);
+// one byte per entry keeps the sync kernel's LDS small.
+constexpr uint32_t kStepEnds = 15;
+__host__ __device__ __forceinline__ uint32_t step_bits(uint32_t e) { return e & 15; }
+__host__ __device__ __forceinline__ uint32_t step_zadv(uint32_t e) { return e >> 4; }   // kStepEnds: EOB
+
+// Step entry of an AC table for the kLutBits-bit prefix p: units decoded from
+// p alone, in order, until one does not fit, an EOB (taken, last) or z would
+// move by more than 14.  Every unit is one the LUT decodes (codes <= kLutBits bits).
+__host__ __device__ __forceinline__ uint8_t step_entry(const HuffLut& t, uint32_t p)
+{
+    uint32_t o = 0, zadv = 0;
+    while (o < static_cast<uint32_t>(kLutBits)) {
+        const uint32_t e = t.lut[(p << o) & ((1u << kLutBits) - 1)];
+        const uint32_t total = e & 31, zk = e >> 9;
+        if (e == 0 || o + total > static_cast<uint32_t>(kLutBits)) break;
+        if (zk == 64) {   // EOB: the block ends
+            o += total;
+            zadv = kStepEnds;
+            break;
+        }
+        if (zadv + zk >= kStepEnds) break;
+        zadv += zk;
+        o += total;
+    }
+    return static_cast<uint8_t>(o | zadv << 4);
+}
 
 // The record of bitstream block j.
 __host__ __device__ __forceinline__ BlockInfo block_of(const RunCtx& c, uint32_t j) { return c.blocks[j]; }
@@ -459,8 +495,29 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
                     continue;
                 }
             }
-            // ---- one unit: Huffman symbol + extra bits (unit_entry fields) ----
             const bool dc = z == 0;
+            // ---- sync mode: the AC units the peek holds, in one step ----
+            // Taken only where single units would give the same state: all of
+            // them end before `stop`, >= 8 bits before the segment end (no pad
+            // check in between), and z stays <= 63 (no index-63 error case).
+            if (!kWrite && c.steps && !dc) {
+                const uint32_t se = c.steps[bi.sac + (peek >> (32 - kLutBits))];
+                const uint32_t nb = step_bits(se), za = step_zadv(se);
+                const bool ends = za == kStepEnds;
+                // an EOB entry's units before the EOB move z by <= 14: z <= 49 keeps them <= 63
+                if (se != 0 && z + (ends ? 14 : za) <= 63 && left >= static_cast<int32_t>(nb) + 8 && pos + nb <= stop) {
+                    pos += nb;
+                    if (ends) {
+                        z = 0;
+                        j = j + 1 == static_cast<uint32_t>(c.bpm) ? 0 : j + 1;
+                        bi = block_of(c, j);
+                    } else {
+                        z += za;
+                    }
+                    continue;
+                }
+            }
+            // ---- one unit: Huffman symbol + extra bits (unit_entry fields) ----
             const HuffLut& t = *reinterpret_cast<const HuffLut*>(reinterpret_cast<const char*>(c.tabs) +
                                                                  (dc ? bi.tdc : bi.tac));
             uint32_t e = t.lut[peek >> (32 - kLutBits)];
