@@ -1628,6 +1628,7 @@ int gdec_issue(hjd_gdec* g, void* const* d_outs, const int32_t* pitches, int16_t
     int64_t moved = static_cast<int64_t>(g->H.used), host_bytes = 0;
     std::vector<void*> bd, bs;          // caller-pinned raw scans: one batched DMA submission
     std::vector<size_t> bn;
+    std::vector<std::pair<int, int>> bf;   // frames [first, last) each copy covers
     for (int i = 0; i < n;) {
         const Prepared& p = g->frames[i];
         const size_t len = p.destuff == kDestuffHost ? p.data_bits / 8 : p.raw_len;
@@ -1645,6 +1646,7 @@ int gdec_issue(hjd_gdec* g, void* const* d_outs, const int32_t* pitches, int16_t
             bd.push_back(g->d_raw + p.raw_off);
             bs.push_back(const_cast<uint8_t*>(p.raw_src));
             bn.push_back(span);
+            bf.emplace_back(i, j);
             moved += static_cast<int64_t>(span);
             i = j;
             continue;
@@ -1671,7 +1673,20 @@ int gdec_issue(hjd_gdec* g, void* const* d_outs, const int32_t* pitches, int16_t
     }
     // (hipMemcpyBatchAsync would submit these at once, but the HIP runtime this
     // library shares with PyTorch -- DESIGN.md s8 -- predates it)
-    for (size_t k = 0; k < bd.size(); ++k) HJD_HIP(hipMemcpyAsync(bd[k], bs[k], bn[k], hipMemcpyHostToDevice, s));
+    for (size_t k = 0; k < bd.size(); ++k) {
+        if (hipMemcpyAsync(bd[k], bs[k], bn[k], hipMemcpyHostToDevice, s) == hipSuccess) continue;
+        // A merged span can cross from one pinned allocation into another (the
+        // caller's buffers merely lie close together), which the DMA rejects
+        // before queueing anything: copy those scans one by one.
+        (void)hipGetLastError();
+        if (bf[k].second - bf[k].first < 2)
+            return set_error(HJD_E_HIP, "hipMemcpyAsync of a pinned scan (%zu bytes) failed", bn[k]);
+        for (int f = bf[k].first; f < bf[k].second; ++f) {
+            const Prepared& q = g->frames[f];
+            HJD_HIP(hipMemcpyAsync(g->d_raw + q.raw_off, const_cast<uint8_t*>(q.raw_src), q.raw_len,
+                                   hipMemcpyHostToDevice, s));
+        }
+    }
     g->last_h2d = moved;
     g->last_host_scan_bytes = host_bytes;
     HJD_HIP(hipEventRecord(g->staged, s));

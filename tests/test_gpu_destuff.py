@@ -174,6 +174,50 @@ def test_pinned_inputs_gpu_decoder(hjd, ctx, monkeypatch):
         assert s & ~1 == 0
 
 
+def test_pinned_scans_in_separate_registrations(hjd, ctx, monkeypatch):
+    """Two scans in separately page-locked ranges that lie less than 64 KiB
+    apart: the decoder mirrors their distance and tries one DMA over both,
+    which crosses the unregistered page between them and is rejected; it then
+    copies the scans one by one (torch's pinned blocks can lie this close)."""
+    import mmap
+    import torch
+    monkeypatch.setenv("HJD_DESTUFF", "auto")
+    datas = _pil_files()[:2]
+    page = mmap.PAGESIZE
+    n1 = -(-len(datas[0]) // page) * page
+    n2 = -(-len(datas[1]) // page) * page
+    mm = mmap.mmap(-1, n1 + page + n2)
+    arr = np.frombuffer(mm, np.uint8)
+    o1 = n1 - len(datas[0])                      # file 1 ends where region 1 ends
+    o2 = n1 + page                               # file 2 starts region 2, one page later
+    arr[o1:o1 + len(datas[0])] = np.frombuffer(datas[0], np.uint8)
+    arr[o2:o2 + len(datas[1])] = np.frombuffer(datas[1], np.uint8)
+    lib = hjd._lib.load()
+    base = arr.ctypes.data
+    hjd._lib.check(lib.hjd_host_register(ctypes.c_void_p(base), n1), "register 1")
+    hjd._lib.check(lib.hjd_host_register(ctypes.c_void_p(base + o2), n2), "register 2")
+    views = None
+    try:
+        views = [torch.from_numpy(arr[o1:o1 + len(datas[0])]), torch.from_numpy(arr[o2:o2 + len(datas[1])])]
+        infos = [hjd.parse(d) for d in datas]
+        total = sum(i.nblocks for i in infos)
+        coefs = torch.full((total, 64), 0x5A5A, dtype=torch.int16, device="cuda")
+        with hjd.GpuDecoder(ctx, 2, sum(map(len, datas)), total) as gd:
+            offs = gd.decode_coefs(views, coefs)
+            status = gd.sync()
+        host = coefs.cpu().numpy()
+        for d, o, i, s in zip(datas, offs, infos, status):
+            ref, _ = hjd.decode_coefs(d)
+            np.testing.assert_array_equal(host[o:o + i.nblocks], ref)
+            assert s & ~1 == 0
+    finally:
+        lib.hjd_host_unregister(ctypes.c_void_p(base + o2))
+        lib.hjd_host_unregister(ctypes.c_void_p(base))
+        views = None
+        del arr
+        mm.close()
+
+
 def test_pinned_inputs_stream_no_host_scan_bytes(hjd, ctx, monkeypatch):
     import torch
     monkeypatch.setenv("HJD_DESTUFF", "auto")
