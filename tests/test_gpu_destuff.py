@@ -202,7 +202,8 @@ def test_pinned_scans_in_separate_registrations(hjd, ctx, monkeypatch):
         infos = [hjd.parse(d) for d in datas]
         total = sum(i.nblocks for i in infos)
         coefs = torch.full((total, 64), 0x5A5A, dtype=torch.int16, device="cuda")
-        with hjd.GpuDecoder(ctx, 2, sum(map(len, datas)), total) as gd:
+        # raw-area capacity for the mirrored layout: both scans plus the page between
+        with hjd.GpuDecoder(ctx, 2, n1 + page + n2 + (1 << 16), total) as gd:
             offs = gd.decode_coefs(views, coefs)
             status = gd.sync()
         host = coefs.cpu().numpy()
@@ -213,9 +214,7 @@ def test_pinned_scans_in_separate_registrations(hjd, ctx, monkeypatch):
     finally:
         lib.hjd_host_unregister(ctypes.c_void_p(base + o2))
         lib.hjd_host_unregister(ctypes.c_void_p(base))
-        views = None
-        del arr
-        mm.close()
+        views = None   # the mapping goes with its last reference
 
 
 def test_pinned_inputs_stream_no_host_scan_bytes(hjd, ctx, monkeypatch):
