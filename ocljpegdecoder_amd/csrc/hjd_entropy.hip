@@ -241,7 +241,6 @@ int prepare(const uint8_t* data, size_t size, uint8_t* dst, size_t cap, Prepared
 // kernels are unchanged; the host only parses the header.
 constexpr uint32_t kTileBytes = 16384;
 constexpr int kTileThreads = 256;
-constexpr uint32_t kThreadBytes = kTileBytes / kTileThreads;   // 64 contiguous bytes per thread
 constexpr uint32_t kNoEnd = 0xFFFFFFFFu;
 
 // The raw bytes of a frame sit at any byte offset of the raw area (so that
