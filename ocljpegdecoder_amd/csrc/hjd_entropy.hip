@@ -365,12 +365,12 @@ __host__ __device__ __forceinline__ RunCtx make_ctx(const EntBatchDev& b, const 
     return c;
 }
 
-// The frame's AC step tables (step_entry) from its LUTs: [table][1 << kLutBits].
+// The frame's AC step tables (step_entry) from its LUTs: [table][1 << kStepBits].
 __host__ __device__ __forceinline__ void fill_steps(uint8_t* steps, const HuffLut* tabs, int ntab, int tid,
                                                     int nthreads)
 {
-    for (int i = tid; i < (ntab << kLutBits); i += nthreads)
-        steps[i] = step_entry(tabs[i >> kLutBits], static_cast<uint32_t>(i) & ((1u << kLutBits) - 1));
+    for (int i = tid; i < (ntab << kStepBits); i += nthreads)
+        steps[i] = step_entry(tabs[i >> kStepBits], static_cast<uint32_t>(i) & ((1u << kStepBits) - 1));
 }
 
 // Host side of the block records (the kernels fill their LDS copy per thread).
@@ -464,7 +464,7 @@ struct SyncLds {
 
 __host__ __device__ constexpr size_t sync_lds_bytes(uint32_t ntab)
 {
-    return (sizeof(HuffLut) + (1u << kLutBits)) * ntab + sizeof(SyncLds);
+    return (sizeof(HuffLut) + (1u << kStepBits)) * ntab + sizeof(SyncLds);
 }
 
 __global__ __launch_bounds__(kGroupSubs) void ent_sync_kernel(EntBatchDev b)
@@ -472,7 +472,7 @@ __global__ __launch_bounds__(kGroupSubs) void ent_sync_kernel(EntBatchDev b)
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     HuffLut* tabs = reinterpret_cast<HuffLut*>(smem);
     uint8_t* steps = smem + sizeof(HuffLut) * b.ntab_max;
-    SyncLds& L = *reinterpret_cast<SyncLds*>(smem + (sizeof(HuffLut) + (1u << kLutBits)) * b.ntab_max);
+    SyncLds& L = *reinterpret_cast<SyncLds*>(smem + (sizeof(HuffLut) + (1u << kStepBits)) * b.ntab_max);
     const int tid = threadIdx.x;
     const uint32_t w = blockIdx.x;
     const uint32_t f = b.wg_frame[w];
@@ -1100,7 +1100,7 @@ void emulate(const EntBatchDev& b)
         const EntFrame& F = b.frames[b.wg_frame[w]];
         BlockInfo blocks[kMaxBpm];
         fill_blocks(blocks, F);
-        std::vector<uint8_t> steps(static_cast<size_t>(F.ntab) << kLutBits);
+        std::vector<uint8_t> steps(static_cast<size_t>(F.ntab) << kStepBits);
         fill_steps(steps.data(), b.tabs + F.tab_base, F.ntab, 0, 1);
         const RunCtx c = make_ctx(b, F, b.tabs + F.tab_base, blocks, steps.data());
         const uint32_t gl = w - F.wg_base;

@@ -39,6 +39,10 @@ namespace hjd {
 namespace ent {
 
 constexpr int kLutBits = 10;                    // first-level lookup width
+#ifndef HJD_STEP_BITS
+#define HJD_STEP_BITS 11   // same-box: 11 bits best on the stream, 12 on a lone batch (profiles/r02_entropy_step_bits_ab.json)
+#endif
+constexpr int kStepBits = HJD_STEP_BITS;        // sync-mode AC step table width (>= kLutBits, <= 15)
 constexpr int kMaxTables = 6;                   // DC+AC per component at most
 constexpr int kGroupSubs = 256;                 // subsequences per workgroup (one per thread)
 constexpr int kWarm = 8;                        // leading subsequences a group shares with its predecessor
@@ -206,7 +210,7 @@ __host__ __device__ __forceinline__ BlockInfo block_info(uint32_t ji)
     b.m1 = comp == 1;
     b.m2 = comp == 2;
     b.ji = ji;
-    b.sac = ((ji >> 3) & 7) << kLutBits;
+    b.sac = ((ji >> 3) & 7) << kStepBits;
     b.pad = 0;
     return b;
 }
@@ -224,7 +228,7 @@ struct RunCtx {
     uint32_t nseg, data_bits;
     int bpm;
     uint32_t seg_blocks;       // EntFrame::seg_blocks
-    const uint8_t* steps;      // [table][1 << kLutBits] AC step entries (LDS), or null: one unit per step
+    const uint8_t* steps;      // [table][1 << kStepBits] AC step entries (LDS), or null: one unit per step
 };
 
 // AC step entry (sync mode): the AC units that a 10-bit peek decodes
@@ -244,10 +248,10 @@ __host__ __device__ __forceinline__ uint32_t step_zadv(uint32_t e) { return e >>
 __host__ __device__ __forceinline__ uint8_t step_entry(const HuffLut& t, uint32_t p)
 {
     uint32_t o = 0, zadv = 0;
-    while (o < static_cast<uint32_t>(kLutBits)) {
-        const uint32_t e = t.lut[(p << o) & ((1u << kLutBits) - 1)];
+    while (o < static_cast<uint32_t>(kStepBits)) {
+        const uint32_t e = t.lut[((p << o) & ((1u << kStepBits) - 1)) >> (kStepBits - kLutBits)];
         const uint32_t total = e & 31, zk = e >> 9;
-        if (e == 0 || o + total > static_cast<uint32_t>(kLutBits)) break;
+        if (e == 0 || o + total > static_cast<uint32_t>(kStepBits)) break;
         if (zk == 64) {   // EOB: the block ends
             o += total;
             zadv = kStepEnds;
@@ -501,7 +505,7 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
             // them end before `stop`, >= 8 bits before the segment end (no pad
             // check in between), and z stays <= 63 (no index-63 error case).
             if (!kWrite && c.steps && !dc) {
-                const uint32_t se = c.steps[bi.sac + (peek >> (32 - kLutBits))];
+                const uint32_t se = c.steps[bi.sac + (peek >> (32 - kStepBits))];
                 const uint32_t nb = step_bits(se), za = step_zadv(se);
                 const bool ends = za == kStepEnds;
                 // an EOB entry's units before the EOB move z by <= 14: z <= 49 keeps them <= 63
