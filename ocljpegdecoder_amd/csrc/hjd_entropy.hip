@@ -1745,9 +1745,10 @@ extern "C" {
 // Hence 4096 for decoders sized for >= 48 frames per call (the stream's
 // 48-frame batches: profiles/r01_stream_batch_ab.json).  A decoder for one or
 // two images is latency-bound by the serial chain of a subsequence: one FHD
-// q90 JPEG, end to end, takes 1.16 ms at S = 1024 against 1.35 ms at 2048
+// q90 JPEG, end to end, took 1.16 ms at S = 1024 against 1.35 ms at 2048
 // (512: 1.04 ms, but its 4096-bit warm-up overlap fails to link often enough
 // at 256 to fall back; profiles/r02_fhd_jpeg_subbits.json), so 1024 there.
+// With the sync kernel's step tables: 1.05 ms at 1024, 0.96 at 512, 1.21 at 2048.
 // HJD_SUB_BITS overrides it (tuning hook, tools/gpu_subbits_sweep.sh).
 static int default_sub_bits(int max_frames)
 {
