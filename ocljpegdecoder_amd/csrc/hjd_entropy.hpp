@@ -231,7 +231,7 @@ struct RunCtx {
     const uint8_t* steps;      // [table][1 << kStepBits] AC step entries (LDS), or null: one unit per step
 };
 
-// AC step entry (sync mode): the AC units that a 10-bit peek decodes
+// AC step entry (sync mode): the AC units that a kStepBits-bit peek decodes
 // completely, taken in one step, since a sync run needs no AC values --
 // only how far they move pos and z.  One byte: [3:0] bits consumed, [7:4] 15
 // if the last unit is an EOB (the block ends), else how far the units move z
@@ -242,7 +242,7 @@ constexpr uint32_t kStepEnds = 15;
 __host__ __device__ __forceinline__ uint32_t step_bits(uint32_t e) { return e & 15; }
 __host__ __device__ __forceinline__ uint32_t step_zadv(uint32_t e) { return e >> 4; }   // kStepEnds: EOB
 
-// Step entry of an AC table for the kLutBits-bit prefix p: units decoded from
+// Step entry of an AC table for the kStepBits-bit prefix p: units decoded from
 // p alone, in order, until one does not fit, an EOB (taken, last) or z would
 // move by more than 14.  Every unit is one the LUT decodes (codes <= kLutBits bits).
 __host__ __device__ __forceinline__ uint8_t step_entry(const HuffLut& t, uint32_t p)
@@ -502,7 +502,7 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
             const bool dc = z == 0;
             // ---- sync mode: the AC units the peek holds, in one step ----
             // Taken only where single units would give the same state: all of
-            // them end before `stop`, >= 8 bits before the segment end (no pad
+            // them end at or before `stop`, >= 8 bits before the segment end (no pad
             // check in between), and z stays <= 63 (no index-63 error case).
             if (!kWrite && c.steps && !dc) {
                 const uint32_t se = c.steps[bi.sac + (peek >> (32 - kStepBits))];
