@@ -373,16 +373,11 @@ def run_jpeg_single(args, wl, hjd, torch, dist, world, rank, dev):
     def timed(fn, k):
         for _ in range(args.warmup):
             fn()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        t0 = time.perf_counter()
-        for _ in range(k):
-            fn()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        return shard.aggregate({"seconds": time.perf_counter() - t0})["seconds"] / k
+
+        def body():
+            for _ in range(k):
+                fn()
+        return timed_region(dist, world, body, torch.cuda.synchronize)[1] / k
 
     t_gpu = timed(gpu_pageable, args.steps)
     # the output of the last timed step vs the oracle on the host decoder's coefficients
@@ -455,6 +450,10 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
     else:
         ring = None
         outs = [torch.empty(shape, dtype=dtype, device=dev) for _ in range(nf)]
+    # the middle timed step writes a second set of outputs, so that two steps
+    # (the middle and the last) are checked after the timed region
+    mid_step = args.warmup + args.steps // 2
+    outs_mid = outs if d2h else [torch.empty(shape, dtype=dtype, device=dev) for _ in range(nf)]
     if gpu_entropy:
         st = hjd.GpuJpegStream(ctx, per_batch, per_batch * max(len(d) for d in pool) + (1 << 20),
                                per_batch * max_blocks, nslots=nslots, nthreads=nthreads, out_format=ofmt)
@@ -482,36 +481,37 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
         from ocljpegdecoder_amd.jpeg import _buf
         pool_c = [_buf(d) for d in pool]
     G = nf * world
-    mine = shard.shard_round_robin(G, rank, world)        # this rank's positions within every step
 
     def step(k):
-        base = k * G
-        for i, pos in enumerate(mine):
-            st.submit(pool_c[(base + pos) % npool], outs[i])
+        o = outs_mid if k == mid_step else outs
+        for i, fid in enumerate(stream_step_ids(k, nf, rank, world)):
+            st.submit(pool_c[fid % npool], o[i])
         return st.sync()
 
     for k in range(args.warmup):
         step(k)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    before = st.sync()                 # stats are cumulative
-    after = before
-    for k in range(args.warmup, args.warmup + args.steps):
-        after = step(k)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    wall = time.perf_counter() - t0
+    stats = {}
+
+    def body():
+        stats["before"] = st.sync()                 # stats are cumulative
+        stats["after"] = stats["before"]
+        for k in range(args.warmup, args.warmup + args.steps):
+            stats["after"] = step(k)
+            if (k - args.warmup) % 16 == 15:
+                log(f"stream step {k - args.warmup + 1}/{args.steps}")
+
+    wall, wall_max = timed_region(dist, world, body, torch.cuda.synchronize)   # max over ranks
+    before, after = stats["before"], stats["after"]
     host_ns = after[stat_key] - before[stat_key]
     host_scan = after.get("host_scan_bytes", 0) - before.get("host_scan_bytes", 0)
-    wall_max = shard.aggregate({"seconds": wall})["seconds"]   # max over ranks
     px = nf * w * h * args.steps * world
 
-    # ---- correctness of the last step, outside the timed region ----------------
+    # ---- correctness of the middle and the last step, outside the timed region ----
     # expected pixels per pool file: host Huffman coefficients -> oracle (the checker)
-    last = (args.warmup + args.steps - 1) * G
+    last_step = args.warmup + args.steps - 1
+    checks = [(last_step, outs)]
+    if not d2h and mid_step != last_step:
+        checks.insert(0, (mid_step, outs_mid))
     live = range(nf - len(ring), nf) if d2h else range(nf)     # D2H ring: only the last frames survive
     g = torch.Generator(device=dev)
     g.manual_seed(12345)
@@ -520,22 +520,26 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_py as O
     exp_cs = {}
-    for i in live:
-        f = (last + mine[i]) % npool
-        if f not in exp_cs:
-            coefs, info = hjd.decode_coefs(pool[f])
-            e = O.decode_q16(coefs, info.qt, info.width, info.height, info.sampling)
-            if ofmt != hjd.OUT_BGRX:
-                e = np.zeros((h, pitch), np.uint8)
-                e[:, :3 * w] = O.decode_q16(coefs, info.qt, w, h, s).view(np.uint8).reshape(h, w, 4)[..., :3] \
-                    .reshape(h, 3 * w)
-            exp_cs[f] = frame_checksum(torch, torch.from_numpy(np.ascontiguousarray(e)), weights)
-    got = sum(frame_checksum(torch, outs[i], weights) for i in live)
-    exp = sum(exp_cs[(last + mine[i]) % npool] for i in live)
+    got = exp = id_sum = nchecked = 0
+    for k, o in checks:
+        ids = stream_step_ids(k, nf, rank, world)
+        for i in live:
+            f = ids[i] % npool
+            if f not in exp_cs:
+                coefs, info = hjd.decode_coefs(pool[f])
+                e = O.decode_q16(coefs, info.qt, info.width, info.height, info.sampling)
+                if ofmt != hjd.OUT_BGRX:
+                    e = np.zeros((h, pitch), np.uint8)
+                    e[:, :3 * w] = O.decode_q16(coefs, info.qt, w, h, s).view(np.uint8).reshape(h, w, 4)[..., :3] \
+                        .reshape(h, 3 * w)
+                exp_cs[f] = frame_checksum(torch, torch.from_numpy(np.ascontiguousarray(e)), weights)
+            got += frame_checksum(torch, o[i], weights)
+            exp += exp_cs[f]
+            id_sum += ids[i]
+            nchecked += 1
     # sums of < 2^31 values over <= 2^21 frames are exact in float64 (shard.aggregate's dtype)
-    agg = shard.aggregate({"frames_checked": len(live), "checksum": got, "checksum_oracle": exp,
-                           "id_sum": sum(last + mine[i] for i in live)})
-    ok = agg["checksum"] == agg["checksum_oracle"]
+    agg, ok = stream_check_totals(got, exp, id_sum, nchecked)
+    h2d = h2d_ceiling(torch, dev) if gpu_entropy and not d2h else None
     if rank == 0:
         jpeg_bytes = int(np.mean([len(d) for d in pool]))
         res = {
@@ -561,11 +565,19 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
                 "destuff": ("gpu (pinned JPEG pool, raw scans DMA'd)" if pinned_pool else "host (pageable pool)")
                            if gpu_entropy else "n/a (host Huffman)",
                 "host_scan_bytes_per_frame": round(host_scan / (nf * args.steps), 1) if gpu_entropy else None,
+                "h2d_ceiling": None if h2d is None else {
+                    "pinned_h2d_GBps": h2d, "jpeg_GBps_in_per_gpu": round(nf * args.steps * jpeg_bytes / wall_max / 1e9, 2),
+                    "frac": round(nf * args.steps * jpeg_bytes / wall_max / 1e9 / h2d, 3),
+                    "how": "pinned host -> device copy of 256 MiB buffers on this GPU after the timed region "
+                           "(tools/h2d_bw.py); the JPEG bytes are what crosses PCIe"},
                 "output_checked_vs_oracle": bool(ok)},
+            "timed_seconds": round(wall_max, 3),
             "stream_check": {"frames_checked": int(agg["frames_checked"]), "checksum": int(agg["checksum"]),
                              "checksum_oracle": int(agg["checksum_oracle"]), "id_sum": int(agg["id_sum"]),
-                             "how": "last step: per-frame position-weighted checksum of the output, summed over "
-                                    "ranks (shard.aggregate); oracle = host Huffman coefficients -> "
+                             "steps_checked": [k for k, _ in checks],
+                             "how": "middle and last timed steps (separate output buffers): per-frame "
+                                    "position-weighted checksum of the output, summed over ranks "
+                                    "(shard.aggregate); oracle = host Huffman coefficients -> "
                                     "oracle_decode_frame_q16 of the same ids"},
             "roofline": None, "cpu_baseline": None,
         }
@@ -576,6 +588,24 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
     if not ok:
         log("FATAL: stream output differs from the oracle")
         sys.exit(1)
+
+
+def h2d_ceiling(torch, dev, mb=256, reps=8):
+    """Pinned host -> device copy rate on this GPU (GB/s), the PCIe ceiling of
+    the JPEG stream (the same measurement as tools/h2d_bw.py)."""
+    n = mb << 20
+    hbuf = torch.empty(n, dtype=torch.uint8).pin_memory()
+    dbuf = torch.empty(n, dtype=torch.uint8, device=dev)
+    s = torch.cuda.Stream(dev)
+    with torch.cuda.stream(s):
+        dbuf.copy_(hbuf, non_blocking=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with torch.cuda.stream(s):
+        for _ in range(reps):
+            dbuf.copy_(hbuf, non_blocking=True)
+    torch.cuda.synchronize()
+    return round(n * reps / (time.perf_counter() - t0) / 1e9, 2)
 
 
 def numa_nodes():
@@ -649,6 +679,194 @@ def run_host_prep(args):
                       "rows": rows}), flush=True)
 
 
+def timed_region(dist, world, body, sync):
+    """The contract's timed region on every code path: barrier + device
+    synchronize, body(), synchronize + barrier.  Returns (this rank's wall
+    seconds, the max over ranks via shard.aggregate's MAX all-reduce).  With N
+    ranks over RCCL this is the only cross-GPU traffic: two barriers and the
+    two all-reduces of shard.aggregate."""
+    from ocljpegdecoder_amd import shard
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    body()
+    sync()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    return wall, shard.aggregate({"seconds": wall})["seconds"]
+
+
+def stream_step_ids(k, frames_per_gpu, rank, world):
+    """Global frame ids rank `rank` decodes in stream step k: step k covers ids
+    [k*G, (k+1)*G), G = frames_per_gpu * world, dealt round-robin over ranks."""
+    from ocljpegdecoder_amd import shard
+    G = frames_per_gpu * world
+    return [k * G + p for p in shard.shard_round_robin(G, rank, world)]
+
+
+def stream_check_totals(got, exp, id_sum, nchecked):
+    """Sums of the per-rank stream checks over ranks (shard.aggregate: SUM);
+    ok when the output checksums equal the oracle's."""
+    from ocljpegdecoder_amd import shard
+    agg = shard.aggregate({"frames_checked": nchecked, "checksum": got, "checksum_oracle": exp, "id_sum": id_sum})
+    return agg, agg["checksum"] == agg["checksum_oracle"]
+
+
+_TORCHRUN_VARS = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE", "ROLE_RANK",
+                  "ROLE_NAME", "ROLE_WORLD_SIZE", "MASTER_PORT", "TORCHELASTIC_RUN_ID", "TORCHELASTIC_RESTART_COUNT",
+                  "TORCHELASTIC_MAX_RESTARTS", "TORCHELASTIC_USE_AGENT_STORE", "TORCHELASTIC_ERROR_FILE",
+                  "TORCHELASTIC_ENABLED")
+
+
+def stream_leg_command(world, dist_backend, frame_ids, per_gpu, port, environ):
+    """The config-5 child run rank 0 starts: (argv, env, steps).  N=1: plain
+    python; N>1: torch.distributed.run over the same N GPUs on `port` at
+    127.0.0.1.  Enough steps of per_gpu frames per GPU to cover frame_ids
+    global ids (>= 3).  The env drops this rank's torchrun variables, so the
+    child agent sets its own."""
+    steps = max(3, -(-frame_ids // (per_gpu * world)))
+    args = [os.path.abspath(__file__), "--gpus", str(world), "--workload", "stream4k420", "--steps", str(steps),
+            "--warmup", "1", "--no-cpu", "--dist-backend", dist_backend, "--frames", str(per_gpu)]
+    if world == 1:
+        cmd = [sys.executable] + args
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+               "--master-addr", "127.0.0.1", "--master-port", str(port)] + args
+    env = {k: v for k, v in environ.items() if k not in _TORCHRUN_VARS}
+    return cmd, env, steps
+
+
+def roofline_obj(achieved, bytes_per_launch, kernel_ms, traffic, trace):
+    """The line's roofline object: achieved = algorithmic bytes per launch / the
+    mean launch time measured with HIP events on the launch stream in this run;
+    traffic (PMC HBM bytes per launch) and the kernel-trace dispatch split come
+    from the committed profiles of the same command (profiles/)."""
+    r = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+         "frac": round(achieved / HBM_PEAK_GBPS, 4),
+         "traffic": traffic[0] if traffic else None,
+         "traffic_source": traffic[1] if traffic else None,
+         "algorithmic_bytes_per_launch": bytes_per_launch,
+         "kernel_ms_per_launch": round(kernel_ms, 4)}
+    if trace:
+        d, path = trace
+        r["kernel_trace_source"] = path
+        r["timed_dispatch_mean_ms"] = d["timed_mean_ms"]
+        r["frac_from_trace"] = round(bytes_per_launch / (d["timed_mean_ms"] / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)
+    return r
+
+
+def committed_dispatch_trace(workload, frames):
+    """The committed rocprofv3 kernel trace of the bench command, split into
+    warmup and timed dispatches (tools/ktrace_dispatch.py writes
+    profiles/*dispatch*.json); the latest file that covers this workload at this
+    launch size, or None."""
+    best = None
+    for p in sorted(glob.glob(os.path.join(REPO, "profiles", "*dispatch*.json"))):
+        try:
+            d = json.load(open(p))
+        except Exception:
+            continue
+        e = d.get("workloads", {}).get(workload) if isinstance(d, dict) else None
+        if e and e.get("frames_per_launch") == frames and e.get("timed_mean_ms"):
+            best = (e, os.path.relpath(p, REPO))
+    return best
+
+
+def pixel_batch(args, wl, hjd, torch, dist, world, rank, dev, qt, steps, warmup):
+    """One pixel workload on this rank: inputs resident in HBM, W untimed + K
+    timed launches of one plan over the whole batch (barrier + synchronize on
+    both sides, max over ranks), then every frame of the last launch checked
+    against the oracle.  Frees its device buffers before returning."""
+    from ocljpegdecoder_amd import shard
+    w, h, s, nf = wl["width"], wl["height"], wl["sampling"], wl["frames"]
+    mw, mh, bpm, _ = hjd.mcu_geometry(w, h, s)
+    nblk = mw * mh * bpm
+    npool = min(POOL, nf)
+    i32 = wl.get("input") == "i32"
+    pool16 = torch.empty((npool, nblk, 64), dtype=torch.int16, device=dev)
+    for i in range(npool):
+        pool16[i] = synth_frame_gpu(torch, nblk, s, qt, seed=1000 * rank + i, device=dev)
+    if i32:
+        # the idct.h format: dequantised (src/decoder.cpp:338-342) int32 in natural order
+        inv = [0] * 64
+        for k, n in enumerate(ZIGZAG_NAT):
+            inv[n] = k
+        comp = torch.from_numpy(hjd.block_components(s, nblk)).to(dev)
+        qz = torch.from_numpy(np.asarray(qt, dtype=np.int32)).to(dev)[comp]          # [nblk, 64] file order
+        src = (pool16.to(torch.int32) * qz)[:, :, torch.tensor(inv, device=dev)]     # natural order
+        coefs = torch.empty((nf, nblk, 64), dtype=torch.int32, device=dev)
+        for i in range(npool):
+            coefs[i] = src[i]
+        del src
+    else:
+        coefs = torch.empty((nf, nblk, 64), dtype=torch.int16, device=dev)
+        for i in range(npool):
+            coefs[i] = pool16[i]
+    for i in range(npool, nf):
+        coefs[i].copy_(coefs[i % npool])
+    ofmt = wl.get("out_format", hjd.OUT_BGRX)
+    pitch = hjd.default_pitch(w, ofmt)
+    out = torch.empty((nf, h, pitch), dtype=torch.uint8, device=dev)
+    specs = [hjd.FrameSpec(w, h, s, coef_offset=i * nblk, out_offset=i * h * pitch, out_pitch=pitch,
+                           qt_index=(0, 1, 2), out_format=ofmt) for i in range(nf)]
+    ctx = hjd.Context(dev.index)
+    plan = hjd.Plan(ctx, specs, hjd.IN_I32_NATURAL if i32 else hjd.IN_Q16_ZIGZAG, qtables=None if i32 else qt)
+    torch.cuda.synchronize()
+
+    stream = torch.cuda.current_stream()
+    for _ in range(warmup):
+        plan.launch(coefs, out, stream, grid_blocks=args.grid)
+    torch.cuda.synchronize()
+
+    # ---- timed region: exactly K launches ----------------------------------------
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+
+    def body():
+        ev0.record(stream)
+        for _ in range(steps):
+            plan.launch(coefs, out, stream, grid_blocks=args.grid)
+        ev1.record(stream)
+
+    wall, wall_max = timed_region(dist, world, body, torch.cuda.synchronize)   # max over ranks
+    kernel_ms = ev0.elapsed_time(ev1) / steps   # HIP events on the launch stream
+
+    px_per_launch = plan.pixels
+    bytes_per_launch = plan.coef_bytes + hjd.OUT_BYTES[ofmt] * plan.pixels
+    total_px = px_per_launch * steps * world
+    value = total_px / wall_max / 1e6
+    achieved = bytes_per_launch / (kernel_ms / 1e3) / 1e9
+
+    # device-to-device copy bandwidth for context (same-size read+write)
+    copy_gbps = None
+    try:
+        a = torch.empty(1 << 30, dtype=torch.uint8, device=dev)
+        b = torch.empty_like(a)
+        b.copy_(a); torch.cuda.synchronize()
+        c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        c0.record(stream)
+        for _ in range(5):
+            b.copy_(a)
+        c1.record(stream); torch.cuda.synchronize()
+        copy_gbps = round(2 * 5 * a.numel() / (c0.elapsed_time(c1) / 1e3) / 1e9, 1)
+        del a, b
+    except Exception:
+        pass
+
+    # every frame of the timed launch's output vs the oracle (outside the timed region)
+    pool_host = pool16.cpu().numpy()
+    checked = check_batch_vs_oracle(torch, out, pool_host, qt, wl, ofmt)
+    tasks = plan.tasks
+    plan.close()
+    del coefs, out, pool16, plan
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return {"value": round(value, 1), "output_check": checked, "device_copy_GBps": copy_gbps,
+            "_pool_host": pool_host, "_wall_max": wall_max, "_kernel_ms": kernel_ms, "_achieved": achieved,
+            "_bytes_per_launch": bytes_per_launch, "_tasks": tasks}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -658,6 +876,10 @@ def main():
     ap.add_argument("--frames", type=int, default=0, help="override batch size")
     ap.add_argument("--grid", type=int, default=0, help="persistent grid (workgroups), 0 = default")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-444", action="store_true",
+                    help="4k420: skip the configs[3] 4:4:4 batch reported under config4_444")
+    ap.add_argument("--stream-frame-ids", type=int, default=100000,
+                    help="config-5 stream leg: global frame ids to cover (BASELINE configs[4]: 100k images)")
     ap.add_argument("--no-stream", action="store_true",
                     help="N=1 pixel workloads: skip the config-5 stream leg (a child bench.py run, reported "
                          "under config5_stream)")
@@ -698,8 +920,6 @@ def main():
     if args.frames:
         wl["frames"] = args.frames
     w, h, s, nf = wl["width"], wl["height"], wl["sampling"], wl["frames"]
-    mw, mh, bpm, _ = hjd.mcu_geometry(w, h, s)
-    nblk = mw * mh * bpm
     qt = std_qtables(1.0)
 
     if args.workload.startswith("stream"):
@@ -707,87 +927,37 @@ def main():
     if wl.get("jpeg"):
         return run_jpeg_single(args, wl, hjd, torch, dist, world, rank, dev)
 
-    # ---- inputs resident in HBM --------------------------------------------------
-    npool = min(POOL, nf)
+    res_px = pixel_batch(args, wl, hjd, torch, dist, world, rank, dev, qt, args.steps, args.warmup)
+    checked = res_px["output_check"]
+    value = res_px["value"]
+    pool_host = res_px.pop("_pool_host")
+    npool = pool_host.shape[0]
     i32 = wl.get("input") == "i32"
-    pool16 = torch.empty((npool, nblk, 64), dtype=torch.int16, device=dev)
-    for i in range(npool):
-        pool16[i] = synth_frame_gpu(torch, nblk, s, qt, seed=1000 * rank + i, device=dev)
-    if i32:
-        # the idct.h format: dequantised (src/decoder.cpp:338-342) int32 in natural order
-        inv = [0] * 64
-        for k, n in enumerate(ZIGZAG_NAT):
-            inv[n] = k
-        comp = torch.from_numpy(hjd.block_components(s, nblk)).to(dev)
-        qz = torch.from_numpy(np.asarray(qt, dtype=np.int32)).to(dev)[comp]          # [nblk, 64] file order
-        src = (pool16.to(torch.int32) * qz)[:, :, torch.tensor(inv, device=dev)]     # natural order
-        coefs = torch.empty((nf, nblk, 64), dtype=torch.int32, device=dev)
-        for i in range(npool):
-            coefs[i] = src[i]
-        del src
-    else:
-        coefs = torch.empty((nf, nblk, 64), dtype=torch.int16, device=dev)
-        for i in range(npool):
-            coefs[i] = pool16[i]
-    for i in range(npool, nf):
-        coefs[i].copy_(coefs[i % npool])
     ofmt = wl.get("out_format", hjd.OUT_BGRX)
-    pitch = hjd.default_pitch(w, ofmt)
-    out = torch.empty((nf, h, pitch), dtype=torch.uint8, device=dev)
-    specs = [hjd.FrameSpec(w, h, s, coef_offset=i * nblk, out_offset=i * h * pitch, out_pitch=pitch,
-                           qt_index=(0, 1, 2), out_format=ofmt) for i in range(nf)]
-    ctx = hjd.Context(dev.index)
-    plan = hjd.Plan(ctx, specs, hjd.IN_I32_NATURAL if i32 else hjd.IN_Q16_ZIGZAG, qtables=None if i32 else qt)
-    torch.cuda.synchronize()
+    wall_max, kernel_ms, achieved = res_px["_wall_max"], res_px["_kernel_ms"], res_px["_achieved"]
+    bytes_per_launch, tasks = res_px["_bytes_per_launch"], res_px["_tasks"]
 
-    stream = torch.cuda.current_stream()
-    for _ in range(args.warmup):
-        plan.launch(coefs, out, stream, grid_blocks=args.grid)
-    torch.cuda.synchronize()
-
-    # ---- timed region: exactly K launches ----------------------------------------
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
-        plan.launch(coefs, out, stream, grid_blocks=args.grid)
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    wall = time.perf_counter() - t0
-    kernel_ms = ev0.elapsed_time(ev1) / args.steps   # HIP events on the launch stream
-
-    wall_max = shard.aggregate({"seconds": wall})["seconds"]   # max over ranks
-
-    px_per_launch = plan.pixels
-    bytes_per_launch = plan.coef_bytes + hjd.OUT_BYTES[ofmt] * plan.pixels
-    total_px = px_per_launch * args.steps * world
-    value = total_px / wall_max / 1e6
-    achieved = bytes_per_launch / (kernel_ms / 1e3) / 1e9
-
-    # device-to-device copy bandwidth for context (same-size read+write)
-    copy_gbps = None
-    try:
-        a = torch.empty(1 << 30, dtype=torch.uint8, device=dev)
-        b = torch.empty_like(a)
-        b.copy_(a); torch.cuda.synchronize()
-        c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        c0.record(stream)
-        for _ in range(5):
-            b.copy_(a)
-        c1.record(stream); torch.cuda.synchronize()
-        copy_gbps = round(2 * 5 * a.numel() / (c0.elapsed_time(c1) / 1e3) / 1e9, 1)
-        del a, b
-    except Exception:
-        pass
-
-    # every frame of the timed launch's output vs the oracle (outside the timed region)
-    pool_host = pool16.cpu().numpy()
-    checked = check_batch_vs_oracle(torch, out, pool_host, qt, wl, ofmt)
+    # configs[3] (1024 x 4K 4:4:4) in the same default run, after configs[2]
+    config4 = None
+    if args.workload == "4k420" and not args.no_444:
+        wl4 = dict(WORKLOADS["4k444"])
+        if args.frames:
+            wl4["frames"] = args.frames
+        r4 = pixel_batch(args, wl4, hjd, torch, dist, world, rank, dev, qt, args.steps, args.warmup)
+        r4.pop("_pool_host")
+        traffic4 = committed_traffic("4k444", wl4["frames"])
+        trace4 = committed_dispatch_trace("4k444", wl4["frames"])
+        config4 = {
+            "metric": "Mpixels/s decoded (dequant+IDCT+colour)", "value": r4["value"], "unit": "Mpixels/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(r4["_wall_max"] / args.steps * 1e3, 4),
+            "workload": wl4["desc"], "frames_per_gpu": wl4["frames"], "sampling": "4:4:4",
+            "output_checked_vs_oracle": r4["output_check"]["ok"], "output_check": r4["output_check"],
+            "roofline": roofline_obj(r4["_achieved"], r4["_bytes_per_launch"], r4["_kernel_ms"], traffic4, trace4),
+            "reference_path": "src/idct8x8.cl:168-192 (batch_idct_csc_444), src/decoder.cpp:457-471"}
+        checked_all_ok = checked["ok"] and r4["output_check"]["ok"]
+    else:
+        checked_all_ok = checked["ok"]
 
     if rank == 0:
         cpu = None
@@ -796,13 +966,13 @@ def main():
             cpu = cpu_baseline(pool_host, qt, wl, value)
         stream5 = None
         if not args.no_stream and args.workload == "4k420":
-            del coefs, out
             torch.cuda.synchronize()
             torch.cuda.empty_cache()
             if world > 1:
                 dist.destroy_process_group()   # the other ranks are leaving; the child run has its own group
-            stream5 = config5_stream_leg(world, args.dist_backend)
+            stream5 = config5_stream_leg(world, args.dist_backend, args.stream_frame_ids)
         traffic = committed_traffic(args.workload, nf)
+        trace = committed_dispatch_trace(args.workload, nf)
         res = {
             "metric": "Mpixels/s decoded (dequant+IDCT+colour) at 1/2/4/8 GPUs; % HBM roofline",
             "value": round(value, 1),
@@ -823,17 +993,13 @@ def main():
                                 else "int16 quantised zigzag + qtables",
                        "output": "BGRX 4 B/px in HBM" if ofmt == hjd.OUT_BGRX else "BGR24 3 B/px in HBM",
                        "parallelism": f"image-parallel x{world} (no collective)",
-                       "tasks_per_launch": plan.tasks},
+                       "tasks_per_launch": tasks},
             "output_checked_vs_oracle": checked["ok"],
             "output_check": checked,
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                         "traffic": traffic[0] if traffic else None,
-                         "traffic_source": traffic[1] if traffic else None,
-                         "algorithmic_bytes_per_launch": bytes_per_launch,
-                         "kernel_ms_per_launch": round(kernel_ms, 4)},
+            "roofline": roofline_obj(achieved, bytes_per_launch, kernel_ms, traffic, trace),
             "cpu_baseline": cpu,
-            "device_copy_GBps": copy_gbps,
+            "device_copy_GBps": res_px["device_copy_GBps"],
+            "config4_444": config4,
             "config5_stream": stream5,
         }
         if cpu and "reference" in cpu:
@@ -841,8 +1007,8 @@ def main():
         print(json.dumps(res), flush=True)
     if world > 1 and dist.is_initialized():
         dist.destroy_process_group()
-    if not checked["ok"]:
-        log("FATAL: the timed launch's output differs from the oracle:", checked)
+    if not checked_all_ok:
+        log("FATAL: a timed launch's output differs from the oracle")
         sys.exit(1)
 
 
@@ -869,7 +1035,7 @@ def _wait_sibling_ranks_exit(timeout_s=60.0):
         time.sleep(0.5)
 
 
-def config5_stream_leg(world, dist_backend):
+def config5_stream_leg(world, dist_backend, frame_ids=100000):
     """BASELINE configs[4] on the same GPUs, measured in the same default run:
     rank 0 starts a child `bench.py --workload stream4k420` (N=1: plain python;
     N>1: torch.distributed.run over the same N GPUs on a fresh port, the frame
@@ -881,44 +1047,40 @@ def config5_stream_leg(world, dist_backend):
     import signal
     import socket
     import subprocess
-    args = [os.path.abspath(__file__), "--gpus", str(world), "--workload", "stream4k420", "--steps", "3",
-            "--warmup", "1", "--no-cpu", "--dist-backend", dist_backend]
-    if os.environ.get("HJD_BENCH_STREAM_FRAMES"):   # tests: smaller steps
-        args += ["--frames", os.environ["HJD_BENCH_STREAM_FRAMES"]]
-    if world == 1:
-        cmd = [sys.executable] + args
-    else:
+    # BASELINE configs[4] is a 100k-image stream: enough steps of 1024 frames per
+    # GPU (G = 1024 * world ids per step) to cover `frame_ids` global ids
+    per_gpu = int(os.environ.get("HJD_BENCH_STREAM_FRAMES", WORKLOADS["stream4k420"]["frames"]))  # tests: smaller
+    port = 0
+    if world > 1:
         sk = socket.socket()
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
         sk.close()
-        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
-               "--master-addr", "127.0.0.1", "--master-port", str(port)] + args
-    drop = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE", "ROLE_RANK",
-            "ROLE_NAME", "ROLE_WORLD_SIZE", "MASTER_PORT", "TORCHELASTIC_RUN_ID", "TORCHELASTIC_RESTART_COUNT",
-            "TORCHELASTIC_MAX_RESTARTS", "TORCHELASTIC_USE_AGENT_STORE", "TORCHELASTIC_ERROR_FILE",
-            "TORCHELASTIC_ENABLED")
-    env = {k: v for k, v in os.environ.items() if k not in drop}
+    cmd, env, _ = stream_leg_command(world, dist_backend, frame_ids, per_gpu, port, os.environ)
     if world > 1:
         _wait_sibling_ranks_exit()
     log("running config-5 stream leg:", " ".join(cmd[1:]))
     p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env,
                          start_new_session=True)
     try:
-        out, err = p.communicate(timeout=600)
+        out, err = p.communicate(timeout=900)
     except subprocess.TimeoutExpired:
         os.killpg(p.pid, signal.SIGKILL)   # the child's own process group (its torchrun workers included)
         p.communicate()
-        return {"error": "timeout after 600 s"}
+        return {"error": "timeout after 900 s"}
     line = next((l for l in reversed(out.splitlines()) if l.startswith("{")), None)
     if p.returncode != 0 or line is None:
         return {"error": f"rc {p.returncode}", "stderr_tail": err[-400:]}
     d = json.loads(line)
     return {"value": d["value"], "unit": d["unit"], "n_gpus": d["n_gpus"], "ms_per_step": d["ms_per_step"],
             "steps": d["steps"], "frames_per_gpu_per_step": d["config"]["frames_per_gpu_per_step"],
+            "timed_frame_ids": d["config"]["timed_frame_ids"], "timed_seconds": d["timed_seconds"],
             "workload": d["config"]["workload"], "sharding": d["config"]["sharding"],
+            "value_per_gpu": round(d["value"] / d["n_gpus"], 1),
             "jpeg_GBps_in": d["end_to_end"]["jpeg_GBps_in"], "destuff": d["end_to_end"]["destuff"],
+            "h2d_ceiling": d["end_to_end"].get("h2d_ceiling"),
             "output_checked_vs_oracle": d["end_to_end"]["output_checked_vs_oracle"],
+            "steps_checked": d["stream_check"]["steps_checked"],
             "command": " ".join(["python"] + [os.path.basename(c) if c.endswith("bench.py") else c
                                               for c in cmd[1:]])}
 

@@ -95,8 +95,13 @@ int hjd_stream_set_output_format(hjd_stream* s, int out_format);
  * (DESIGN.md s10).  The fused pixel kernel follows on the same stream. */
 typedef struct hjd_gdec hjd_gdec;
 
-/* Capacity: max_frames JPEGs per call whose entropy-coded bytes total at most
- * max_scan_bytes and whose coefficient blocks total at most max_blocks.
+/* Capacity: max_frames JPEGs per call whose coefficient blocks total at most
+ * max_blocks.  max_scan_bytes = the total size of the files of a call (the
+ * sum of sizes[]) is always enough, wherever the files lie in memory.  The
+ * sum of their entropy-coded bytes is enough too: pinned files then take the
+ * host destuff path where their raw scans (stuffing, restart markers and the
+ * bytes after EOI included) would not fit, unless HJD_DESTUFF=device, which
+ * reports the overflow.
  * sub_bits = bits per parallel subsequence (0 = default 1024; >= 32). */
 int hjd_gdec_create(hjd_ctx* ctx, int max_frames, int64_t max_scan_bytes, int64_t max_blocks, int sub_bits,
                     hjd_gdec** out);
@@ -104,7 +109,9 @@ int hjd_gdec_destroy(hjd_gdec* g);
 
 /* Decode n JPEGs to BGRX in device memory (d_outs[i], row pitch pitches[i];
  * 16-byte aligned).  Asynchronous on `stream` (hipStream_t, NULL = default);
- * the input bytes may be reused as soon as the call returns.  A later call on
+ * the input bytes may be reused as soon as the call returns (for pinned input,
+ * which the DMA reads in place, the call returns once those uploads have
+ * landed; the kernels stay asynchronous).  A later call on
  * the same object waits (on the host) for this call's uploads and is ordered
  * (on the device) after its kernels, whatever stream it uses; hjd_gdec_sync
  * reports the statuses of the most recent call. */
@@ -125,6 +132,9 @@ int hjd_gdec_sync(hjd_gdec* g, int32_t* status);
  * or HJD_OUT_BGR24 (include/hjd.h; 3-byte pixels, d_outs 4-byte aligned,
  * pitches >= 3*width, multiple of 4). */
 int hjd_gdec_set_output_format(hjd_gdec* g, int out_format);
+/* Bytes of the most recent decode call: scan bytes the host CPU read + wrote
+ * (0 when every scan was destuffed on the GPU) and bytes moved host -> device. */
+int hjd_gdec_last_bytes(hjd_gdec* g, int64_t* host_scan_bytes, int64_t* h2d_bytes);
 
 #define HJD_GDEC_SEQUENTIAL 1   /* verification fell back to the sequential path */
 #define HJD_GDEC_CORRUPT 2      /* invalid Huffman data on the decoded chain */

@@ -139,6 +139,7 @@ def _bind_host(lib):
                                                  ctypes.c_int, vp, ctypes.POINTER(ctypes.c_int64), vp]),
         "hjd_gdec_sync": (ctypes.c_int, [vp, c_i32p]),
         "hjd_gdec_set_output_format": (ctypes.c_int, [vp, ctypes.c_int]),
+        "hjd_gdec_last_bytes": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
         "hjd_gstream_create": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
                                               ctypes.c_int, ctypes.POINTER(vp)]),
         "hjd_gstream_destroy": (ctypes.c_int, [vp]),

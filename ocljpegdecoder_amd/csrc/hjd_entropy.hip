@@ -264,22 +264,43 @@ __host__ __device__ __forceinline__ uint32_t raw_region_len(uint32_t begin, uint
 // the previous one in the caller's memory within kMirrorGap bytes (a JPEG
 // header, typically) is placed at the same distance, so the run moves with one
 // DMA; anything else goes after the area in use, at the source's alignment mod 16.
+//
+// Capacity contract: a batch whose files total F bytes fits a raw area of
+// F + kSlack bytes per frame, whatever lies between the files.  Mirroring
+// consumes the gap between two scans (the next file's header, plus whatever
+// the caller left between the files), so it is taken only while the area in
+// use stays within the bytes of the files placed so far plus kSlack each
+// (`allow`); otherwise, or when the mirrored offset would not fit, the scan
+// is placed compactly (<= 30 bytes of alignment) and starts a new DMA run.
+// By induction the area in use never exceeds F + 48 bytes per frame, and the
+// 32-byte read-ahead fits in the kDataPad + 16 bytes data_cap() adds per frame.
 struct RawCursor {
     static constexpr uint64_t kMirrorGap = 64 * 1024;
+    static constexpr uint64_t kSlack = 48;
+    static constexpr uint64_t kReadAhead = 32;   // destuff kernels' 16-B loads straddling the end
     const uint8_t* last_src = nullptr;
     uint64_t last_off = 0;
     uint64_t end = 0;
-    bool place(const uint8_t* src, size_t n, bool mirror, size_t cap, uint64_t& off)
+    uint64_t allow = 0;      // sum of (file bytes + kSlack) over the frames placed
+    // n = scan bytes at src; file = bytes of the whole file; reserve = area
+    // that must stay free after this scan (for frames still to come).
+    bool place(const uint8_t* src, size_t n, size_t file, bool mirror, size_t cap, uint64_t& off,
+               uint64_t reserve = 0)
     {
-        uint64_t o;
+        const uint64_t allow_next = allow + file + kSlack;
+        uint64_t o = ~0ull;
         if (mirror && last_src && src > last_src && last_off + static_cast<uint64_t>(src - last_src) >= end &&
-            last_off + static_cast<uint64_t>(src - last_src) - end <= kMirrorGap)
+            last_off + static_cast<uint64_t>(src - last_src) - end <= kMirrorGap) {
             o = last_off + static_cast<uint64_t>(src - last_src);
-        else
+            if (o + n > allow_next || o + n + kReadAhead + reserve > cap) o = ~0ull;
+        }
+        if (o == ~0ull) {
             o = (end + 15) / 16 * 16 + (reinterpret_cast<uintptr_t>(src) & 15);
-        if (o + n + 32 > cap) return false;   // + the kernels' read-ahead inside the area
+            if (o + n + kReadAhead + reserve > cap) return false;
+        }
         off = o;
         end = o + n;
+        allow = allow_next;
         last_src = mirror ? src : nullptr;
         last_off = o;
         return true;
@@ -810,20 +831,24 @@ __device__ __forceinline__ uint32_t byte_at(const Lane16& v, uint32_t k)
 
 // Classify the 16 region bytes at s (16-B aligned): bytes before `begin` (not
 // the scan's) and at or past `lim` (the region's length, or the known scan
-// end) are dropped.
+// end) are dropped.  Nothing at or past `lim` is loaded: a lane whose 16 bytes
+// start there (most of a frame's last tile) issues no load, and a lane that
+// straddles it reads at most 15 bytes past the region, inside the 32-byte
+// read-ahead every raw placement reserves (RawCursor::place).
 __device__ __forceinline__ Lane16 classify16(const uint8_t* r, uint32_t s, uint32_t begin, uint32_t len, uint32_t lim)
 {
     Lane16 v;
-    const u32x4 q = *reinterpret_cast<const u32x4*>(r + s);
-    v.lo = static_cast<uint64_t>(q.x) | (static_cast<uint64_t>(q.y) << 32);
-    v.hi = static_cast<uint64_t>(q.z) | (static_cast<uint64_t>(q.w) << 32);
     v.marks = 0;
     v.end = kNoEnd;
-    uint32_t drop = 0;
     if (s >= lim) {
+        v.lo = v.hi = 0;
         v.drop = 0xFFFFu;
         return v;
     }
+    const u32x4 q = *reinterpret_cast<const u32x4*>(r + s);
+    v.lo = static_cast<uint64_t>(q.x) | (static_cast<uint64_t>(q.y) << 32);
+    v.hi = static_cast<uint64_t>(q.z) | (static_cast<uint64_t>(q.w) << 32);
+    uint32_t drop = 0;
     if (lim - s < 16) drop = 0xFFFFu & ~((1u << (lim - s)) - 1u);
     uint32_t ff = ff_mask4(q.x) | (ff_mask4(q.y) << 4) | (ff_mask4(q.z) << 8) | (ff_mask4(q.w) << 12);
     if (s < begin) {                                // only in a frame's first 16 bytes (begin < 16)
@@ -1275,8 +1300,13 @@ struct hjd_gdec {
     // (thread-safe for distinct i and disjoint data ranges).
     int prepare_frame(int i, const uint8_t* data, size_t size, size_t data_off, size_t cap, int mode,
                       uint64_t raw_off);
-    // destuff mode of a JPEG and, for the device modes, its place in the raw area
-    int plan_raw(const uint8_t* data, size_t size, RawCursor& cur, int& mode, uint64_t& raw_off, bool& fits);
+    // Destuff mode of a JPEG and, for the device modes, its place in the raw
+    // area.  fits = false when the raw scan does not fit the raw area, or
+    // data_room (free bytes of the data area) minus `reserve` (bytes kept for
+    // the frames still to come); with host_fallback, HJD_DESTUFF=auto then
+    // picks the host path instead (fits stays true).
+    int plan_raw(const uint8_t* data, size_t size, RawCursor& cur, int& mode, uint64_t& raw_off, bool& fits,
+                 size_t data_room, uint64_t reserve, bool host_fallback);
     // Lays out and fills the header for the staged frames (pixel records too
     // when d_outs is given); returns the device view (pointers into `blob`).
     int assemble(uint8_t* blob, int16_t* coefs, int64_t* block_offsets, void* const* d_outs, const int32_t* pitches,
@@ -1331,7 +1361,8 @@ bool pinned_host(const void* p, size_t n)
 
 }  // namespace
 
-int hjd_gdec::plan_raw(const uint8_t* data, size_t size, RawCursor& cur, int& mode, uint64_t& raw_off, bool& fits)
+int hjd_gdec::plan_raw(const uint8_t* data, size_t size, RawCursor& cur, int& mode, uint64_t& raw_off, bool& fits,
+                       size_t data_room, uint64_t reserve, bool host_fallback)
 {
     mode = kDestuffHost;
     raw_off = 0;
@@ -1346,7 +1377,17 @@ int hjd_gdec::plan_raw(const uint8_t* data, size_t size, RawCursor& cur, int& mo
     const int rc = hjd_internal::parse_scan_header(data, size, &h);
     if (rc) return rc;
     if (h.scan_offset >= size) return set_error(HJD_E_INVALID, "empty scan");
-    fits = cur.place(data + h.scan_offset, size - h.scan_offset, mode == kDestuffFromCaller, data_cap(), raw_off);
+    const size_t raw = size - h.scan_offset;
+    // the device path needs the raw scan (stuffing, markers and the bytes
+    // after EOI included) in both the raw and the data area; the host path
+    // only the destuffed bytes in the data area
+    fits = align_up(raw + kDataPad, 16) + reserve <= data_room &&
+           cur.place(data + h.scan_offset, raw, size, mode == kDestuffFromCaller, data_cap(), raw_off, reserve);
+    if (!fits && host_fallback && pol == 1) {   // auto: destuff this one on the host instead
+        mode = kDestuffHost;
+        raw_off = 0;
+        fits = true;
+    }
     return HJD_OK;
 }
 
@@ -1371,12 +1412,17 @@ int hjd_gdec::stage_frames(const uint8_t* const* datas, const size_t* sizes, int
     data_used = 0;
     int64_t blocks = 0;
     RawCursor cur;
+    // what the frames after i may need in either area, whichever path they
+    // take: a frame with a device-destuffed scan is placed only if the rest
+    // still fit, so a batch sized by its file bytes never fails on placement
+    std::vector<uint64_t> tail(static_cast<size_t>(n) + 1, 0);
+    for (int i = n - 1; i >= 0; --i) tail[i] = tail[i + 1] + align_up(sizes[i] + kDataPad, 16);
     for (int i = 0; i < n; ++i) {
         if (data_used >= data_cap()) return set_error(HJD_E_INVALID, "scan bytes exceed the batch capacity");
         int mode;
         uint64_t raw_off;
         bool fits;
-        int rc = plan_raw(datas[i], sizes[i], cur, mode, raw_off, fits);
+        int rc = plan_raw(datas[i], sizes[i], cur, mode, raw_off, fits, data_cap() - data_used, tail[i + 1], true);
         if (rc) return set_error(rc, "frame %d: %s", i, hjd_last_error());
         if (!fits) return set_error(HJD_E_INVALID, "scan bytes exceed the batch capacity");
         rc = prepare_frame(i, datas[i], sizes[i], data_used, data_cap() - data_used, mode, raw_off);
@@ -1729,7 +1775,17 @@ int gdec_run(hjd_gdec* g, const uint8_t* const* datas, const size_t* sizes, int 
     if (rc) return rc;
     rc = g->stage_frames(datas, sizes, n);
     if (rc) return rc;
-    return gdec_issue(g, d_outs, pitches, coefs_out, block_offsets, s);
+    rc = gdec_issue(g, d_outs, pitches, coefs_out, block_offsets, s);
+    if (rc) return rc;
+    // The caller may reuse its bytes once this returns (include/hjd_host.h):
+    // scans read by DMA straight from the caller's pinned memory must have
+    // landed first.  Only the uploads are waited for, not the kernels.
+    for (const Prepared& p : g->frames)
+        if (p.destuff == kDestuffFromCaller) {
+            HJD_HIP(hipEventSynchronize(g->staged));
+            break;
+        }
+    return HJD_OK;
 }
 
 }  // namespace
@@ -1831,6 +1887,14 @@ int hjd_gdec_decode_coefs(hjd_gdec* g, const uint8_t* const* datas, const size_t
     if (!d_coefs || (reinterpret_cast<uintptr_t>(d_coefs) & 15))
         return set_error(HJD_E_INVALID, "d_coefs must be a 16-byte aligned device pointer");
     return gdec_run(g, datas, sizes, n, nullptr, nullptr, d_coefs, block_offsets, static_cast<hipStream_t>(stream));
+}
+
+int hjd_gdec_last_bytes(hjd_gdec* g, int64_t* host_scan_bytes, int64_t* h2d_bytes)
+{
+    if (!g) return set_error(HJD_E_INVALID, "gdec is NULL");
+    if (host_scan_bytes) *host_scan_bytes = g->last_host_scan_bytes;
+    if (h2d_bytes) *h2d_bytes = g->last_h2d;
+    return HJD_OK;
 }
 
 int hjd_gdec_set_output_format(hjd_gdec* g, int out_format)
@@ -2299,7 +2363,7 @@ static int gstream_submit(hjd_gstream* st, const uint8_t* data, size_t size, voi
         GBatch* b = st->open;
         hjd_gdec* g = st->slots[b->slot];
         RawCursor cur = b->raw;
-        rc = g->plan_raw(data, size, cur, mode, raw_off, fits);
+        rc = g->plan_raw(data, size, cur, mode, raw_off, fits, g->data_cap(), 0, false);
         if (rc) return rc;
         if (!fits || b->nframes == g->caps.max_frames || b->bytes + need > g->data_cap() ||
             b->blocks + h.nblocks > g->caps.max_blocks) {
@@ -2314,7 +2378,7 @@ static int gstream_submit(hjd_gstream* st, const uint8_t* data, size_t size, voi
         rc = st->open_batch(lk);
         if (rc) return rc;
         GBatch* b = st->open;
-        rc = st->slots[b->slot]->plan_raw(data, size, b->raw, mode, raw_off, fits);
+        rc = st->slots[b->slot]->plan_raw(data, size, b->raw, mode, raw_off, fits, g0->data_cap(), 0, false);
         if (rc) return rc;
         if (!fits) return set_error(HJD_E_INVALID, "JPEG larger than one batch's capacity");
     }

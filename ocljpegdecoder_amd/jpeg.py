@@ -266,6 +266,14 @@ class GpuDecoder:
         self._n = n
         return list(offs)
 
+    def last_bytes(self) -> dict:
+        """Bytes of the most recent decode call: scan bytes the host CPU
+        read + wrote (0 when every scan was destuffed on the GPU) and bytes
+        moved host -> device."""
+        hb, h2d = ctypes.c_int64(0), ctypes.c_int64(0)
+        check(self.lib.hjd_gdec_last_bytes(self.handle, ctypes.byref(hb), ctypes.byref(h2d)), "hjd_gdec_last_bytes")
+        return {"host_scan_bytes": hb.value, "h2d_bytes": h2d.value}
+
     def sync(self, raise_on_error: bool = True) -> List[int]:
         status = (ctypes.c_int32 * max(self._n, 1))()
         rc = self.lib.hjd_gdec_sync(self.handle, status)

@@ -1,0 +1,118 @@
+"""bench.py's N-rank bookkeeping on CPU: the functions every
+bench code path times and aggregates through, run by two gloo ranks.
+
+- timed_region: barrier + synchronize around the body, and the wall time is
+  the MAX over ranks (shard.aggregate's MAX all-reduce), on every rank;
+- stream_step_ids: the config-5 global frame-id list, dealt round-robin, covers
+  every id of a step exactly once whatever the rank count;
+- stream_check_totals: the stream's checksums are SUMMED over ranks;
+- stream_leg_command: the child run rank 0 starts (plain python at N=1,
+  torch.distributed.run at 127.0.0.1 for N>1), its step count for 100k ids,
+  and the scrubbing of this rank's torchrun variables from its environment.
+
+The real N=8 run uses the same functions over RCCL (DESIGN.md s7 lists its
+collectives); only the device layer differs (torch.cuda.synchronize).
+"""
+import os
+import socket
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    sys.path.insert(0, ROOT)
+    import time
+
+    import torch.distributed as dist
+
+    import bench
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    syncs = []
+    # rank r's body takes (r + 1) * 50 ms: every rank must report the slowest
+    wall, wall_max = bench.timed_region(dist, world, lambda: time.sleep(0.05 * (rank + 1)),
+                                        lambda: syncs.append(1))
+    ids = [bench.stream_step_ids(k, 6, rank, world) for k in range(3)]
+    got = sum(3 * i for i in ids[-1])           # stand-ins for per-frame checksums
+    agg, ok = bench.stream_check_totals(got, got, sum(ids[-1]), len(ids[-1]))
+    agg_bad, ok_bad = bench.stream_check_totals(got, got + rank, 0, 0)
+    q.put((rank, wall, wall_max, len(syncs), ids, agg, ok, ok_bad))
+    dist.destroy_process_group()
+
+
+def test_two_rank_timing_and_stream_bookkeeping():
+    import torch.multiprocessing as mp
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    walls = [r[1] for r in res]
+    for rank, wall, wall_max, nsync, ids, agg, ok, ok_bad in res:
+        assert nsync == 2                                   # synchronize before and after the body
+        assert wall_max == max(walls) and wall_max >= 0.1   # max over ranks, on every rank
+        assert ok and not ok_bad
+        assert agg["frames_checked"] == 12                  # 6 frames per GPU x 2 ranks, summed
+        assert agg["id_sum"] == sum(range(24, 36))          # step 2 covers ids [24, 36)
+        assert agg["checksum"] == 3 * sum(range(24, 36))
+    # every id of every step exactly once over the ranks
+    for k in range(3):
+        allids = sorted(i for r in res for i in r[4][k])
+        assert allids == list(range(12 * k, 12 * (k + 1)))
+
+
+def test_stream_step_ids_match_one_rank():
+    sys.path.insert(0, ROOT)
+    import bench
+    for world in (1, 2, 3, 8):
+        for k in (0, 5):
+            allids = sorted(i for r in range(world) for i in bench.stream_step_ids(k, 1024, r, world))
+            assert allids == list(range(k * 1024 * world, (k + 1) * 1024 * world))
+
+
+@pytest.mark.parametrize("world", [1, 2, 8])
+def test_stream_leg_command(world):
+    sys.path.insert(0, ROOT)
+    import bench
+    environ = {"RANK": "3", "WORLD_SIZE": str(world), "LOCAL_RANK": "3", "MASTER_PORT": "29500",
+               "TORCHELASTIC_RUN_ID": "x", "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1",
+               "HSA_ENABLE_IPC_MODE_LEGACY": "0", "PATH": "/usr/bin"}
+    cmd, env, steps = bench.stream_leg_command(world, "nccl", 100000, 1024, 41234, environ)
+    assert steps * 1024 * world >= 100000 and (steps - 1) * 1024 * world < 100000
+    assert steps == {1: 98, 2: 49, 8: 13}[world]
+    assert cmd[0] == sys.executable
+    i = cmd.index("--steps")
+    assert cmd[i + 1] == str(steps)
+    assert cmd[cmd.index("--frames") + 1] == "1024" and cmd[cmd.index("--gpus") + 1] == str(world)
+    assert cmd[cmd.index("--workload") + 1] == "stream4k420" and "--no-cpu" in cmd
+    if world == 1:
+        assert "torch.distributed.run" not in cmd
+    else:
+        assert cmd[1:3] == ["-m", "torch.distributed.run"]
+        assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+        assert cmd[cmd.index("--master-port") + 1] == "41234"
+        assert cmd[cmd.index("--nproc-per-node") + 1] == str(world)
+    # this rank's torchrun identity is not inherited; the rest of the environment is
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT", "TORCHELASTIC_RUN_ID", "GROUP_RANK"):
+        assert k not in env
+    assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0" and env["MASTER_ADDR"] == "127.0.0.1"
+    assert env["PATH"] == "/usr/bin"
+    # small runs (tests) still time >= 3 steps
+    assert bench.stream_leg_command(world, "gloo", 10, 12, 1, environ)[2] == 3

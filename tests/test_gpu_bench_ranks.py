@@ -47,7 +47,7 @@ def test_two_ranks_pixel_bench():
     extra_env = {"HJD_BENCH_STREAM_FRAMES": "12", "HJD_STREAM_POOL": "8"}
     os.environ.update(extra_env)
     try:
-        r = _run("4k420", 8, timeout=240)
+        r = _run("4k420", 8, extra=("--stream-frame-ids", "72"), timeout=240)
     finally:
         for k in extra_env:
             os.environ.pop(k, None)
@@ -58,10 +58,14 @@ def test_two_ranks_pixel_bench():
     px = 2 * 3 * 8 * 3840 * 2160
     assert abs(r["value"] - px / (r["ms_per_step"] * 3 / 1e3) / 1e6) / r["value"] < 0.02
     assert "no collective" in r["config"]["parallelism"] or "x2" in r["config"]["parallelism"]
+    c4 = r["config4_444"]                                  # configs[3] in the same run
+    assert c4["output_checked_vs_oracle"] is True and c4["frames_per_gpu"] == 8 and c4["n_gpus"] == 2
+    assert abs(c4["value"] - px / (c4["ms_per_step"] * 3 / 1e3) / 1e6) / c4["value"] < 0.02
     s5 = r["config5_stream"]
     assert "error" not in s5, s5
     assert s5["n_gpus"] == 2 and s5["value"] > 0 and s5["output_checked_vs_oracle"] is True
     assert s5["frames_per_gpu_per_step"] == 12 and "shard_round_robin over 2 rank(s)" in s5["sharding"]
+    assert s5["steps"] == 3 and s5["timed_frame_ids"] == 72 and s5["steps_checked"] == [2, 3]
 
 
 @pytest.mark.gpu

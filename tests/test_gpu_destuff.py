@@ -217,6 +217,150 @@ def test_pinned_scans_in_separate_registrations(hjd, ctx, monkeypatch):
         views = None   # the mapping goes with its last reference
 
 
+def _registered_layout(hjd, datas, gaps, first=5):
+    """The files in one anonymous mapping, file i+1 starting gaps[i] bytes after
+    file i ends; files sharing a page are page-locked together, the others in
+    registrations of their own (hjd_host_register), so the gaps between the
+    registrations are unregistered pages.  Returns (views, cleanup)."""
+    import mmap
+    import torch
+    page = mmap.PAGESIZE
+    pos, starts = first, []
+    for d, g in zip(datas, list(gaps) + [0]):
+        starts.append(pos)
+        pos += len(d) + int(g)
+    size = -(-(pos + page) // page) * page
+    mm = mmap.mmap(-1, size)
+    arr = np.frombuffer(mm, np.uint8)
+    for s, d in zip(starts, datas):
+        arr[s:s + len(d)] = np.frombuffer(d, np.uint8)
+    groups = []                                     # [first page, last page] per registration
+    for s, d in zip(starts, datas):
+        p0, p1 = s // page, (s + len(d) - 1) // page
+        if groups and p0 <= groups[-1][1]:
+            groups[-1][1] = max(groups[-1][1], p1)
+        else:
+            groups.append([p0, p1])
+    lib = hjd._lib.load()
+    base = arr.ctypes.data
+    done = []
+    for p0, p1 in groups:
+        hjd._lib.check(lib.hjd_host_register(ctypes.c_void_p(base + p0 * page), (p1 - p0 + 1) * page), "register")
+        done.append(base + p0 * page)
+    views = [torch.from_numpy(arr[s:s + len(d)]) for s, d in zip(starts, datas)]
+
+    def cleanup():
+        for p in done:
+            lib.hjd_host_unregister(ctypes.c_void_p(p))
+    return views, cleanup, len(groups)
+
+
+@pytest.mark.parametrize("policy", ["auto", "device"])
+def test_pinned_separate_registrations_exact_capacity(hjd, ctx, monkeypatch, policy):
+    """scans in separately page-locked regions at gaps of
+    1 B to 60 KiB, decoder capacity exactly the sum of the file sizes (the
+    documented sizing): every frame decodes bit-exactly on the device path
+    (no host destuff), whatever the gaps cost the mirrored DMA layout."""
+    import torch
+    monkeypatch.setenv("HJD_DESTUFF", policy)
+    base = _pil_files()
+    datas = (base * 3)[:14]
+    gaps = [1, 3, 40, 4096 + 5, 61440, 2 * 4096 + 1, 16, 20000, 60 * 1024, 7, 100, 8191, 2]
+    views, cleanup, nreg = _registered_layout(hjd, datas, gaps)
+    try:
+        assert nreg >= 6
+        infos = [hjd.parse(d) for d in datas]
+        total = sum(i.nblocks for i in infos)
+        coefs = torch.full((total + 64, 64), 0x5A5A, dtype=torch.int16, device="cuda")
+        with hjd.GpuDecoder(ctx, len(datas), sum(map(len, datas)), total) as gd:
+            for _ in range(2):
+                coefs.fill_(0x5A5A)
+                offs = gd.decode_coefs(views, coefs)
+                assert gd.last_bytes()["host_scan_bytes"] == 0
+                status = gd.sync()
+                host = coefs.cpu().numpy()
+                for d, o, i, s in zip(datas, offs, infos, status):
+                    ref, _ = hjd.decode_coefs(d)
+                    np.testing.assert_array_equal(host[o:o + i.nblocks], ref)
+                    assert s & ~1 == 0
+                assert (host[total:] == 0x5A5A).all()
+    finally:
+        views = None
+        cleanup()
+
+
+def test_pinned_capacity_by_entropy_bytes_falls_back_to_host(hjd, ctx, monkeypatch):
+    """sized by entropy-coded bytes (the older sizing), pinned
+    frames whose raw scans would not fit are destuffed on the host in auto
+    mode instead of failing the batch; HJD_DESTUFF=device reports it."""
+    import torch
+    datas = _pil_files()
+    ent = 0
+    for d in datas:
+        scan = np.frombuffer(d[hjd.parse(d).scan_offset:], np.uint8).copy()
+        ent += len(_host(hjd, scan)[0])
+    pinned = [hjd.pinned_bytes(d) for d in datas]
+    infos = [hjd.parse(d) for d in datas]
+    total = sum(i.nblocks for i in infos)
+    coefs = torch.full((total, 64), 0x5A5A, dtype=torch.int16, device="cuda")
+    monkeypatch.setenv("HJD_DESTUFF", "auto")
+    with hjd.GpuDecoder(ctx, len(datas), ent, total) as gd:
+        offs = gd.decode_coefs(pinned, coefs)
+        assert gd.last_bytes()["host_scan_bytes"] > 0
+        status = gd.sync()
+        host = coefs.cpu().numpy()
+        for d, o, i, s in zip(datas, offs, infos, status):
+            ref, _ = hjd.decode_coefs(d)
+            np.testing.assert_array_equal(host[o:o + i.nblocks], ref)
+            assert s & ~1 == 0
+        monkeypatch.setenv("HJD_DESTUFF", "device")
+        with pytest.raises(hjd._lib.HjdError):
+            gd.decode_coefs(pinned, coefs)
+
+
+def test_pinned_input_reusable_on_return(hjd, ctx, monkeypatch):
+    """hjd_gdec_decode* may return before the kernels run, but
+    not before the DMA has read the caller's pinned bytes; overwriting them
+    right after the call must not change the result."""
+    import torch
+    monkeypatch.setenv("HJD_DESTUFF", "auto")
+    datas = [E._pil(2048, 1536, 95, 0, seed=41), E._pil(1920, 1080, 90, 2, seed=42)] + _pil_files()[:2]
+    infos = [hjd.parse(d) for d in datas]
+    total = sum(i.nblocks for i in infos)
+    coefs = torch.full((total, 64), 0x5A5A, dtype=torch.int16, device="cuda")
+    with hjd.GpuDecoder(ctx, len(datas), sum(map(len, datas)), total) as gd:
+        for rep in range(3):
+            pinned = [hjd.pinned_bytes(d) for d in datas]
+            offs = gd.decode_coefs(pinned, coefs)
+            for p in pinned:
+                p.fill_(0xFF)                  # the caller reuses its buffers at once
+            status = gd.sync()
+            host = coefs.cpu().numpy()
+            for d, o, i, s in zip(datas, offs, infos, status):
+                ref, _ = hjd.decode_coefs(d)
+                np.testing.assert_array_equal(host[o:o + i.nblocks], ref)
+                assert s & ~1 == 0
+
+
+@pytest.mark.parametrize("policy", ["auto", "device"])
+def test_small_last_scan_tight_decoder(hjd, ctx, monkeypatch, policy):
+    """the destuff kernels walk a frame's whole last 16-KiB
+    tile; a small scan that ends a tightly sized raw area must decode (lanes
+    past the scan's end load nothing)."""
+    import torch
+    monkeypatch.setenv("HJD_DESTUFF", policy)
+    for d in [E._pil(1, 1, 90, 2, seed=3), E._pil(33, 17, 90, 0, seed=4), E._pil(64, 64, 50, 2, seed=5)]:
+        info = hjd.parse(d)
+        p = hjd.pinned_bytes(d)
+        coefs = torch.full((info.nblocks, 64), 0x5A5A, dtype=torch.int16, device="cuda")
+        with hjd.GpuDecoder(ctx, 1, len(d), info.nblocks) as gd:
+            gd.decode_coefs([p], coefs)
+            assert gd.last_bytes()["host_scan_bytes"] == 0
+            assert gd.sync()[0] & ~1 == 0
+        ref, _ = hjd.decode_coefs(d)
+        np.testing.assert_array_equal(coefs.cpu().numpy(), ref)
+
+
 def test_pinned_inputs_stream_no_host_scan_bytes(hjd, ctx, monkeypatch):
     import torch
     monkeypatch.setenv("HJD_DESTUFF", "auto")
