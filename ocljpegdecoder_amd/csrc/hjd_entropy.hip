@@ -361,13 +361,20 @@ struct EntBatchDev {
     uint32_t* status;
     int16_t* coefs;
     uint32_t nframes, nwg, sub_bits, ntab_max;   // ntab_max: tables of the largest frame (dynamic LDS)
+    uint32_t nsub_total;                         // subsequences of the batch
     // device destuff (ntiles == 0: every frame of the batch was destuffed on the host)
     const uint8_t* raw;          // raw scan bytes, frame f at frames[f].data_off
     RawFrame* rawf;              // [nframes]
     const uint32_t* tile_frame;  // [ntiles] frame of each tile
     uint32_t* tiles;             // [3][ntiles] scratch: emitted bytes, markers, end (then offsets)
     uint32_t ntiles;
+    // speculative sync (latency decoders; null otherwise): [sub][kMaxBpm] records
+    struct SpecRec* spec;        // [sub][kMaxBpm]
+    struct CandRec* cand;        // [sub][kSlots]
+    uint8_t* cmap;               // [sub][kSlotRow]
+    uint32_t spec_lead;          // lead-in of the spec runs (bits)
 };
+
 
 // `blocks`: the frame's block_info() records (fill_blocks), LDS on the device.
 __host__ __device__ __forceinline__ RunCtx make_ctx(const EntBatchDev& b, const EntFrame& F, const HuffLut* tabs,
@@ -411,6 +418,148 @@ __host__ __device__ __forceinline__ uint32_t frame_groups(uint32_t nsub) { retur
 __host__ __device__ __forceinline__ int64_t group_sub(uint32_t gl, int t)
 {
     return static_cast<int64_t>(gl) * kOwn - kWarm + t;
+}
+
+// Speculative sync (latency mode, DESIGN.md s10 "Single-image latency").
+// The round-based sync guesses one entry per subsequence, (k*S, j = 0,
+// z = 0): bits and z fall into step with the true decode within a few hundred
+// bits, but the block-in-MCU index j only by chance, so a lone frame's chains
+// take ~7 serial rounds of S-bit re-runs to verify (measured by the emulation:
+// 4-10 rounds per group on an FHD q90 frame at S = 1024).  Here:
+//   ent_spec_kernel   runs every subsequence k from all P = bpm guesses
+//                     (k*S - W, j, 0), a lead-in of W bits before its start:
+//                     the state at its middle (checkpoint), its exit and the
+//                     second half's statistics.  One of the P guesses meets
+//                     the true decode within 512 bits for 89 % of starts and
+//                     within 1024 for 98 % (one guess: 25 % and 54 %;
+//                     hjd_debug_entropy_syncstats with HJD_SYNC_PHASES);
+//   ent_cand_kernel   runs k from each of its predecessor's P spec exits
+//                     (subsequence 0: from the frame start), stopping at the
+//                     middle when the run meets one of k's checkpoints; the
+//                     exit's index among k's spec exits is k+1's entry slot
+//                     (cmap).  An exit that is none of them opens an overflow
+//                     slot of k+1 (two levels), so the maps are total on real
+//                     data;
+//   ent_chain_kernel  one workgroup per frame composes the slot maps (a scan
+//                     over threads, each owning a range of subsequences) from
+//                     the frame start: every subsequence's verified entry,
+//                     statistics and mid-state follow without serial rounds,
+//                     and the group records (agg, wentries, linked) the link,
+//                     fallback and write kernels read.
+// The chain is exact by construction (every record comes from a real run of
+// its subsequence from the entry it names, starting at the frame start); a
+// chain that leaves all slots (none seen) falls back to the sequential repair.
+struct SpecRec {          // spec run of subsequence k from guess (k*S - W, j, 0)
+    uint64_t cp;          // state at the first unit boundary >= k*S + S/2
+    uint64_t x;           // exit
+    SubStats s2;          // statistics cp -> x
+};
+static_assert(sizeof(SpecRec) == 32, "SpecRec layout");
+struct CandRec {          // subsequence k run from the entry of one of its slots
+    SubStats s1, s;       // statistics entry -> mid and entry -> exit
+    uint64_t e, mid, y;   // entry, mid-state, exit
+    uint64_t pad;
+};
+static_assert(sizeof(CandRec) == 64, "CandRec layout");
+constexpr uint32_t kNoCand = 0xFF;                   // no slot
+constexpr int kOvfLevels = 2;                        // overflow slots: P per level
+constexpr int kSlots = (1 + kOvfLevels) * kMaxBpm;   // candidate and overflow slots per subsequence
+constexpr int kRepairSlot = kSlots;                  // written by ent_chain_kernel's repair
+constexpr int kChainSlots = kSlots + 1;
+constexpr int kCandRow = kChainSlots;                // CandRec row stride
+constexpr int kSlotRow = 20;                         // cmap row stride (bytes, >= kChainSlots)
+static_assert(kSlotRow >= kChainSlots, "cmap row");
+
+// The spec run of subsequence k from guess j, with a lead-in of `lead` bits.
+__host__ __device__ __forceinline__ SpecRec spec_run(const RunCtx& c, uint32_t k, uint32_t j, uint32_t S, uint32_t lead)
+{
+    const uint32_t start = k * S > lead ? k * S - lead : 0u;
+    const uint64_t g = guess_entry(c, start);
+    SpecRec r;
+    SubStats s1 = stats_identity();
+    r.cp = run<false>(c, pack_state(st_pos(g), j, 0, st_seg(g)), k * S + S / 2, s1, nullptr);
+    r.s2 = stats_identity();
+    r.x = run<false>(c, r.cp, (k + 1) * S, r.s2, nullptr);
+    return r;
+}
+
+// Subsequence k from entry e: to the middle; if that state is one of k's
+// spec checkpoints, the rest is that spec run's, else decode on.  sk: k's P
+// spec records.  Returns the index of the exit among k's spec exits, or kNoCand.
+__host__ __device__ __forceinline__ uint32_t cand_run(const RunCtx& c, uint32_t k, uint64_t e, uint32_t S,
+                                                      const SpecRec* sk, uint32_t P, CandRec& out)
+{
+    out.e = e;
+    out.pad = 0;
+    out.s1 = stats_identity();
+    out.mid = run<false>(c, e, k * S + S / 2, out.s1, nullptr);
+    uint32_t jm = kNoCand;
+    for (uint32_t j = 0; j < P; ++j)
+        if (jm == kNoCand && same_state(out.mid, sk[j].cp)) jm = j;
+    if (jm != kNoCand) {
+        out.y = sk[jm].x;
+        out.s = stats_combine(out.s1, sk[jm].s2);
+    } else {
+        SubStats s2 = stats_identity();
+        out.y = run<false>(c, out.mid, (k + 1) * S, s2, nullptr);
+        out.s = stats_combine(out.s1, s2);
+    }
+    uint32_t idx = kNoCand;
+    for (uint32_t j = 0; j < P; ++j)
+        if (idx == kNoCand && same_state(out.y, sk[j].x)) idx = j;
+    return idx;
+}
+
+// Candidate c < P of subsequence k (entry: spec exit c of k-1, or the frame
+// start), and its overflow continuation: while the exit is none of the
+// successor's spec exits, the successor is run from it in overflow slot
+// (level + 1) * P + c, up to kOvfLevels levels.  Each slot has exactly one writer.
+__host__ __device__ __forceinline__ void cand_chain(const RunCtx& c, const EntBatchDev& b, const EntFrame& F,
+                                                    uint32_t k, uint32_t cidx)
+{
+    const uint32_t P = F.bpm, S = b.sub_bits;
+    uint64_t e = k == 0 ? guess_entry(c, 0)
+                        : b.spec[(static_cast<uint64_t>(F.sub_base) + k - 1) * kMaxBpm + cidx].x;
+    uint32_t slot = cidx;
+    for (int level = 0;; ++level) {
+        const uint64_t row = static_cast<uint64_t>(F.sub_base) + k;
+        CandRec r;
+        const uint32_t nx = cand_run(c, k, e, S, b.spec + row * kMaxBpm, P, r);
+        b.cand[row * kCandRow + slot] = r;
+        if (nx != kNoCand || level == kOvfLevels || k + 1 >= F.nsub) {
+            b.cmap[row * kSlotRow + slot] = static_cast<uint8_t>(nx);
+            return;
+        }
+        const uint32_t next = static_cast<uint32_t>(level + 1) * P + cidx;
+        b.cmap[row * kSlotRow + slot] = static_cast<uint8_t>(next);
+        e = r.y;
+        slot = next;
+        ++k;
+    }
+}
+
+// The chain leaves every slot at subsequence brk (its predecessor, entered at
+// slot sp, exits at a state none of brk's slots holds): run brk on from that
+// exit in the repair slot, and its successors until the exit is a spec exit
+// again, linking the predecessor's map to the repair slot.
+__host__ __device__ __forceinline__ void chain_repair(const RunCtx& c, const EntBatchDev& b, const EntFrame& F,
+                                                      uint32_t brk, uint32_t sp)
+{
+    uint8_t* cm = b.cmap + static_cast<uint64_t>(F.sub_base) * kSlotRow;
+    uint64_t e = b.cand[(static_cast<uint64_t>(F.sub_base) + brk - 1) * kCandRow + sp].y;
+    cm[static_cast<uint64_t>(brk - 1) * kSlotRow + sp] = static_cast<uint8_t>(kRepairSlot);
+    for (uint32_t k = brk;; ++k) {
+        const uint64_t row = static_cast<uint64_t>(F.sub_base) + k;
+        CandRec r;
+        const uint32_t nx = cand_run(c, k, e, b.sub_bits, b.spec + row * kMaxBpm, F.bpm, r);
+        b.cand[row * kCandRow + kRepairSlot] = r;
+        if (nx != kNoCand || k + 1 >= F.nsub) {
+            cm[static_cast<uint64_t>(k) * kSlotRow + kRepairSlot] = static_cast<uint8_t>(nx);
+            return;
+        }
+        cm[static_cast<uint64_t>(k) * kSlotRow + kRepairSlot] = static_cast<uint8_t>(kRepairSlot);
+        e = r.y;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -639,6 +788,223 @@ __global__ __launch_bounds__(kGroupSubs) void ent_sync_kernel(EntBatchDev b)
         SubStats a = L.wsum[0];
         for (int i = 1; i < kGroupSubs / 64; ++i) a = stats_combine(a, L.wsum[i]);
         b.agg[w] = a;
+    }
+}
+
+// ---- speculative sync (latency decoders) ------------------------------------
+// Grid (groups, kMaxBpm): block (w, j) runs guess j of group w's owned
+// subsequences (the warm-up ones belong to the previous group).
+__global__ __launch_bounds__(kGroupSubs) void ent_spec_kernel(EntBatchDev b)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    HuffLut* tabs = reinterpret_cast<HuffLut*>(smem);
+    uint8_t* steps = smem + sizeof(HuffLut) * b.ntab_max;
+    __shared__ BlockInfo blocks[kMaxBpm];
+    const int tid = threadIdx.x;
+    const uint32_t w = blockIdx.x, j = blockIdx.y;
+    const uint32_t f = b.wg_frame[w];
+    const EntFrame F = b.frames[f];
+    const uint32_t gl = w - F.wg_base;
+    if (gl >= frame_groups(F.nsub) || j >= F.bpm) return;
+    load_tables(tabs, blocks, b.tabs + F.tab_base, F, b.frames + f, tid, kGroupSubs);
+    __syncthreads();
+    fill_steps(steps, tabs, F.ntab, tid, kGroupSubs);
+    __syncthreads();
+    const int64_t k = group_sub(gl, tid);
+    if (tid < kWarm || k >= static_cast<int64_t>(F.nsub)) return;
+    const RunCtx c = make_ctx(b, F, tabs, blocks, steps);
+    const uint64_t idx = (static_cast<uint64_t>(F.sub_base) + static_cast<uint64_t>(k)) * kMaxBpm + j;
+    b.spec[idx] = spec_run(c, static_cast<uint32_t>(k), j, b.sub_bits, b.spec_lead);
+}
+
+// Grid (groups, kMaxBpm): block (w, i) runs candidate i of group w's owned
+// subsequences, with its overflow continuation (cand_chain).
+__global__ __launch_bounds__(kGroupSubs) void ent_cand_kernel(EntBatchDev b)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    HuffLut* tabs = reinterpret_cast<HuffLut*>(smem);
+    uint8_t* steps = smem + sizeof(HuffLut) * b.ntab_max;
+    __shared__ BlockInfo blocks[kMaxBpm];
+    const int tid = threadIdx.x;
+    const uint32_t w = blockIdx.x, i = blockIdx.y;
+    const uint32_t f = b.wg_frame[w];
+    const EntFrame F = b.frames[f];
+    const uint32_t gl = w - F.wg_base;
+    if (gl >= frame_groups(F.nsub) || i >= F.bpm) return;
+    load_tables(tabs, blocks, b.tabs + F.tab_base, F, b.frames + f, tid, kGroupSubs);
+    __syncthreads();
+    fill_steps(steps, tabs, F.ntab, tid, kGroupSubs);
+    __syncthreads();
+    const int64_t k = group_sub(gl, tid);
+    if (tid < kWarm || k >= static_cast<int64_t>(F.nsub)) return;
+    const RunCtx c = make_ctx(b, F, tabs, blocks, steps);
+    cand_chain(c, b, F, static_cast<uint32_t>(k), i);
+}
+
+// One workgroup per frame walks the chain from the frame start (slot 0 of
+// subsequence 0) through chunks of kChainChunk subsequences: the chunk's slot
+// maps are loaded into LDS (coalesced), thread t composes its kChainRows
+// consecutive rows into one function, the group scans those functions, and the
+// chunk's entering slot under the prefix is thread t's entering slot.  Where
+// the chain leaves every slot (an exit that is none of the successor's
+// candidates even after the overflow levels; rare), thread 0 re-runs it from
+// the known exit in the repair slot of the following subsequences until it
+// lands in a slot again, and the chunk is scanned anew.  Each thread then
+// copies its rows' records into the sync outputs; last, one wave per group
+// reduces the group's statistics (agg) and writes its warm-up entries.
+constexpr int kChainThreads = 512;
+
+constexpr int kChainRows = 8;                                  // rows per thread and chunk
+constexpr int kChainChunk = kChainThreads * kChainRows;        // 4096 subsequences
+
+struct ChainLds {
+    uint8_t rows[kChainChunk][kSlotRow];        // the chunk's slot maps
+    uint8_t fn[2][kChainThreads][kSlotRow];     // scan of the threads' functions (double buffer)
+    unsigned long long brk;                     // first break: subsequence << 8 | its predecessor's slot
+    uint32_t carry;                             // slot entering the chunk
+    HuffLut tabs[kMaxTables];                   // the frame's tables (repairs)
+    uint8_t steps[kMaxTables << kStepBits];
+    BlockInfo blocks[kMaxBpm];
+};
+
+__global__ __launch_bounds__(kChainThreads) void ent_chain_kernel(EntBatchDev b)
+{
+    __shared__ ChainLds L;
+    HuffLut* tabs = L.tabs;
+    uint8_t* steps = L.steps;
+    BlockInfo* blocks = L.blocks;
+    const int tid = threadIdx.x;
+    const uint32_t f = blockIdx.x;
+    const EntFrame F = b.frames[f];
+    const uint32_t n = F.nsub;
+    uint8_t* cm = b.cmap + static_cast<uint64_t>(F.sub_base) * kSlotRow;
+    load_tables(tabs, blocks, b.tabs + F.tab_base, F, b.frames + f, tid, kChainThreads);
+    if (tid == 0) L.carry = 0;
+    __syncthreads();
+    fill_steps(steps, tabs, F.ntab, tid, kChainThreads);
+    const RunCtx c = make_ctx(b, F, tabs, blocks, steps);
+    for (uint32_t c0 = 0; c0 < n; c0 += kChainChunk) {
+        const uint32_t cn = n - c0 < static_cast<uint32_t>(kChainChunk) ? n - c0 : kChainChunk;
+        const uint32_t r0 = static_cast<uint32_t>(tid) * kChainRows;   // this thread's rows within the chunk
+        uint32_t slot;
+        for (;;) {
+            __syncthreads();
+            {   // the chunk's rows, 4-byte words, coalesced; all of a thread's loads in flight at once
+                constexpr int kWords = kChainChunk * (kSlotRow / 4) / kChainThreads;   // 40
+                const uint32_t* src = reinterpret_cast<const uint32_t*>(cm + static_cast<uint64_t>(c0) * kSlotRow);
+                uint32_t* dst = reinterpret_cast<uint32_t*>(&L.rows[0][0]);
+                const uint32_t nw = cn * (kSlotRow / 4);
+                uint32_t t[kWords];
+#pragma unroll
+                for (int i = 0; i < kWords; ++i) {
+                    const uint32_t j = static_cast<uint32_t>(tid + i * kChainThreads);
+                    t[i] = j < nw ? src[j] : 0u;
+                }
+#pragma unroll
+                for (int i = 0; i < kWords; ++i) dst[tid + i * kChainThreads] = t[i];
+            }
+            if (tid == 0) L.brk = ~0ull;
+            __syncthreads();
+            uint32_t v[kChainSlots];
+#pragma unroll
+            for (int s = 0; s < kChainSlots; ++s) v[s] = static_cast<uint32_t>(s);
+#pragma unroll 1
+            for (uint32_t r = r0; r < r0 + kChainRows && r < cn; ++r) {
+#pragma unroll
+                for (int s = 0; s < kChainSlots; ++s) v[s] = v[s] == kNoCand ? kNoCand : L.rows[r][v[s]];
+            }
+#pragma unroll
+            for (int s = 0; s < kChainSlots; ++s) L.fn[0][tid][s] = static_cast<uint8_t>(v[s]);
+            __syncthreads();
+            int cur = 0;
+#pragma unroll 1
+            for (int d = 1; d < kChainThreads; d <<= 1) {   // inclusive: fn[t] = thread 0's rows then ... then t's
+#pragma unroll
+                for (int s = 0; s < kChainSlots; ++s) {
+                    const uint8_t a = tid >= d ? L.fn[cur][tid - d][s] : static_cast<uint8_t>(s);
+                    L.fn[cur ^ 1][tid][s] = a == kNoCand ? static_cast<uint8_t>(kNoCand) : L.fn[cur][tid][a];
+                }
+                cur ^= 1;
+                __syncthreads();
+            }
+            const uint32_t carry = L.carry;
+            slot = tid == 0 ? carry : (carry == kNoCand ? kNoCand : L.fn[cur][tid - 1][carry]);
+            // the first subsequence without a slot: the row whose map sends the
+            // chain's slot to none (subsequence 0's slots all exist)
+            uint32_t s = slot;
+            for (uint32_t r = r0; r < r0 + kChainRows && r < cn && s != kNoCand; ++r) {
+                const uint32_t nx = L.rows[r][s];
+                if (nx == kNoCand && c0 + r + 1 < n) {
+                    atomicMin(&L.brk, (static_cast<unsigned long long>(c0 + r + 1) << 8) | s);
+                    break;
+                }
+                s = nx;
+            }
+            __syncthreads();
+            const unsigned long long brk = L.brk;
+            if (brk == ~0ull) break;
+            if (tid == 0) chain_repair(c, b, F, static_cast<uint32_t>(brk >> 8), static_cast<uint32_t>(brk & 0xFF));
+        }
+        // copy the records of this thread's rows: the slots first (LDS), then
+        // the loads of four records at a time in flight (16-B vector copies: a
+        // SubStats copy goes through scratch)
+        uint32_t s = slot, sl[kChainRows];
+#pragma unroll
+        for (int i = 0; i < kChainRows; ++i) {
+            sl[i] = s;
+            if (r0 + i < cn) s = L.rows[r0 + i][s];
+        }
+#pragma unroll
+        for (int h = 0; h < kChainRows; h += 4) {
+            u32x4 q[4][3];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint64_t row = static_cast<uint64_t>(F.sub_base) + c0 + r0 + h + i;
+                if (r0 + h + i < cn) {
+                    const u32x4* rec = reinterpret_cast<const u32x4*>(b.cand + row * kCandRow + sl[h + i]);
+                    q[i][0] = rec[0];
+                    q[i][1] = rec[1];
+                    q[i][2] = rec[2];
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint64_t row = static_cast<uint64_t>(F.sub_base) + c0 + r0 + h + i;
+                if (r0 + h + i < cn) {
+                    reinterpret_cast<u32x4*>(b.stats1)[row] = q[i][0];
+                    reinterpret_cast<u32x4*>(b.stats)[row] = q[i][1];
+                    b.entries[row] = static_cast<uint64_t>(q[i][2].x) | static_cast<uint64_t>(q[i][2].y) << 32;
+                    b.mids[row] = static_cast<uint64_t>(q[i][2].z) | static_cast<uint64_t>(q[i][2].w) << 32;
+                }
+            }
+        }
+        __syncthreads();
+        if (r0 < cn && (r0 + kChainRows >= cn)) L.carry = s;   // the thread holding the chunk's last row
+    }
+    __syncthreads();
+    // per group: ordered reduction of the owned statistics (one wave per group)
+    const int wv = tid >> 6, lane = tid & 63;
+    for (uint32_t g = wv; g < frame_groups(n); g += kChainThreads / 64) {
+        const uint32_t w = F.wg_base + g;
+        const uint32_t end = (g + 1) * kOwn < n ? (g + 1) * kOwn : n;
+        SubStats a = stats_identity();
+        SubStats q[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {   // 4 x 64 >= kOwn; the four loads in flight together
+            const uint32_t k = g * kOwn + lane * 4 + i;
+            q[i] = k < end ? b.stats[F.sub_base + k] : stats_identity();
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a = stats_combine(a, q[i]);
+        a = wave_reduce_ordered(a, lane);
+        if (lane == 0) {
+            b.agg[w] = a;
+            b.linked[w] = 1u;
+        }
+        if (lane < kWarm) {
+            const int64_t k = group_sub(g, lane);
+            b.wentries[static_cast<uint64_t>(w) * kWarm + lane] = k >= 0 ? b.entries[F.sub_base + k] : 0;
+        }
     }
 }
 
@@ -1117,11 +1483,89 @@ __global__ __launch_bounds__(kTileThreads) void destuff_write_kernel(EntBatchDev
 // Host emulation of the four kernels (test hook; same state machine and the
 // same group geometry, without the LDS window)
 // ---------------------------------------------------------------------------
+// Host emulation of ent_spec_kernel, ent_cand_kernel and ent_chain_kernel.
+void emulate_spec_sync(const EntBatchDev& b)
+{
+    const uint32_t S = b.sub_bits;
+    for (int pass = 0; pass < 2; ++pass) {   // 0: spec runs, 1: candidate chains
+        for (uint32_t w = 0; w < b.nwg; ++w) {
+            const EntFrame& F = b.frames[b.wg_frame[w]];
+            const uint32_t gl = w - F.wg_base;
+            if (gl >= frame_groups(F.nsub)) continue;
+            BlockInfo blocks[kMaxBpm];
+            fill_blocks(blocks, F);
+            std::vector<uint8_t> steps(static_cast<size_t>(F.ntab) << kStepBits);
+            fill_steps(steps.data(), b.tabs + F.tab_base, F.ntab, 0, 1);
+            const RunCtx c = make_ctx(b, F, b.tabs + F.tab_base, blocks, steps.data());
+            for (int t = kWarm; t < kGroupSubs; ++t) {
+                const int64_t k = group_sub(gl, t);
+                if (k >= static_cast<int64_t>(F.nsub)) break;
+                for (uint32_t j = 0; j < F.bpm; ++j) {
+                    if (pass == 0)
+                        b.spec[(static_cast<uint64_t>(F.sub_base) + static_cast<uint64_t>(k)) * kMaxBpm + j] =
+                            spec_run(c, static_cast<uint32_t>(k), j, S, b.spec_lead);
+                    else
+                        cand_chain(c, b, F, static_cast<uint32_t>(k), j);
+                }
+            }
+        }
+    }
+    for (uint32_t f = 0; f < b.nframes; ++f) {   // the chain kernel's walk, in order, with its repairs
+        const EntFrame& F = b.frames[f];
+        const uint32_t n = F.nsub;
+        BlockInfo blocks[kMaxBpm];
+        fill_blocks(blocks, F);
+        std::vector<uint8_t> steps(static_cast<size_t>(F.ntab) << kStepBits);
+        fill_steps(steps.data(), b.tabs + F.tab_base, F.ntab, 0, 1);
+        const RunCtx c = make_ctx(b, F, b.tabs + F.tab_base, blocks, steps.data());
+        uint32_t slot = 0, prev = 0;
+        int nrepair = 0;
+        for (uint32_t k = 0; k < n; ++k) {
+            const uint64_t row = static_cast<uint64_t>(F.sub_base) + k;
+            if (slot == kNoCand) {
+                chain_repair(c, b, F, k, prev);
+                slot = kRepairSlot;
+                ++nrepair;
+            }
+            const CandRec& r = b.cand[row * kCandRow + slot];
+            b.entries[row] = r.e;
+            b.stats[row] = r.s;
+            b.mids[row] = r.mid;
+            b.stats1[row] = r.s1;
+            prev = slot;
+            slot = b.cmap[row * kSlotRow + slot];
+        }
+        if (getenv("HJD_EMU_ROUNDS")) {
+            int novf[kOvfLevels + 2] = {};
+            for (uint32_t k = 0; k < n; ++k)
+                for (uint32_t q = 0; q < F.bpm; ++q) {
+                    const uint32_t v = b.cmap[(static_cast<uint64_t>(F.sub_base) + k) * kSlotRow + q];
+                    novf[v == kNoCand ? kOvfLevels + 1 : v >= static_cast<uint32_t>(kSlots) ? 0 : v / F.bpm]++;
+                }
+            fprintf(stderr, "chain: nsub %u repairs %d; level-0 candidates -> spec %d, overflow %d, none %d\n", n,
+                    nrepair, novf[0], novf[1], novf[kOvfLevels + 1]);
+        }
+        for (uint32_t g = 0; g < frame_groups(n); ++g) {
+            const uint32_t w = F.wg_base + g;
+            SubStats a = stats_identity();
+            const uint32_t end = (g + 1) * kOwn < n ? (g + 1) * kOwn : n;
+            for (uint32_t k = g * kOwn; k < end; ++k) a = stats_combine(a, b.stats[F.sub_base + k]);
+            b.agg[w] = a;
+            for (int t = 0; t < kWarm; ++t) {
+                const int64_t k = group_sub(g, t);
+                b.wentries[static_cast<uint64_t>(w) * kWarm + t] = k >= 0 ? b.entries[F.sub_base + k] : 0;
+            }
+            b.linked[w] = 1u;
+        }
+    }
+}
+
 void emulate(const EntBatchDev& b)
 {
     const uint32_t S = b.sub_bits;
-    // sync: per group, phase 1 then the rounds
-    for (uint32_t w = 0; w < b.nwg; ++w) {
+    // sync: per group, phase 1 then the rounds (or the speculative sync)
+    if (b.spec) emulate_spec_sync(b);
+    for (uint32_t w = 0; w < (b.spec ? 0u : b.nwg); ++w) {
         const EntFrame& F = b.frames[b.wg_frame[w]];
         BlockInfo blocks[kMaxBpm];
         fill_blocks(blocks, F);
@@ -1185,7 +1629,10 @@ void emulate(const EntBatchDev& b)
                 (*nxt)[t] = x[t];
             }
             std::swap(cur, nxt);
-            if (!changed) break;
+            if (!changed) {
+                if (getenv("HJD_EMU_ROUNDS")) fprintf(stderr, "group %u: %d rounds\n", gl, round + 1);
+                break;
+            }
         }
         SubStats a = stats_identity();
         for (int t = 0; t < kGroupSubs; ++t) {
@@ -1201,8 +1648,8 @@ void emulate(const EntBatchDev& b)
         }
         b.agg[w] = a;
     }
-    // link
-    for (uint32_t w = 0; w < b.nwg; ++w) {
+    // link (the speculative sync's chain kernel writes the group records itself)
+    for (uint32_t w = 0; w < (b.spec ? 0u : b.nwg); ++w) {
         const uint32_t f = b.wg_frame[w];
         const EntFrame& F = b.frames[f];
         const uint32_t gl = w - F.wg_base;
@@ -1252,6 +1699,13 @@ void emulate(const EntBatchDev& b)
 
 }  // namespace
 
+// Lead-in of the speculative sync's spec runs (HJD_SPEC_LEAD overrides; tuning).
+uint32_t spec_lead_bits()
+{
+    const char* e = getenv("HJD_SPEC_LEAD");   // read per batch (~100 ns): tests switch it in-process
+    return e ? static_cast<uint32_t>(atoi(e)) : 512u;
+}
+
 // ---------------------------------------------------------------------------
 // Batch object
 // ---------------------------------------------------------------------------
@@ -1275,6 +1729,10 @@ struct hjd_gdec {
     int16_t* d_coefs = nullptr;
     uint8_t* d_raw = nullptr;           // raw scan bytes of device-destuffed frames (same offsets as the data area)
     uint32_t* d_tiles = nullptr;        // destuff scratch [3][max_tiles]
+    bool spec = false;                  // speculative sync (latency decoders: ent_spec/cand/sync_spec kernels)
+    SpecRec* d_spec = nullptr;          // [max_subs][kMaxBpm]
+    CandRec* d_cand = nullptr;
+    uint8_t* d_cmap = nullptr;
     hipEvent_t staged = nullptr, done = nullptr;
     int64_t last_h2d = 0;               // bytes the last issue moved host -> device
     int64_t last_host_scan_bytes = 0;   // scan bytes the host CPU read + wrote for the staged frames
@@ -1289,6 +1747,9 @@ struct hjd_gdec {
     std::vector<uint32_t> e_linked;
     std::vector<SubStats> e_stats, e_agg, e_stats1;
     std::vector<uint32_t> e_status;
+    std::vector<SpecRec> e_spec;
+    std::vector<CandRec> e_cand;
+    std::vector<uint8_t> e_cmap;
 
     uint8_t* data_area() { return h_stage + caps.data; }
     size_t data_cap() const { return static_cast<size_t>(caps.max_scan_bytes) + kDataPad * caps.max_frames +
@@ -1546,6 +2007,11 @@ int hjd_gdec::assemble(uint8_t* blob, int16_t* coefs, int64_t* block_offsets, vo
     }
 
     d.ntiles = static_cast<uint32_t>(ntiles);
+    d.spec = nullptr;
+    d.cand = nullptr;
+    d.cmap = nullptr;
+    d.spec_lead = 0;
+    d.nsub_total = sub_base;
     d.rawf = nullptr;
     d.tile_frame = nullptr;
     if (ntiles) {
@@ -1605,6 +2071,12 @@ int gdec_alloc(hjd_gdec* g)
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_coefs), 128 * static_cast<size_t>(g->caps.max_blocks)));
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_raw), g->data_cap()));
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_tiles), 12 * static_cast<size_t>(g->caps.max_tiles)));
+    if (g->spec) {
+        const size_t n = static_cast<size_t>(g->caps.max_subs);
+        HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_spec), sizeof(SpecRec) * kMaxBpm * n));
+        HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_cand), sizeof(CandRec) * kCandRow * n));
+        HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_cmap), kSlotRow * n));
+    }
     HJD_HIP(hipEventCreateWithFlags(&g->staged, hipEventDisableTiming));
     HJD_HIP(hipEventCreateWithFlags(&g->done, hipEventDisableTiming));
     return HJD_OK;
@@ -1623,10 +2095,21 @@ int launch_entropy(hjd_gdec* g, const EntBatchDev& b, hipStream_t s)
         hipLaunchKernelGGL(destuff_write_kernel, dim3(b.ntiles), dim3(kTileThreads), 0, s, b);
         HJD_HIP(hipGetLastError());
     }
-    hipLaunchKernelGGL(ent_sync_kernel, dim3(b.nwg), dim3(kGroupSubs), sync_lds_bytes(b.ntab_max), s, b);
-    HJD_HIP(hipGetLastError());
-    hipLaunchKernelGGL(ent_link_kernel, dim3((b.nwg + 255) / 256), dim3(256), 0, s, b);
-    HJD_HIP(hipGetLastError());
+    if (b.spec) {   // speculative sync: latency decoders
+        const size_t tl = (sizeof(HuffLut) + (1u << kStepBits)) * b.ntab_max;
+        HJD_HIP(hipMemsetAsync(b.cmap, 0xFF, static_cast<size_t>(b.nsub_total) * kSlotRow, s));
+        hipLaunchKernelGGL(ent_spec_kernel, dim3(b.nwg, kMaxBpm), dim3(kGroupSubs), tl, s, b);
+        HJD_HIP(hipGetLastError());
+        hipLaunchKernelGGL(ent_cand_kernel, dim3(b.nwg, kMaxBpm), dim3(kGroupSubs), tl, s, b);
+        HJD_HIP(hipGetLastError());
+        hipLaunchKernelGGL(ent_chain_kernel, dim3(b.nframes), dim3(kChainThreads), 0, s, b);   // + group records
+        HJD_HIP(hipGetLastError());
+    } else {
+        hipLaunchKernelGGL(ent_sync_kernel, dim3(b.nwg), dim3(kGroupSubs), sync_lds_bytes(b.ntab_max), s, b);
+        HJD_HIP(hipGetLastError());
+        hipLaunchKernelGGL(ent_link_kernel, dim3((b.nwg + 255) / 256), dim3(256), 0, s, b);
+        HJD_HIP(hipGetLastError());
+    }
     hipLaunchKernelGGL(ent_fallback_kernel, dim3(b.nframes), dim3(64), 0, s, b);
     HJD_HIP(hipGetLastError());
     constexpr size_t kStageBytes = sizeof(int16_t) * kWriteThreads * kStageStride;
@@ -1663,6 +2146,12 @@ int gdec_issue(hjd_gdec* g, void* const* d_outs, const int32_t* pitches, int16_t
     b.status = g->d_status;
     b.raw = g->d_raw;
     b.tiles = g->d_tiles;
+    if (g->spec) {
+        b.spec = g->d_spec;
+        b.cand = g->d_cand;
+        b.cmap = g->d_cmap;
+        b.spec_lead = spec_lead_bits();
+    }
     // the device buffers are reused: order this call after the previous one
     // (which may have been issued on another stream)
     if (g->pending) HJD_HIP(hipStreamWaitEvent(s, g->done, 0));
@@ -1822,6 +2311,16 @@ static int default_sub_bits(int max_frames)
 // config-5 stream (profiles/r02_stream_subbits.json): S = 8192 at 32-48
 // frames per batch x 8 slots gives 97-101 Gpx/s against 91-94 at S = 4096;
 // 16384 and 64-96-frame batches are slower.
+// Speculative sync (ent_spec/cand/sync_spec kernels) for latency decoders:
+// one or two frames per call, where the round-based sync's serial rounds are
+// the critical path and most of the GPU is idle.  HJD_SYNC_SPEC=0/1 overrides.
+static bool spec_sync_default(int max_frames)
+{
+    const char* e = getenv("HJD_SYNC_SPEC");
+    if (e) return atoi(e) != 0;
+    return max_frames <= 2;
+}
+
 static int stream_sub_bits(int max_frames)
 {
     const char* e = getenv("HJD_SUB_BITS");
@@ -1843,6 +2342,7 @@ int hjd_gdec_create(hjd_ctx* ctx, int max_frames, int64_t max_scan_bytes, int64_
     g->device = hjd_ctx_device(ctx);
     g->num_cu = hjd_internal::ctx_num_cu(ctx);
     g->caps = make_caps(max_frames, max_scan_bytes, max_blocks, sub_bits);
+    g->spec = spec_sync_default(max_frames);
     const int rc = gdec_alloc(g);
     if (rc) {
         hjd_gdec_destroy(g);
@@ -1865,7 +2365,7 @@ int hjd_gdec_destroy(hjd_gdec* g)
     if (g->h_stage) (void)hipHostFree(g->h_stage);
     if (g->h_status) (void)hipHostFree(g->h_status);
     void* dev[] = {g->d_blob, g->d_entries, g->d_stats, g->d_mids, g->d_stats1, g->d_wentries, g->d_linked, g->d_agg,
-                   g->d_status, g->d_coefs, g->d_raw, g->d_tiles};
+                   g->d_status, g->d_coefs, g->d_raw, g->d_tiles, g->d_spec, g->d_cand, g->d_cmap};
     for (void* p : dev)
         if (p) (void)hipFree(p);
     if (g->staged) (void)hipEventDestroy(g->staged);
@@ -1958,17 +2458,24 @@ int hjd_debug_entropy_syncstats(const uint8_t* data, size_t size, int sub_bits, 
     }
     for (int i = 0; i < nbins; ++i) hist[i] = 0;
     const uint32_t S = static_cast<uint32_t>(sub_bits);
+    // HJD_SYNC_PHASES=n: guesses (k*S, j, 0) for j < n; the first of them to
+    // meet the true decode counts (speculation over block-in-MCU positions)
+    const char* ph = getenv("HJD_SYNC_PHASES");
+    const uint32_t nph = std::max(1, std::min(ph ? atoi(ph) : 1, static_cast<int>(F.bpm)));
     for (uint32_t k = 1; static_cast<uint64_t>(k) * S < p.data_bits; ++k) {
-        uint64_t g = guess_entry(c, k * S);
         int bin = nbins - 1;
-        while (st_pos(g) < static_cast<uint64_t>(k) * S + static_cast<uint32_t>(max_bits) && st_seg(g) < F.nseg) {
-            const uint32_t q = st_pos(g);
-            if (truth[q] == (st_j(g) << 8 | st_z(g))) {
-                bin = std::min<int>(nbins - 1, static_cast<int>((q - k * S) / 64));
-                break;
+        for (uint32_t j0 = 0; j0 < nph; ++j0) {
+            uint64_t g = guess_entry(c, k * S);
+            g = pack_state(st_pos(g), j0, 0, st_seg(g));
+            while (st_pos(g) < static_cast<uint64_t>(k) * S + static_cast<uint32_t>(max_bits) && st_seg(g) < F.nseg) {
+                const uint32_t q = st_pos(g);
+                if (truth[q] == (st_j(g) << 8 | st_z(g))) {
+                    bin = std::min<int>(bin, static_cast<int>((q - k * S) / 64));
+                    break;
+                }
+                SubStats st = stats_identity();
+                g = run<false>(c, g, q + 1, st, nullptr);
             }
-            SubStats st = stats_identity();
-            g = run<false>(c, g, q + 1, st, nullptr);
         }
         hist[bin]++;
     }
@@ -2060,6 +2567,8 @@ int hjd_debug_entropy_emulate(const uint8_t* data, size_t size, int sub_bits, in
     hjd_gdec g;
     g.gpu = false;
     g.caps = make_caps(1, static_cast<int64_t>(size), std::max<int64_t>(capacity_blocks, 1), sub_bits);
+    const char* se = getenv("HJD_SYNC_SPEC");   // the emulation takes the round-based sync unless asked
+    g.spec = se && atoi(se) != 0;
     int rc = gdec_alloc(&g);
     if (rc) return rc;
     struct Free {
@@ -2085,6 +2594,16 @@ int hjd_debug_entropy_emulate(const uint8_t* data, size_t size, int sub_bits, in
     g.e_linked.assign(static_cast<size_t>(g.caps.max_wgs), 0);
     g.e_agg.assign(static_cast<size_t>(g.caps.max_wgs), stats_identity());
     g.e_status.assign(1, 0);
+    if (g.spec) {
+        const size_t n = static_cast<size_t>(g.caps.max_subs);
+        g.e_spec.assign(n * kMaxBpm, SpecRec());
+        g.e_cand.assign(n * kCandRow, CandRec());
+        g.e_cmap.assign(n * kSlotRow, static_cast<uint8_t>(kNoCand));
+        b.spec = g.e_spec.data();
+        b.cand = g.e_cand.data();
+        b.cmap = g.e_cmap.data();
+        b.spec_lead = spec_lead_bits();
+    }
     b.entries = g.e_entries.data();
     b.stats = g.e_stats.data();
     b.mids = g.e_mids.data();

@@ -1,0 +1,50 @@
+"""GPU: the speculative sync of latency decoders (ent_spec_kernel,
+ent_cand_kernel, ent_chain_kernel; DESIGN.md s10 "Single-image latency") on
+the device.  Decoders sized for one or two frames use it by default; here
+HJD_SYNC_SPEC=1 forces it on every decoder and stream, and every test of
+test_gpu_entropy.py runs again (imported below): coefficients equal the host
+decoder's, pixels the reference's and the oracle's, damaged files flagged.
+The lead-in sweep at small S drives the chain kernel's repair path."""
+import numpy as np
+import pytest
+
+import test_gpu_entropy as E
+from test_gpu_entropy import *  # noqa: F401,F403  (re-run the whole module with the speculative sync)
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _spec_sync(monkeypatch):
+    monkeypatch.setenv("HJD_SYNC_SPEC", "1")
+    yield
+
+
+@pytest.mark.parametrize("lead", [0, 256, 1024])
+@pytest.mark.parametrize("sub_bits", [64, 512])
+def test_lead_in_sweep_on_device(hjd, ctx, monkeypatch, lead, sub_bits):
+    monkeypatch.setenv("HJD_SPEC_LEAD", str(lead))
+    datas = [E._pil(1920, 1080, 90, 2, seed=61), E._pil(640, 480, 95, 0, seed=62, restart_marker_blocks=3),
+             E._pil(333, 77, 85, 1, seed=63)] + [d for _, d in E._golden_bytes()[:2]]
+    got, status = E._coefs_gpu(hjd, ctx, datas, sub_bits)
+    for d, g, s in zip(datas, got, status):
+        ref, _ = hjd.decode_coefs(d)
+        np.testing.assert_array_equal(g, ref)
+        assert s & ~1 == 0
+
+
+def test_single_image_default_is_speculative(hjd, ctx, monkeypatch):
+    """A one-frame decoder takes the speculative sync without the override."""
+    monkeypatch.delenv("HJD_SYNC_SPEC", raising=False)
+    import torch
+    d = E._pil(1920, 1080, 90, 2, seed=64)
+    info = hjd.parse(d)
+    out = torch.full((info.height, info.width), -1, dtype=torch.int32, device="cuda")
+    with hjd.GpuDecoder(ctx, 1, len(d), info.nblocks) as gd:
+        for _ in range(3):
+            gd.decode([d], [out])
+            assert gd.sync()[0] & ~1 == 0
+    ref, info = hjd.decode_coefs(d)
+    import oracle_py as O
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32),
+                                  O.decode_q16(ref, info.qt, info.width, info.height, info.sampling))

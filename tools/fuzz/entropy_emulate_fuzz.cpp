@@ -2,7 +2,8 @@
 // with AddressSanitizer + UBSan (tools/fuzz/run_entropy.sh): mutates JPEG
 // files (byte flips, 0xFF runs, truncation) and decodes every single-scan
 // mutant with hjd_debug_entropy_emulate -- the host build of the same
-// destuff, sync/link/repair and write code the gfx950 kernels run, over
+// destuff, sync/link/repair (round-based and speculative) and write code the
+// gfx950 kernels run, over
 // buffers laid out as on the device (each frame's bit string followed by its
 // kDataPad read-ahead bytes; the staging block is sized to the file).  The
 // output buffer is an exact-size heap block, so a write past the frame's
@@ -58,6 +59,11 @@ int main(int argc, char** argv)
             // exact-size output: the frame's blocks and nothing more
             int16_t* coefs = static_cast<int16_t*>(malloc(static_cast<size_t>(mi.nblocks) * 128));
             int32_t status = 0;
+            // every other mutant through the speculative sync (latency decoders),
+            // with a random lead-in of its spec runs
+            setenv("HJD_SYNC_SPEC", i % 2 ? "1" : "0", 1);
+            const char* leads[] = {"0", "100", "512", "1024"};
+            setenv("HJD_SPEC_LEAD", leads[rng() % 4], 1);
             const int rc = hjd_debug_entropy_emulate(buf, d.size(), subs[rng() % 8], coefs, mi.nblocks, &status);
             if (rc == HJD_OK) ++ok;
             else ++corrupt;
