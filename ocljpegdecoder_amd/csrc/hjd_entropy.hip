@@ -372,6 +372,7 @@ struct EntBatchDev {
     struct SpecRec* spec;        // [sub][kMaxBpm]
     struct CandRec* cand;        // [sub][kSlots]
     uint8_t* cmap;               // [sub][kSlotRow]
+    uint8_t* cslot;              // [sub] the verified chain's slot (ent_chain_kernel)
     uint32_t spec_lead;          // lead-in of the spec runs (bits)
 };
 
@@ -560,6 +561,41 @@ __host__ __device__ __forceinline__ void chain_repair(const RunCtx& c, const Ent
         cm[static_cast<uint64_t>(k) * kSlotRow + kRepairSlot] = static_cast<uint8_t>(kRepairSlot);
         e = r.y;
     }
+}
+
+// The verified chain's record of subsequence k: the speculative sync leaves it
+// in the chain's slot of k (cslot), the round-based sync in the sync arrays.
+// 16-B vector reads (a SubStats copy goes through scratch on the device).
+__host__ __device__ __forceinline__ SubStats stats_of(const u32x4& v)
+{
+    SubStats r;
+    memcpy(&r, &v, sizeof(r));
+    return r;
+}
+__host__ __device__ __forceinline__ const u32x4* sub_rec(const EntBatchDev& b, const EntFrame& F, uint32_t k)
+{
+    const uint64_t row = static_cast<uint64_t>(F.sub_base) + k;
+    return reinterpret_cast<const u32x4*>(b.cand + row * kCandRow + b.cslot[row]);
+}
+__host__ __device__ __forceinline__ SubStats sub_stats(const EntBatchDev& b, const EntFrame& F, uint32_t k)
+{
+    return b.spec ? stats_of(sub_rec(b, F, k)[1]) : b.stats[F.sub_base + k];
+}
+__host__ __device__ __forceinline__ SubStats sub_stats1(const EntBatchDev& b, const EntFrame& F, uint32_t k)
+{
+    return b.spec ? stats_of(sub_rec(b, F, k)[0]) : b.stats1[F.sub_base + k];
+}
+__host__ __device__ __forceinline__ uint64_t sub_entry(const EntBatchDev& b, const EntFrame& F, uint32_t k)
+{
+    if (!b.spec) return b.entries[F.sub_base + k];
+    const u32x4 v = sub_rec(b, F, k)[2];
+    return static_cast<uint64_t>(v.x) | static_cast<uint64_t>(v.y) << 32;
+}
+__host__ __device__ __forceinline__ uint64_t sub_mid(const EntBatchDev& b, const EntFrame& F, uint32_t k)
+{
+    if (!b.spec) return b.mids[F.sub_base + k];
+    const u32x4 v = sub_rec(b, F, k)[2];
+    return static_cast<uint64_t>(v.z) | static_cast<uint64_t>(v.w) << 32;
 }
 
 // ---------------------------------------------------------------------------
@@ -813,8 +849,13 @@ __global__ __launch_bounds__(kGroupSubs) void ent_spec_kernel(EntBatchDev b)
     const int64_t k = group_sub(gl, tid);
     if (tid < kWarm || k >= static_cast<int64_t>(F.nsub)) return;
     const RunCtx c = make_ctx(b, F, tabs, blocks, steps);
-    const uint64_t idx = (static_cast<uint64_t>(F.sub_base) + static_cast<uint64_t>(k)) * kMaxBpm + j;
-    b.spec[idx] = spec_run(c, static_cast<uint32_t>(k), j, b.sub_bits, b.spec_lead);
+    const uint64_t row = static_cast<uint64_t>(F.sub_base) + static_cast<uint64_t>(k);
+    if (j == 0) {   // the subsequence's slot map starts empty (ent_cand_kernel fills what exists)
+        uint32_t* m = reinterpret_cast<uint32_t*>(b.cmap + row * kSlotRow);
+#pragma unroll
+        for (int i = 0; i < kSlotRow / 4; ++i) m[i] = 0xFFFFFFFFu;
+    }
+    b.spec[row * kMaxBpm + j] = spec_run(c, static_cast<uint32_t>(k), j, b.sub_bits, b.spec_lead);
 }
 
 // Grid (groups, kMaxBpm): block (w, i) runs candidate i of group w's owned
@@ -849,40 +890,87 @@ __global__ __launch_bounds__(kGroupSubs) void ent_cand_kernel(EntBatchDev b)
 // the chain leaves every slot (an exit that is none of the successor's
 // candidates even after the overflow levels; rare), thread 0 re-runs it from
 // the known exit in the repair slot of the following subsequences until it
-// lands in a slot again, and the chunk is scanned anew.  Each thread then
-// copies its rows' records into the sync outputs; last, one wave per group
-// reduces the group's statistics (agg) and writes its warm-up entries.
+// lands in a slot again, and the chunk is scanned anew.  The output is the
+// chain's slot of every subsequence (cslot): the write kernel reads each
+// subsequence's entry, statistics and mid-state from that slot's record.  Last,
+// one wave per group reduces the group's statistics (agg).
+// Maps and functions are rows of kSlotRow bytes handled as 5 dwords; a lookup
+// selects its byte in registers (LDS byte reads cost ~5x more here).
 constexpr int kChainThreads = 512;
-
 constexpr int kChainRows = 8;                                  // rows per thread and chunk
 constexpr int kChainChunk = kChainThreads * kChainRows;        // 4096 subsequences
+constexpr int kRowWords = kSlotRow / 4;
 
 struct ChainLds {
-    uint8_t rows[kChainChunk][kSlotRow];        // the chunk's slot maps
-    uint8_t fn[2][kChainThreads][kSlotRow];     // scan of the threads' functions (double buffer)
+    uint32_t rows[kChainChunk][kRowWords];      // the chunk's slot maps
+    uint32_t fn[2][kChainThreads][kRowWords];   // scan of the threads' functions (double buffer)
     unsigned long long brk;                     // first break: subsequence << 8 | its predecessor's slot
     uint32_t carry;                             // slot entering the chunk
-    HuffLut tabs[kMaxTables];                   // the frame's tables (repairs)
+    uint32_t tables_loaded;
+    HuffLut tabs[kMaxTables];                   // the frame's tables (repairs only)
     uint8_t steps[kMaxTables << kStepBits];
     BlockInfo blocks[kMaxBpm];
 };
 
+struct SlotRow {
+    uint32_t w[kRowWords];
+};
+
+__device__ __forceinline__ uint32_t row_get(const SlotRow& r, uint32_t a)   // a < kChainSlots
+{
+    const uint32_t x = a < 8 ? (a < 4 ? r.w[0] : r.w[1]) : a < 16 ? (a < 12 ? r.w[2] : r.w[3]) : r.w[4];
+    return (x >> ((a & 3) * 8)) & 0xFFu;
+}
+
+__device__ __forceinline__ SlotRow row_load(const uint32_t* p)
+{
+    SlotRow r;
+#pragma unroll
+    for (int i = 0; i < kRowWords; ++i) r.w[i] = p[i];
+    return r;
+}
+
+// f then g: (g . f)(s) = g(f(s)), kNoCand absorbing; bytes past kChainSlots stay kNoCand
+__device__ __forceinline__ SlotRow row_compose(const SlotRow& f, const SlotRow& g)
+{
+    SlotRow r;
+#pragma unroll
+    for (int i = 0; i < kRowWords; ++i) r.w[i] = 0xFFFFFFFFu;
+#pragma unroll
+    for (int s = 0; s < kChainSlots; ++s) {
+        const uint32_t a = row_get(f, static_cast<uint32_t>(s));
+        const uint32_t v = a == kNoCand ? kNoCand : row_get(g, a);
+        r.w[s >> 2] = (r.w[s >> 2] & ~(0xFFu << ((s & 3) * 8))) | (v << ((s & 3) * 8));
+    }
+    return r;
+}
+
 __global__ __launch_bounds__(kChainThreads) void ent_chain_kernel(EntBatchDev b)
 {
     __shared__ ChainLds L;
-    HuffLut* tabs = L.tabs;
-    uint8_t* steps = L.steps;
-    BlockInfo* blocks = L.blocks;
+#ifdef HJD_CHAIN_PROFILE   // tuning build: phase timestamps (100 MHz) printed by block 0
+    uint64_t tp[48];
+    int np = 0;
+#define CHAIN_T() do { if (threadIdx.x == 0 && blockIdx.x == 0 && np < 48) tp[np++] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define CHAIN_T() do {} while (0)
+#endif
+    CHAIN_T();
     const int tid = threadIdx.x;
     const uint32_t f = blockIdx.x;
     const EntFrame F = b.frames[f];
     const uint32_t n = F.nsub;
     uint8_t* cm = b.cmap + static_cast<uint64_t>(F.sub_base) * kSlotRow;
-    load_tables(tabs, blocks, b.tabs + F.tab_base, F, b.frames + f, tid, kChainThreads);
-    if (tid == 0) L.carry = 0;
-    __syncthreads();
-    fill_steps(steps, tabs, F.ntab, tid, kChainThreads);
-    const RunCtx c = make_ctx(b, F, tabs, blocks, steps);
+    if (tid == 0) {
+        L.carry = 0;
+        L.tables_loaded = 0;
+    }
+    SlotRow ident;
+#pragma unroll
+    for (int i = 0; i < kRowWords; ++i) ident.w[i] = 0xFFFFFFFFu;
+#pragma unroll
+    for (int s = 0; s < kChainSlots; ++s)
+        ident.w[s >> 2] = (ident.w[s >> 2] & ~(0xFFu << ((s & 3) * 8))) | (static_cast<uint32_t>(s) << ((s & 3) * 8));
     for (uint32_t c0 = 0; c0 < n; c0 += kChainChunk) {
         const uint32_t cn = n - c0 < static_cast<uint32_t>(kChainChunk) ? n - c0 : kChainChunk;
         const uint32_t r0 = static_cast<uint32_t>(tid) * kChainRows;   // this thread's rows within the chunk
@@ -890,50 +978,47 @@ __global__ __launch_bounds__(kChainThreads) void ent_chain_kernel(EntBatchDev b)
         for (;;) {
             __syncthreads();
             {   // the chunk's rows, 4-byte words, coalesced; all of a thread's loads in flight at once
-                constexpr int kWords = kChainChunk * (kSlotRow / 4) / kChainThreads;   // 40
+                constexpr int kWords = kChainChunk * kRowWords / kChainThreads;   // 40
                 const uint32_t* src = reinterpret_cast<const uint32_t*>(cm + static_cast<uint64_t>(c0) * kSlotRow);
-                uint32_t* dst = reinterpret_cast<uint32_t*>(&L.rows[0][0]);
-                const uint32_t nw = cn * (kSlotRow / 4);
+                uint32_t* dst = &L.rows[0][0];
+                const uint32_t nw = cn * kRowWords;
                 uint32_t t[kWords];
 #pragma unroll
                 for (int i = 0; i < kWords; ++i) {
                     const uint32_t j = static_cast<uint32_t>(tid + i * kChainThreads);
-                    t[i] = j < nw ? src[j] : 0u;
+                    t[i] = j < nw ? src[j] : 0xFFFFFFFFu;
                 }
 #pragma unroll
                 for (int i = 0; i < kWords; ++i) dst[tid + i * kChainThreads] = t[i];
             }
             if (tid == 0) L.brk = ~0ull;
             __syncthreads();
-            uint32_t v[kChainSlots];
-#pragma unroll
-            for (int s = 0; s < kChainSlots; ++s) v[s] = static_cast<uint32_t>(s);
+            CHAIN_T();
+            SlotRow v = ident;
 #pragma unroll 1
-            for (uint32_t r = r0; r < r0 + kChainRows && r < cn; ++r) {
+            for (uint32_t r = r0; r < r0 + kChainRows && r < cn; ++r) v = row_compose(v, row_load(L.rows[r]));
 #pragma unroll
-                for (int s = 0; s < kChainSlots; ++s) v[s] = v[s] == kNoCand ? kNoCand : L.rows[r][v[s]];
-            }
-#pragma unroll
-            for (int s = 0; s < kChainSlots; ++s) L.fn[0][tid][s] = static_cast<uint8_t>(v[s]);
+            for (int i = 0; i < kRowWords; ++i) L.fn[0][tid][i] = v.w[i];
             __syncthreads();
+            CHAIN_T();
             int cur = 0;
 #pragma unroll 1
             for (int d = 1; d < kChainThreads; d <<= 1) {   // inclusive: fn[t] = thread 0's rows then ... then t's
+                const SlotRow mine = row_load(L.fn[cur][tid]);
+                const SlotRow o = tid >= d ? row_compose(row_load(L.fn[cur][tid - d]), mine) : mine;
 #pragma unroll
-                for (int s = 0; s < kChainSlots; ++s) {
-                    const uint8_t a = tid >= d ? L.fn[cur][tid - d][s] : static_cast<uint8_t>(s);
-                    L.fn[cur ^ 1][tid][s] = a == kNoCand ? static_cast<uint8_t>(kNoCand) : L.fn[cur][tid][a];
-                }
+                for (int i = 0; i < kRowWords; ++i) L.fn[cur ^ 1][tid][i] = o.w[i];
                 cur ^= 1;
                 __syncthreads();
             }
+            CHAIN_T();
             const uint32_t carry = L.carry;
-            slot = tid == 0 ? carry : (carry == kNoCand ? kNoCand : L.fn[cur][tid - 1][carry]);
+            slot = tid == 0 ? carry : (carry == kNoCand ? kNoCand : row_get(row_load(L.fn[cur][tid - 1]), carry));
             // the first subsequence without a slot: the row whose map sends the
             // chain's slot to none (subsequence 0's slots all exist)
             uint32_t s = slot;
             for (uint32_t r = r0; r < r0 + kChainRows && r < cn && s != kNoCand; ++r) {
-                const uint32_t nx = L.rows[r][s];
+                const uint32_t nx = row_get(row_load(L.rows[r]), s);
                 if (nx == kNoCand && c0 + r + 1 < n) {
                     atomicMin(&L.brk, (static_cast<unsigned long long>(c0 + r + 1) << 8) | s);
                     break;
@@ -941,44 +1026,37 @@ __global__ __launch_bounds__(kChainThreads) void ent_chain_kernel(EntBatchDev b)
                 s = nx;
             }
             __syncthreads();
+            CHAIN_T();
             const unsigned long long brk = L.brk;
             if (brk == ~0ull) break;
-            if (tid == 0) chain_repair(c, b, F, static_cast<uint32_t>(brk >> 8), static_cast<uint32_t>(brk & 0xFF));
+            if (!L.tables_loaded) {   // the frame's tables, for the repair runs (rare)
+                load_tables(L.tabs, L.blocks, b.tabs + F.tab_base, F, b.frames + f, tid, kChainThreads);
+                __syncthreads();
+                fill_steps(L.steps, L.tabs, F.ntab, tid, kChainThreads);
+                __syncthreads();
+                if (tid == 0) L.tables_loaded = 1;
+            }
+            if (tid == 0)
+                chain_repair(make_ctx(b, F, L.tabs, L.blocks, L.steps), b, F, static_cast<uint32_t>(brk >> 8),
+                             static_cast<uint32_t>(brk & 0xFF));
         }
-        // copy the records of this thread's rows: the slots first (LDS), then
-        // the loads of four records at a time in flight (16-B vector copies: a
-        // SubStats copy goes through scratch)
-        uint32_t s = slot, sl[kChainRows];
+        // the chain's slot of each of this thread's rows
+        uint32_t s = slot;
+        uint32_t packed[kChainRows / 4] = {};
 #pragma unroll
         for (int i = 0; i < kChainRows; ++i) {
-            sl[i] = s;
-            if (r0 + i < cn) s = L.rows[r0 + i][s];
+            packed[i >> 2] |= (s & 0xFFu) << ((i & 3) * 8);
+            if (r0 + i < cn) s = row_get(row_load(L.rows[r0 + i]), s);
         }
+        uint8_t* out = b.cslot + F.sub_base + c0 + r0;
+        if (r0 + kChainRows <= cn && ((F.sub_base + c0 + r0) & 3) == 0) {
 #pragma unroll
-        for (int h = 0; h < kChainRows; h += 4) {
-            u32x4 q[4][3];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const uint64_t row = static_cast<uint64_t>(F.sub_base) + c0 + r0 + h + i;
-                if (r0 + h + i < cn) {
-                    const u32x4* rec = reinterpret_cast<const u32x4*>(b.cand + row * kCandRow + sl[h + i]);
-                    q[i][0] = rec[0];
-                    q[i][1] = rec[1];
-                    q[i][2] = rec[2];
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const uint64_t row = static_cast<uint64_t>(F.sub_base) + c0 + r0 + h + i;
-                if (r0 + h + i < cn) {
-                    reinterpret_cast<u32x4*>(b.stats1)[row] = q[i][0];
-                    reinterpret_cast<u32x4*>(b.stats)[row] = q[i][1];
-                    b.entries[row] = static_cast<uint64_t>(q[i][2].x) | static_cast<uint64_t>(q[i][2].y) << 32;
-                    b.mids[row] = static_cast<uint64_t>(q[i][2].z) | static_cast<uint64_t>(q[i][2].w) << 32;
-                }
-            }
+            for (int i = 0; i < kChainRows / 4; ++i) reinterpret_cast<uint32_t*>(out)[i] = packed[i];
+        } else {
+            for (uint32_t i = 0; i < kChainRows && r0 + i < cn; ++i) out[i] = static_cast<uint8_t>(packed[i >> 2] >> ((i & 3) * 8));
         }
         __syncthreads();
+        CHAIN_T();
         if (r0 < cn && (r0 + kChainRows >= cn)) L.carry = s;   // the thread holding the chunk's last row
     }
     __syncthreads();
@@ -987,13 +1065,13 @@ __global__ __launch_bounds__(kChainThreads) void ent_chain_kernel(EntBatchDev b)
     for (uint32_t g = wv; g < frame_groups(n); g += kChainThreads / 64) {
         const uint32_t w = F.wg_base + g;
         const uint32_t end = (g + 1) * kOwn < n ? (g + 1) * kOwn : n;
-        SubStats a = stats_identity();
         SubStats q[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {   // 4 x 64 >= kOwn; the four loads in flight together
             const uint32_t k = g * kOwn + lane * 4 + i;
-            q[i] = k < end ? b.stats[F.sub_base + k] : stats_identity();
+            q[i] = k < end ? sub_stats(b, F, k) : stats_identity();
         }
+        SubStats a = stats_identity();
 #pragma unroll
         for (int i = 0; i < 4; ++i) a = stats_combine(a, q[i]);
         a = wave_reduce_ordered(a, lane);
@@ -1001,12 +1079,18 @@ __global__ __launch_bounds__(kChainThreads) void ent_chain_kernel(EntBatchDev b)
             b.agg[w] = a;
             b.linked[w] = 1u;
         }
-        if (lane < kWarm) {
-            const int64_t k = group_sub(g, lane);
-            b.wentries[static_cast<uint64_t>(w) * kWarm + lane] = k >= 0 ? b.entries[F.sub_base + k] : 0;
-        }
     }
+#ifdef HJD_CHAIN_PROFILE
+    __syncthreads();
+    CHAIN_T();
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        printf("chain n=%u:", n);
+        for (int i = 1; i < np; ++i) printf(" %d", static_cast<int>(tp[i] - tp[i - 1]));
+        printf("\n");
+    }
+#endif
 }
+#undef CHAIN_T
 
 __global__ __launch_bounds__(256) void ent_link_kernel(EntBatchDev b)
 {
@@ -1130,16 +1214,16 @@ __global__ __launch_bounds__(kWriteThreads) void ent_write_kernel(EntBatchDev b)
     const bool own = t >= kWarm && k < static_cast<int64_t>(F.nsub);
     const uint32_t ku = static_cast<uint32_t>(k);
     // subsequence prefixes (the upper 256 entries are identities and do not disturb them)
-    const SubStats mine = own && !second ? b.stats[F.sub_base + ku] : stats_identity();
+    const SubStats mine = own && !second ? sub_stats(b, F, ku) : stats_identity();
     block_scan_inclusive<kWriteThreads>(mine, buf, tid);
     SubStats excl = stats_combine(pre, t > 0 ? buf[t - 1] : stats_identity());
     __syncthreads();   // scratch reads done before blocks are staged
     if (!own) return;
-    uint64_t entry = b.entries[F.sub_base + ku];
+    uint64_t entry = sub_entry(b, F, ku);
     uint32_t stop = ku * S + S / 2;
     if (second) {
-        excl = stats_combine(excl, b.stats1[F.sub_base + ku]);
-        entry = b.mids[F.sub_base + ku];
+        excl = stats_combine(excl, sub_stats1(b, F, ku));
+        entry = sub_mid(b, F, ku);
         stop = (ku + 1) * S;
     }
     const RunCtx c = make_ctx(b, F, tabs, blocks);
@@ -1528,6 +1612,7 @@ void emulate_spec_sync(const EntBatchDev& b)
                 ++nrepair;
             }
             const CandRec& r = b.cand[row * kCandRow + slot];
+            b.cslot[row] = static_cast<uint8_t>(slot);
             b.entries[row] = r.e;
             b.stats[row] = r.s;
             b.mids[row] = r.mid;
@@ -1677,7 +1762,7 @@ void emulate(const EntBatchDev& b)
         SubStats pre = stats_identity();
         for (uint32_t i = 0; i < F.nsub; ++i) {
             for (int half = 0; half < 2; ++half) {   // as ent_write_kernel: entry -> mid, mid -> end
-                const SubStats p = half ? stats_combine(pre, b.stats1[F.sub_base + i]) : pre;
+                const SubStats p = half ? stats_combine(pre, sub_stats1(b, F, i)) : pre;
                 RunOut o;
                 o.coefs = b.coefs + F.coef_off * 64;
                 o.stage = stage;
@@ -1687,12 +1772,12 @@ void emulate(const EntBatchDev& b)
                 o.pred[1] = p.dc[1];
                 o.pred[2] = p.dc[2];
                 SubStats s = stats_identity();
-                run<true>(c, half ? b.mids[F.sub_base + i] : b.entries[F.sub_base + i],
+                run<true>(c, half ? sub_mid(b, F, i) : sub_entry(b, F, i),
                           half ? (i + 1) * S : i * S + S / 2, s, &o);
                 if (s.flags & kError) b.status[f] |= kStatusCorrupt;
                 if (half && i == F.nsub - 1 && p.nblk + s.nblk != F.nblocks) b.status[f] |= kStatusCount;
             }
-            pre = stats_combine(pre, b.stats[F.sub_base + i]);
+            pre = stats_combine(pre, sub_stats(b, F, i));
         }
     }
 }
@@ -1733,6 +1818,7 @@ struct hjd_gdec {
     SpecRec* d_spec = nullptr;          // [max_subs][kMaxBpm]
     CandRec* d_cand = nullptr;
     uint8_t* d_cmap = nullptr;
+    uint8_t* d_cslot = nullptr;
     hipEvent_t staged = nullptr, done = nullptr;
     int64_t last_h2d = 0;               // bytes the last issue moved host -> device
     int64_t last_host_scan_bytes = 0;   // scan bytes the host CPU read + wrote for the staged frames
@@ -1749,7 +1835,7 @@ struct hjd_gdec {
     std::vector<uint32_t> e_status;
     std::vector<SpecRec> e_spec;
     std::vector<CandRec> e_cand;
-    std::vector<uint8_t> e_cmap;
+    std::vector<uint8_t> e_cmap, e_cslot;
 
     uint8_t* data_area() { return h_stage + caps.data; }
     size_t data_cap() const { return static_cast<size_t>(caps.max_scan_bytes) + kDataPad * caps.max_frames +
@@ -2010,6 +2096,7 @@ int hjd_gdec::assemble(uint8_t* blob, int16_t* coefs, int64_t* block_offsets, vo
     d.spec = nullptr;
     d.cand = nullptr;
     d.cmap = nullptr;
+    d.cslot = nullptr;
     d.spec_lead = 0;
     d.nsub_total = sub_base;
     d.rawf = nullptr;
@@ -2076,6 +2163,7 @@ int gdec_alloc(hjd_gdec* g)
         HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_spec), sizeof(SpecRec) * kMaxBpm * n));
         HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_cand), sizeof(CandRec) * kCandRow * n));
         HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_cmap), kSlotRow * n));
+        HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_cslot), n + 16));
     }
     HJD_HIP(hipEventCreateWithFlags(&g->staged, hipEventDisableTiming));
     HJD_HIP(hipEventCreateWithFlags(&g->done, hipEventDisableTiming));
@@ -2097,7 +2185,6 @@ int launch_entropy(hjd_gdec* g, const EntBatchDev& b, hipStream_t s)
     }
     if (b.spec) {   // speculative sync: latency decoders
         const size_t tl = (sizeof(HuffLut) + (1u << kStepBits)) * b.ntab_max;
-        HJD_HIP(hipMemsetAsync(b.cmap, 0xFF, static_cast<size_t>(b.nsub_total) * kSlotRow, s));
         hipLaunchKernelGGL(ent_spec_kernel, dim3(b.nwg, kMaxBpm), dim3(kGroupSubs), tl, s, b);
         HJD_HIP(hipGetLastError());
         hipLaunchKernelGGL(ent_cand_kernel, dim3(b.nwg, kMaxBpm), dim3(kGroupSubs), tl, s, b);
@@ -2110,8 +2197,10 @@ int launch_entropy(hjd_gdec* g, const EntBatchDev& b, hipStream_t s)
         hipLaunchKernelGGL(ent_link_kernel, dim3((b.nwg + 255) / 256), dim3(256), 0, s, b);
         HJD_HIP(hipGetLastError());
     }
-    hipLaunchKernelGGL(ent_fallback_kernel, dim3(b.nframes), dim3(64), 0, s, b);
-    HJD_HIP(hipGetLastError());
+    if (!b.spec) {   // the chain kernel repairs its chains itself: never a fallback
+        hipLaunchKernelGGL(ent_fallback_kernel, dim3(b.nframes), dim3(64), 0, s, b);
+        HJD_HIP(hipGetLastError());
+    }
     constexpr size_t kStageBytes = sizeof(int16_t) * kWriteThreads * kStageStride;
     hipLaunchKernelGGL(ent_write_kernel, dim3(b.nwg), dim3(kWriteThreads), kStageBytes + sizeof(HuffLut) * b.ntab_max,
                        s, b);
@@ -2150,6 +2239,7 @@ int gdec_issue(hjd_gdec* g, void* const* d_outs, const int32_t* pitches, int16_t
         b.spec = g->d_spec;
         b.cand = g->d_cand;
         b.cmap = g->d_cmap;
+        b.cslot = g->d_cslot;
         b.spec_lead = spec_lead_bits();
     }
     // the device buffers are reused: order this call after the previous one
@@ -2333,7 +2423,12 @@ int hjd_gdec_create(hjd_ctx* ctx, int max_frames, int64_t max_scan_bytes, int64_
 {
     if (!ctx || !out || max_frames <= 0 || max_scan_bytes <= 0 || max_blocks <= 0)
         return set_error(HJD_E_INVALID, "invalid gdec arguments");
-    if (sub_bits == 0) sub_bits = default_sub_bits(max_frames);
+    const bool spec = spec_sync_default(max_frames);
+    // the speculative sync's critical path is a few runs of S (+ the lead-in)
+    // bits, no longer ~7 serial rounds: shorter subsequences pay there.  One
+    // FHD q90 JPEG end to end (profiles/r03_fhd420_jpeg_spec_sweep.json):
+    // 0.65 ms at S = 512 / lead-in 512, 0.71 at 1024, 0.69-0.76 at 768.
+    if (sub_bits == 0) sub_bits = spec && !getenv("HJD_SUB_BITS") ? kDefaultSubBits / 4 : default_sub_bits(max_frames);
     if (sub_bits < 32 || sub_bits > (1 << 20)) return set_error(HJD_E_INVALID, "sub_bits out of range [32, 2^20]");
     *out = nullptr;
     hjd_gdec* g = new (std::nothrow) hjd_gdec;
@@ -2342,7 +2437,7 @@ int hjd_gdec_create(hjd_ctx* ctx, int max_frames, int64_t max_scan_bytes, int64_
     g->device = hjd_ctx_device(ctx);
     g->num_cu = hjd_internal::ctx_num_cu(ctx);
     g->caps = make_caps(max_frames, max_scan_bytes, max_blocks, sub_bits);
-    g->spec = spec_sync_default(max_frames);
+    g->spec = spec;
     const int rc = gdec_alloc(g);
     if (rc) {
         hjd_gdec_destroy(g);
@@ -2365,7 +2460,7 @@ int hjd_gdec_destroy(hjd_gdec* g)
     if (g->h_stage) (void)hipHostFree(g->h_stage);
     if (g->h_status) (void)hipHostFree(g->h_status);
     void* dev[] = {g->d_blob, g->d_entries, g->d_stats, g->d_mids, g->d_stats1, g->d_wentries, g->d_linked, g->d_agg,
-                   g->d_status, g->d_coefs, g->d_raw, g->d_tiles, g->d_spec, g->d_cand, g->d_cmap};
+                   g->d_status, g->d_coefs, g->d_raw, g->d_tiles, g->d_spec, g->d_cand, g->d_cmap, g->d_cslot};
     for (void* p : dev)
         if (p) (void)hipFree(p);
     if (g->staged) (void)hipEventDestroy(g->staged);
@@ -2462,19 +2557,27 @@ int hjd_debug_entropy_syncstats(const uint8_t* data, size_t size, int sub_bits, 
     // meet the true decode counts (speculation over block-in-MCU positions)
     const char* ph = getenv("HJD_SYNC_PHASES");
     const uint32_t nph = std::max(1, std::min(ph ? atoi(ph) : 1, static_cast<int>(F.bpm)));
+    // HJD_SYNC_OFFSETS=m: also guesses m-1 bit positions before k*S (offsets
+    // 7, 19, 37, 61, ... bits), each with the n phases
+    const char* os = getenv("HJD_SYNC_OFFSETS");
+    const uint32_t noff = std::max(1, os ? atoi(os) : 1);
+    static const uint32_t kOffs[] = {0, 7, 19, 37, 61, 91, 127, 169, 217, 271, 331, 397};
     for (uint32_t k = 1; static_cast<uint64_t>(k) * S < p.data_bits; ++k) {
         int bin = nbins - 1;
-        for (uint32_t j0 = 0; j0 < nph; ++j0) {
-            uint64_t g = guess_entry(c, k * S);
-            g = pack_state(st_pos(g), j0, 0, st_seg(g));
-            while (st_pos(g) < static_cast<uint64_t>(k) * S + static_cast<uint32_t>(max_bits) && st_seg(g) < F.nseg) {
-                const uint32_t q = st_pos(g);
-                if (truth[q] == (st_j(g) << 8 | st_z(g))) {
-                    bin = std::min<int>(bin, static_cast<int>((q - k * S) / 64));
-                    break;
+        for (uint32_t oi = 0; oi < std::min<uint32_t>(noff, 12); ++oi) {
+            if (kOffs[oi] > k * S) continue;
+            for (uint32_t j0 = 0; j0 < nph; ++j0) {
+                uint64_t g = guess_entry(c, k * S - kOffs[oi]);
+                g = pack_state(st_pos(g), j0, 0, st_seg(g));
+                while (st_pos(g) < static_cast<uint64_t>(k) * S + static_cast<uint32_t>(max_bits) && st_seg(g) < F.nseg) {
+                    const uint32_t q = st_pos(g);
+                    if (truth[q] == (st_j(g) << 8 | st_z(g))) {
+                        bin = std::min<int>(bin, q > k * S ? static_cast<int>((q - k * S) / 64) : 0);
+                        break;
+                    }
+                    SubStats st = stats_identity();
+                    g = run<false>(c, g, q + 1, st, nullptr);
                 }
-                SubStats st = stats_identity();
-                g = run<false>(c, g, q + 1, st, nullptr);
             }
         }
         hist[bin]++;
@@ -2602,6 +2705,8 @@ int hjd_debug_entropy_emulate(const uint8_t* data, size_t size, int sub_bits, in
         b.spec = g.e_spec.data();
         b.cand = g.e_cand.data();
         b.cmap = g.e_cmap.data();
+        g.e_cslot.assign(n + 16, 0);
+        b.cslot = g.e_cslot.data();
         b.spec_lead = spec_lead_bits();
     }
     b.entries = g.e_entries.data();
