@@ -185,6 +185,9 @@ constexpr int kVarWgInterleave = 2;
 // Ablation bits: compiled into the tuning-only library (HJD_ABLATION, see
 // tools/build_native.py --ablation); their outputs are deliberately wrong.
 constexpr int kAblNoStore = 4, kAblNoColour = 8, kAblNoIdct = 16;
+// kAblNoCsc: the colour stage keeps its LDS reads and stores but skips the
+// chroma terms and pixel math (stores raw sample words).
+constexpr int kAblNoCsc = 64;
 // Output format bit (include/hjd.h HJD_OUT_BGR24): 3-byte B,G,R pixels
 // instead of 4-byte BGRX words.
 constexpr int kOutBgr24 = 32;
@@ -305,11 +308,16 @@ __device__ __forceinline__ void colour_stage(const char* __restrict__ slots, int
             const int coff = p * 16 + (xm >> 1) * 2;
             const uint32_t cu = *reinterpret_cast<const uint32_t*>(slots + (m * 6 + 4) * kSlotBytes + coff);
             const uint32_t cv = *reinterpret_cast<const uint32_t*>(slots + (m * 6 + 5) * kSlotBytes + coff);
+            uint8_t* row0 = strip + static_cast<int64_t>(4 * it) * pitch;   // wave-uniform
+            if constexpr ((kVariant & kAblNoCsc) != 0) {
+                store4<kFull, kVariant>(row0, loff, xa, width, ya.x, ya.y, cu, cv);
+                store4<kFull, kVariant>(row0 + pitch, loff, xa, width, yb.x, yb.y, cu, cv);
+                continue;
+            }
             const ChromaTerms c0 = chroma_terms<0>(cu, cv);
             const ChromaTerms c1 = chroma_terms<1>(cu, cv);
             const ChromaPair p0 = pair_of(c0, c0), p1 = pair_of(c1, c1);
             const int ya0 = y_base + y0;
-            uint8_t* row0 = strip + static_cast<int64_t>(4 * it) * pitch;   // wave-uniform
             if (__builtin_amdgcn_ballot_w64((p0.flagged | p1.flagged) != 0)) {   // wave-uniform, rare
                 if (kFull || ya0 < height)
                     emit_row4<true, kVariant, kFull>(row0, loff, xa, width, ya.x, ya.y, p0, p1, &c0, &c0, &c1, &c1);
@@ -339,6 +347,11 @@ __device__ __forceinline__ void colour_stage(const char* __restrict__ slots, int
                 const int2 sy = *reinterpret_cast<const int2*>(base);
                 const uint2 su = *reinterpret_cast<const uint2*>(base + kSlotBytes);
                 const uint2 sv = *reinterpret_cast<const uint2*>(base + 2 * kSlotBytes);
+                if constexpr ((kVariant & kAblNoCsc) != 0) {
+                    store4<kFull, kVariant>(strip + static_cast<int64_t>(4 * it + h) * pitch, loff, xa, width, sy.x,
+                                            sy.y, su.x ^ sv.x, su.y ^ sv.y);
+                    continue;
+                }
                 const ChromaTerms c0 = chroma_terms<0>(su.x, sv.x);
                 const ChromaTerms c1 = chroma_terms<1>(su.x, sv.x);
                 const ChromaTerms c2 = chroma_terms<0>(su.y, sv.y);

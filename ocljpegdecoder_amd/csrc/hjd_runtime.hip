@@ -187,6 +187,8 @@ int hjd_internal::launch_decode(int device, int num_cu, int sampling, int input_
         case 16: k = s420 ? hjd::decode_kernel<1, 0, 16> : hjd::decode_kernel<0, 0, 16>; break;
         case 20: k = s420 ? hjd::decode_kernel<1, 0, 20> : hjd::decode_kernel<0, 0, 20>; break;
         case 24: k = s420 ? hjd::decode_kernel<1, 0, 24> : hjd::decode_kernel<0, 0, 24>; break;
+        case 64: k = s420 ? hjd::decode_kernel<1, 0, 64> : hjd::decode_kernel<0, 0, 64>; break;
+        case 80: k = s420 ? hjd::decode_kernel<1, 0, 80> : hjd::decode_kernel<0, 0, 80>; break;
         default: return hjd_internal::set_error(HJD_E_INVALID, "unknown ablation variant %d", variant);
         }
         hipLaunchKernelGGL(k, dim3(grid), dim3(hjd::kGroupThreads), 0, static_cast<hipStream_t>(stream), d_coefs,
@@ -381,7 +383,7 @@ int hjd_plan_set_variant(hjd_plan* plan, int variant)
 {
     if (!plan) return fail(HJD_E_INVALID, "plan is NULL");
 #ifdef HJD_ABLATION
-    if (variant < 0 || variant > 31) return fail(HJD_E_INVALID, "unknown kernel variant %d", variant);
+    if (variant < 0 || variant > 127) return fail(HJD_E_INVALID, "unknown kernel variant %d", variant);
 #else
     if (variant < 0 || variant > 3) return fail(HJD_E_INVALID, "unknown kernel variant %d", variant);
 #endif
