@@ -3,8 +3,9 @@
  * GPU 0.  The Huffman decode runs on the GPU (hjd_gdec, include/hjd_host.h),
  * then the fused dequant + IDCT + colour kernel writes BGRX into device
  * memory, which is copied back and written as the reference program's 32-bpp
- * BMP (src/decoder.cpp:372-395).  Files the GPU entropy decoder does not take
- * (progressive, multi-scan) go through the host Huffman decoder and a plan.
+ * BMP (src/decoder.cpp:372-395).  Sequential files, with one scan or several,
+ * take the GPU entropy decoder; progressive files, which it does not take, go
+ * through the host Huffman decoder and a plan.
  *
  *   make -C examples && examples/jpeg2bmp out_dir a.jpg [b.jpg ...]
  */
@@ -102,7 +103,7 @@ int main(int argc, char** argv)
         const size_t bytes = (size_t)pitch * (size_t)info.height;
         void* d_out = NULL;
         HIP_CHECK(hipMalloc(&d_out, bytes));
-        if (info.single_scan) {   /* GPU Huffman decode + fused kernel */
+        if (info.process != 2) {   /* sequential (one scan or several): GPU Huffman decode + fused kernel */
             hjd_gdec* gd = NULL;
             CHECK(hjd_gdec_create(ctx, 1, (int64_t)size, info.nblocks, 0, &gd));
             const uint8_t* datas[1] = {data};
@@ -130,8 +131,9 @@ int main(int argc, char** argv)
             return 1;
         }
         fclose(f);
-        printf("%s: %dx%d sampling %d process %d -> %s\n", argv[a], info.width, info.height, info.sampling,
-               info.process, path);
+        printf("%s: %dx%d sampling %d process %d scans %s -> %s (%s Huffman)\n", argv[a], info.width, info.height,
+               info.sampling, info.process, info.single_scan ? "1" : "several", path,
+               info.process != 2 ? "GPU" : "host");
         free(px);
         HIP_CHECK(hipFree(d_out));
         free(data);

@@ -41,7 +41,8 @@ typedef struct hjd_jpeg_info {
     int32_t qt_precision[3];   /* 0 = 8-bit DQT entries, 1 = 16-bit */
     int64_t scan_offset;       /* byte offset of the (first) entropy-coded segment */
     int32_t process;           /* 0 = baseline (SOF0), 1 = extended sequential (SOF1), 2 = progressive (SOF2) */
-    int32_t single_scan;       /* 1: one interleaved sequential scan holds the image (GPU entropy decodable) */
+    int32_t single_scan;       /* 1: one interleaved sequential scan holds the image (0: several scans, or progressive;
+                                  the GPU entropy decoder takes every sequential file, process 0 or 1) */
 } hjd_jpeg_info;
 
 /* Besides the reference's single interleaved baseline scan, the host decoder

@@ -134,11 +134,18 @@ inline int sampling_class(int sampling)
     return hjd_internal::sampling_geom(sampling, &g) ? g.index : 0;
 }
 
-// Host-side result of preparing one JPEG.
+// Host-side result of preparing one JPEG: its (first) scan, which is the
+// whole image for the reference's single interleaved scan, plus `more` for
+// the further scans of a sequential file with several (an extension; each
+// becomes an entropy frame of its own writing into the same coefficients).
+constexpr int kMaxScans = 3;   // sequential: one scan per component at most (T.81 B.2.3)
 struct Prepared {
     int rc = HJD_OK;
     int width = 0, height = 0, sampling = 0, bpm = 0;
-    int64_t nblocks = 0;
+    int64_t nblocks = 0;       // blocks this scan codes
+    int64_t out_blocks = 0;    // blocks of the image
+    uint32_t layout = kLayoutMcu, geo = 0, mcu_w = 0;   // EntFrame fields (block_dest)
+    std::vector<Prepared> more;
     uint32_t data_bits = 0;
     size_t data_off = 0;       // in the batch data area
     int ntab = 0;
@@ -155,11 +162,115 @@ struct Prepared {
     const uint8_t* raw_src = nullptr;   // caller's pinned bytes (kDestuffFromCaller)
     uint32_t raw_len = 0;
     uint64_t raw_off = 0;      // raw-area offset of the first scan byte (RawCursor::place)
+
+    // end of the data area this file uses (all scans, with their pads)
+    size_t data_end() const
+    {
+        size_t e = data_off + data_bits / 8 + kDataPad;
+        for (const Prepared& q : more) e = std::max(e, q.data_off + q.data_bits / 8 + kDataPad);
+        return e;
+    }
 };
+
+// Data-area bytes a JPEG of `size` bytes may need: its destuffed scans are
+// shorter than the file, but each scan is padded and aligned.
+inline size_t data_need(size_t size) { return align_up(size + kDataPad, 16) + (kMaxScans - 1) * (kDataPad + 16); }
 
 constexpr int kDestuffHost = 0;          // memchr/memcpy destuff into pinned staging (destuff() above)
 constexpr int kDestuffFromCaller = 1;    // raw bytes DMA'd from the caller's pinned buffer, destuffed on the GPU
 constexpr int kDestuffFromStaging = 2;   // raw bytes memcpy'd into pinned staging, destuffed on the GPU
+
+// The scan-level fields of q from its header: geometry, and the tables the
+// scan references, deduplicated into slots.
+int scan_fields(const hjd_internal::ScanHeader& h, Prepared& q)
+{
+    q.bpm = h.bpm;
+    q.nblocks = h.scan_blocks;
+    q.restart_mcus = h.restart_interval;
+    q.layout = h.layout ? kLayoutRaster : kLayoutMcu;
+    q.geo = geo_make(static_cast<uint32_t>(h.out_bpm), static_cast<uint32_t>(h.comp_lh),
+                     static_cast<uint32_t>(h.comp_lv), static_cast<uint32_t>(h.comp_bw));
+    q.mcu_w = static_cast<uint32_t>(h.mcu_w);
+    int slot_of[2][4];
+    for (auto& a : slot_of)
+        for (int& v : a) v = -1;
+    q.ntab = 0;
+    for (int j = 0; j < h.bpm; ++j) {
+        const int ids[2] = {h.jdc[j], h.jac[j]};
+        int slot[2];
+        for (int cls = 0; cls < 2; ++cls) {
+            int& s = slot_of[cls][ids[cls]];
+            if (s < 0) {
+                if (q.ntab >= kMaxTables) return set_error(HJD_E_INVALID, "too many Huffman tables");
+                s = q.ntab++;
+                if (build_lut(q.tabs[s], h.counts[cls][ids[cls]], h.symbols[cls][ids[cls]], h.nsym[cls][ids[cls]],
+                              cls == 0))
+                    return set_error(HJD_E_INVALID, "invalid Huffman table");
+            }
+            slot[cls] = s;
+        }
+        q.jinfo[j] = static_cast<uint16_t>(jinfo_make(slot[0], slot[1], h.jcomp[j], h.jslot[j]));
+    }
+    return HJD_OK;
+}
+
+// Restart intervals a scan must hold: DRI counts the scan's MCUs, which are
+// single blocks in a non-interleaved scan.
+inline int64_t scan_segments(const hjd_internal::ScanHeader& h)
+{
+    const int64_t units = h.layout ? h.scan_blocks : static_cast<int64_t>(h.mcu_w) * h.mcu_h;
+    return h.restart_interval > 0 ? (units + h.restart_interval - 1) / h.restart_interval : 1;
+}
+
+// Host destuff of one scan into dst (cap bytes, the pad included).
+int destuff_scan(const hjd_internal::ScanHeader& h, const uint8_t* data, size_t size, uint8_t* dst, size_t cap,
+                 Prepared& q)
+{
+    if (h.scan_offset > size) return set_error(HJD_E_INVALID, "scan offset past the end of the file");
+    if (cap <= kDataPad) return set_error(HJD_E_INVALID, "scan bytes exceed the batch capacity");
+    size_t len = 0;
+    q.raw_len = static_cast<uint32_t>(std::min<size_t>(size - h.scan_offset, 0xFFFFFFFFu));   // bytes the host reads
+    int rc = destuff(data + h.scan_offset, data + size, dst, cap - kDataPad, q.seg_end, len);
+    if (rc) return rc;
+    if (len == 0) return set_error(HJD_E_INVALID, "empty scan");
+    if (len >= (1u << 28)) return set_error(HJD_E_INVALID, "scan too large for one frame (>= 256 MiB)");
+    const int64_t want = scan_segments(h);
+    if (static_cast<int64_t>(q.seg_end.size()) != want)
+        return set_error(HJD_E_INVALID, "%zu restart intervals in the scan, %lld expected", q.seg_end.size(),
+                         static_cast<long long>(want));
+    if (h.nblocks >= (1ll << 31)) return set_error(HJD_E_INVALID, "frame too large");
+    memset(dst + len, 0xFF, kDataPad);
+    q.data_bits = static_cast<uint32_t>(len * 8);
+    return HJD_OK;
+}
+
+// A sequential file with several scans: every scan destuffed on the host, one
+// after the other from dst (cap bytes); quantisation tables as of each
+// component's scan.
+int prepare_multiscan(const uint8_t* data, size_t size, uint8_t* dst, size_t cap, Prepared& pf)
+{
+    std::vector<hjd_internal::ScanHeader> hs;
+    int rc = hjd_internal::parse_scan_headers(data, size, &hs);
+    if (rc) return rc;
+    if (hs.empty() || hs.size() > static_cast<size_t>(kMaxScans)) return set_error(HJD_E_INVALID, "bad scan count");
+    pf.more.resize(hs.size() - 1);
+    size_t off = 0;
+    for (size_t k = 0; k < hs.size(); ++k) {
+        Prepared& q = k == 0 ? pf : pf.more[k - 1];
+        rc = scan_fields(hs[k], q);
+        if (rc) return rc;
+        if (off >= cap) return set_error(HJD_E_INVALID, "scan bytes exceed the batch capacity");
+        q.data_off = pf.data_off + off;
+        rc = destuff_scan(hs[k], data, size, dst + off, cap - off, q);
+        if (rc) return rc;
+        for (int j = 0; j < hs[k].bpm; ++j) {
+            const int c = hs[k].jcomp[j];
+            memcpy(pf.qt[c], hs[k].qt[c], sizeof(pf.qt[c]));
+        }
+        off = align_up(off + q.data_bits / 8 + kDataPad, 16);
+    }
+    return HJD_OK;
+}
 
 int prepare(const uint8_t* data, size_t size, uint8_t* dst, size_t cap, Prepared& pf, int mode = kDestuffHost,
             uint64_t raw_off = 0)
@@ -170,32 +281,14 @@ int prepare(const uint8_t* data, size_t size, uint8_t* dst, size_t cap, Prepared
     pf.width = h.width;
     pf.height = h.height;
     pf.sampling = h.sampling;
-    pf.bpm = h.bpm;
-    pf.nblocks = h.nblocks;
-    pf.restart_mcus = h.restart_interval;
+    pf.out_blocks = h.nblocks;
     memcpy(pf.qt, h.qt, sizeof(pf.qt));
-    // tables referenced by the scan, deduplicated into slots
-    int slot_of[2][4];
-    for (auto& a : slot_of)
-        for (int& v : a) v = -1;
-    pf.ntab = 0;
-    for (int j = 0; j < h.bpm; ++j) {
-        const int ids[2] = {h.jdc[j], h.jac[j]};
-        int slot[2];
-        for (int cls = 0; cls < 2; ++cls) {
-            int& s = slot_of[cls][ids[cls]];
-            if (s < 0) {
-                if (pf.ntab >= kMaxTables) return set_error(HJD_E_INVALID, "too many Huffman tables");
-                s = pf.ntab++;
-                if (build_lut(pf.tabs[s], h.counts[cls][ids[cls]], h.symbols[cls][ids[cls]], h.nsym[cls][ids[cls]],
-                              cls == 0))
-                    return set_error(HJD_E_INVALID, "invalid Huffman table");
-            }
-            slot[cls] = s;
-        }
-        pf.jinfo[j] = static_cast<uint16_t>(jinfo_make(slot[0], slot[1], h.jcomp[j], h.jslot[j]));
+    if (h.extra_scans > 0) {   // several scans: plan_raw keeps them on the host destuff path
+        if (mode != kDestuffHost) return set_error(HJD_E_INVALID, "multi-scan JPEG: host destuff only");
+        return prepare_multiscan(data, size, dst, cap + kDataPad, pf);
     }
-    size_t len = 0;
+    rc = scan_fields(h, pf);
+    if (rc) return rc;
     if (h.scan_offset > size) return set_error(HJD_E_INVALID, "scan offset past the end of the file");
     if (mode != kDestuffHost) {
         // the header is all the host reads; the GPU finds stuffing, markers and the scan's end
@@ -217,20 +310,7 @@ int prepare(const uint8_t* data, size_t size, uint8_t* dst, size_t cap, Prepared
         pf.data_bits = static_cast<uint32_t>(raw * 8);      // upper bound (groups are laid out for it)
         return HJD_OK;
     }
-    pf.raw_len = static_cast<uint32_t>(std::min<size_t>(size - h.scan_offset, 0xFFFFFFFFu));   // bytes the host reads
-    rc = destuff(data + h.scan_offset, data + size, dst, cap, pf.seg_end, len);
-    if (rc) return rc;
-    if (len == 0) return set_error(HJD_E_INVALID, "empty scan");
-    if (len >= (1u << 28)) return set_error(HJD_E_INVALID, "scan too large for one frame (>= 256 MiB)");
-    const int64_t nmcu = static_cast<int64_t>(h.mcu_w) * h.mcu_h;
-    const int64_t want = h.restart_interval > 0 ? (nmcu + h.restart_interval - 1) / h.restart_interval : 1;
-    if (static_cast<int64_t>(pf.seg_end.size()) != want)
-        return set_error(HJD_E_INVALID, "%zu restart intervals in the scan, %lld expected", pf.seg_end.size(),
-                         static_cast<long long>(want));
-    if (h.nblocks >= (1ll << 31)) return set_error(HJD_E_INVALID, "frame too large");
-    memset(dst + len, 0xFF, kDataPad);
-    pf.data_bits = static_cast<uint32_t>(len * 8);
-    return HJD_OK;
+    return destuff_scan(h, data, size, dst, cap + kDataPad, pf);
 }
 
 // Device destuff ("Destuff on the GPU").  A frame whose scan
@@ -328,12 +408,14 @@ Caps make_caps(int max_frames, int64_t max_scan_bytes, int64_t max_blocks, int s
     c.max_scan_bytes = max_scan_bytes;
     c.max_blocks = max_blocks;
     c.sub_bits = sub_bits;
-    c.max_subs = (max_scan_bytes * 8 + sub_bits - 1) / sub_bits + max_frames;
-    c.max_wgs = (c.max_subs + kOwn - 1) / kOwn + max_frames;
-    c.max_segs = max_blocks / 3 + max_frames;
+    // entropy frames: one per scan, kMaxScans per JPEG at most
+    const int64_t ef = static_cast<int64_t>(max_frames) * kMaxScans;
+    c.max_subs = (max_scan_bytes * 8 + sub_bits - 1) / sub_bits + ef;
+    c.max_wgs = (c.max_subs + kOwn - 1) / kOwn + ef;
+    c.max_segs = max_blocks / 3 + ef;
     c.max_tiles = max_scan_bytes / kTileBytes + max_frames;
-    const size_t per_frame = sizeof(EntFrame) + sizeof(HuffLut) * kMaxTables + sizeof(FrameRecord) + 192 * 4 +
-                             sizeof(RawFrame);
+    const size_t per_frame = (sizeof(EntFrame) + sizeof(HuffLut) * kMaxTables) * kMaxScans + sizeof(FrameRecord) +
+                             192 * 4 + sizeof(RawFrame);
     c.hdr_cap = align_up(per_frame * max_frames + 4 * static_cast<size_t>(c.max_segs + c.max_wgs + c.max_tiles) +
                              10 * kAlign, kAlign);
     c.data = c.hdr_cap;
@@ -391,6 +473,9 @@ __host__ __device__ __forceinline__ RunCtx make_ctx(const EntBatchDev& b, const 
     c.bpm = F.bpm;
     c.seg_blocks = F.seg_blocks;
     c.steps = steps;
+    c.layout = F.layout;
+    c.geo = F.geo;
+    c.mcu_w = F.mcu_w;
     return c;
 }
 
@@ -1232,6 +1317,7 @@ __global__ __launch_bounds__(kWriteThreads) void ent_write_kernel(EntBatchDev b)
     o.stage = stage + tid * kStageStride;
     o.blk = excl.nblk;
     o.nblocks = F.nblocks;
+    o.nout = F.nout;
     o.pred[0] = excl.dc[0];
     o.pred[1] = excl.dc[1];
     o.pred[2] = excl.dc[2];
@@ -1768,6 +1854,7 @@ void emulate(const EntBatchDev& b)
                 o.stage = stage;
                 o.blk = p.nblk;
                 o.nblocks = F.nblocks;
+                o.nout = F.nout;
                 o.pred[0] = p.dc[0];
                 o.pred[1] = p.dc[1];
                 o.pred[2] = p.dc[2];
@@ -1838,8 +1925,10 @@ struct hjd_gdec {
     std::vector<uint8_t> e_cmap, e_cslot;
 
     uint8_t* data_area() { return h_stage + caps.data; }
-    size_t data_cap() const { return static_cast<size_t>(caps.max_scan_bytes) + kDataPad * caps.max_frames +
-                                     16 * static_cast<size_t>(caps.max_frames); }
+    // data_need() of every frame: the scan bytes, plus pad and alignment per scan
+    size_t data_cap() const { return static_cast<size_t>(caps.max_scan_bytes) +
+                                     (kDataPad + 16) * kMaxScans * static_cast<size_t>(caps.max_frames); }
+    std::vector<int> scan_file;         // file of each entropy frame past the first n (a file's further scans)
 
     int wait_staging();
     int stage_frames(const uint8_t* const* datas, const size_t* sizes, int n);
@@ -1924,6 +2013,10 @@ int hjd_gdec::plan_raw(const uint8_t* data, size_t size, RawCursor& cur, int& mo
     const int rc = hjd_internal::parse_scan_header(data, size, &h);
     if (rc) return rc;
     if (h.scan_offset >= size) return set_error(HJD_E_INVALID, "empty scan");
+    if (h.extra_scans > 0) {   // several scans: destuffed (and their ends found) on the host
+        mode = kDestuffHost;
+        return HJD_OK;
+    }
     const size_t raw = size - h.scan_offset;
     // the device path needs the raw scan (stuffing, markers and the bytes
     // after EOI included) in both the raw and the data area; the host path
@@ -1963,7 +2056,7 @@ int hjd_gdec::stage_frames(const uint8_t* const* datas, const size_t* sizes, int
     // take: a frame with a device-destuffed scan is placed only if the rest
     // still fit, so a batch sized by its file bytes never fails on placement
     std::vector<uint64_t> tail(static_cast<size_t>(n) + 1, 0);
-    for (int i = n - 1; i >= 0; --i) tail[i] = tail[i + 1] + align_up(sizes[i] + kDataPad, 16);
+    for (int i = n - 1; i >= 0; --i) tail[i] = tail[i + 1] + data_need(sizes[i]);
     for (int i = 0; i < n; ++i) {
         if (data_used >= data_cap()) return set_error(HJD_E_INVALID, "scan bytes exceed the batch capacity");
         int mode;
@@ -1974,8 +2067,8 @@ int hjd_gdec::stage_frames(const uint8_t* const* datas, const size_t* sizes, int
         if (!fits) return set_error(HJD_E_INVALID, "scan bytes exceed the batch capacity");
         rc = prepare_frame(i, datas[i], sizes[i], data_used, data_cap() - data_used, mode, raw_off);
         if (rc) return set_error(rc, "frame %d: %s", i, hjd_last_error());
-        data_used = align_up(data_used + frames[i].data_bits / 8 + kDataPad, 16);
-        blocks += frames[i].nblocks;
+        data_used = align_up(frames[i].data_end(), 16);
+        blocks += frames[i].out_blocks;
     }
     if (blocks > caps.max_blocks)
         return set_error(HJD_E_INVALID, "batch needs %lld blocks (capacity %lld)", static_cast<long long>(blocks),
@@ -1988,16 +2081,38 @@ int hjd_gdec::assemble(uint8_t* blob, int16_t* coefs, int64_t* block_offsets, vo
 {
     const int n = static_cast<int>(frames.size());
     const uint32_t S = static_cast<uint32_t>(caps.sub_bits);
+    // entropy frames: the n JPEGs' (first) scans, then the further scans of
+    // multi-scan files (scan_file: their JPEG), all writing the JPEG's blocks
+    std::vector<const Prepared*> ents;
+    std::vector<int> ent_file;
+    scan_file.clear();
+    for (int i = 0; i < n; ++i) {
+        ents.push_back(&frames[i]);
+        ent_file.push_back(i);
+    }
+    for (int i = 0; i < n; ++i)
+        for (const Prepared& q : frames[i].more) {
+            ents.push_back(&q);
+            ent_file.push_back(i);
+            scan_file.push_back(i);
+        }
+    const int ne = static_cast<int>(ents.size());
+    std::vector<uint64_t> file_coef(static_cast<size_t>(n), 0);
+    uint64_t coef_off = 0;
+    for (int i = 0; i < n; ++i) {
+        file_coef[i] = coef_off;
+        coef_off += static_cast<uint64_t>(frames[i].out_blocks);
+    }
     size_t ntab = 0, nseg = 0, nwg = 0;
-    for (const Prepared& p : frames) {
-        ntab += static_cast<size_t>(p.ntab);
-        nseg += p.seg_end.size();
-        const uint32_t ns = (p.data_bits + S - 1) / S;
+    for (const Prepared* p : ents) {
+        ntab += static_cast<size_t>(p->ntab);
+        nseg += p->seg_end.size();
+        const uint32_t ns = (p->data_bits + S - 1) / S;
         nwg += frame_groups(ns);
     }
     HdrOffsets& o = H;
     o.frames = 0;
-    o.tabs = align_up(sizeof(EntFrame) * n, kAlign);
+    o.tabs = align_up(sizeof(EntFrame) * ne, kAlign);
     o.seg = align_up(o.tabs + sizeof(HuffLut) * ntab, kAlign);
     o.wg = align_up(o.seg + 4 * nseg, kAlign);
     o.recs = align_up(o.wg + 4 * nwg, kAlign);
@@ -2007,7 +2122,7 @@ int hjd_gdec::assemble(uint8_t* blob, int16_t* coefs, int64_t* block_offsets, vo
         if (p.destuff != kDestuffHost)
             ntiles += (raw_region_len(static_cast<uint32_t>(p.raw_off & 15), p.raw_len) + kTileBytes - 1) / kTileBytes;
     o.rawf = align_up(o.qt + (d_outs ? 192 * 4 * static_cast<size_t>(n) : 0), kAlign);
-    o.tilef = align_up(o.rawf + (ntiles ? sizeof(RawFrame) * n : 0), kAlign);
+    o.tilef = align_up(o.rawf + (ntiles ? sizeof(RawFrame) * ne : 0), kAlign);
     o.used = align_up(o.tilef + 4 * ntiles, kAlign);
     if (o.used > caps.hdr_cap || ntiles > static_cast<size_t>(caps.max_tiles))
         return set_error(HJD_E_INVALID, "batch header exceeds its capacity");
@@ -2017,13 +2132,13 @@ int hjd_gdec::assemble(uint8_t* blob, int16_t* coefs, int64_t* block_offsets, vo
     uint32_t* seg = reinterpret_cast<uint32_t*>(h_stage + o.seg);
     uint32_t* wgf = reinterpret_cast<uint32_t*>(h_stage + o.wg);
     uint32_t sub_base = 0, wg_base = 0, seg_base = 0, tab_base = 0;
-    uint64_t coef_off = 0;
-    for (int i = 0; i < n; ++i) {
-        const Prepared& p = frames[i];
+    for (int e = 0; e < ne; ++e) {
+        const Prepared& p = *ents[e];
+        const Prepared& file = frames[ent_file[e]];
         EntFrame F;
         memset(&F, 0, sizeof(F));
         F.data_off = p.data_off;
-        F.coef_off = coef_off;
+        F.coef_off = file_coef[ent_file[e]];
         F.data_bits = p.data_bits;
         F.nsub = (p.data_bits + S - 1) / S;
         F.sub_base = sub_base;
@@ -2034,21 +2149,25 @@ int hjd_gdec::assemble(uint8_t* blob, int16_t* coefs, int64_t* block_offsets, vo
         F.tab_base = tab_base;
         F.ntab = static_cast<uint8_t>(p.ntab);
         F.bpm = static_cast<uint8_t>(p.bpm);
-        F.sampling = static_cast<uint8_t>(p.sampling);
+        F.sampling = static_cast<uint8_t>(file.sampling);
+        F.layout = static_cast<uint8_t>(p.layout);
         memcpy(F.jinfo, p.jinfo, sizeof(F.jinfo));
         F.seg_blocks = F.nseg > 1 ? static_cast<uint32_t>(p.restart_mcus * p.bpm) : 0u;
-        ef[i] = F;
+        F.geo = p.geo;
+        F.mcu_w = p.mcu_w;
+        F.nout = static_cast<uint32_t>(file.out_blocks);
+        ef[e] = F;
         memcpy(tb + tab_base, p.tabs, sizeof(HuffLut) * p.ntab);
         memcpy(seg + seg_base, p.seg_end.data(), 4 * p.seg_end.size());
         const uint32_t nw = frame_groups(F.nsub);
-        for (uint32_t g = 0; g < nw; ++g) wgf[wg_base + g] = static_cast<uint32_t>(i);
-        if (block_offsets) block_offsets[i] = static_cast<int64_t>(coef_off);
+        for (uint32_t g = 0; g < nw; ++g) wgf[wg_base + g] = static_cast<uint32_t>(e);
         sub_base += F.nsub;
         wg_base += nw;
         seg_base += F.nseg;
         tab_base += p.ntab;
-        coef_off += p.nblocks;
     }
+    if (block_offsets)
+        for (int i = 0; i < n; ++i) block_offsets[i] = static_cast<int64_t>(file_coef[i]);
     if (coef_off > static_cast<uint64_t>(caps.max_blocks) || sub_base > caps.max_subs || wg_base > caps.max_wgs)
         return set_error(HJD_E_INVALID, "batch exceeds the decoder's capacity");
 
@@ -2105,15 +2224,15 @@ int hjd_gdec::assemble(uint8_t* blob, int16_t* coefs, int64_t* block_offsets, vo
         RawFrame* rf = reinterpret_cast<RawFrame*>(h_stage + o.rawf);
         uint32_t* tf = reinterpret_cast<uint32_t*>(h_stage + o.tilef);
         uint32_t tbase = 0;
-        for (int i = 0; i < n; ++i) {
-            const Prepared& p = frames[i];
+        for (int e = 0; e < ne; ++e) {   // further scans are host-destuffed (ntiles 0)
+            const Prepared& p = *ents[e];
             RawFrame r{p.raw_off, p.raw_len, static_cast<uint32_t>(p.raw_off & 15), tbase, 0, 0, 0};
             if (p.destuff != kDestuffHost) {
                 r.ntiles = (raw_region_len(r.begin, p.raw_len) + kTileBytes - 1) / kTileBytes;
-                for (uint32_t k = 0; k < r.ntiles; ++k) tf[tbase + k] = static_cast<uint32_t>(i);
+                for (uint32_t k = 0; k < r.ntiles; ++k) tf[tbase + k] = static_cast<uint32_t>(e);
                 tbase += r.ntiles;
             }
-            rf[i] = r;
+            rf[e] = r;
         }
         d.rawf = reinterpret_cast<RawFrame*>(blob + o.rawf);
         d.tile_frame = reinterpret_cast<const uint32_t*>(blob + o.tilef);
@@ -2124,11 +2243,11 @@ int hjd_gdec::assemble(uint8_t* blob, int16_t* coefs, int64_t* block_offsets, vo
     d.wg_frame = reinterpret_cast<const uint32_t*>(blob + o.wg);
     d.data = blob + caps.data;
     d.coefs = coefs;
-    d.nframes = static_cast<uint32_t>(n);
+    d.nframes = static_cast<uint32_t>(ne);
     d.nwg = wg_base;
     d.sub_bits = S;
     d.ntab_max = 1;
-    for (const Prepared& p : frames) d.ntab_max = std::max<uint32_t>(d.ntab_max, static_cast<uint32_t>(p.ntab));
+    for (const Prepared* p : ents) d.ntab_max = std::max<uint32_t>(d.ntab_max, static_cast<uint32_t>(p->ntab));
     return HJD_OK;
 }
 
@@ -2144,8 +2263,8 @@ int gdec_alloc(hjd_gdec* g)
     }
     HJD_HIP(hipSetDevice(g->device));
     HJD_HIP(hipHostMalloc(reinterpret_cast<void**>(&g->h_stage), total, hipHostMallocDefault));
-    HJD_HIP(hipHostMalloc(reinterpret_cast<void**>(&g->h_status), 4 * static_cast<size_t>(g->caps.max_frames),
-                          hipHostMallocDefault));
+    HJD_HIP(hipHostMalloc(reinterpret_cast<void**>(&g->h_status),
+                          4 * kMaxScans * static_cast<size_t>(g->caps.max_frames), hipHostMallocDefault));
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_blob), total));
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_entries), 8 * static_cast<size_t>(g->caps.max_subs)));
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_stats), sizeof(SubStats) * static_cast<size_t>(g->caps.max_subs)));
@@ -2154,7 +2273,7 @@ int gdec_alloc(hjd_gdec* g)
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_wentries), 8 * kWarm * static_cast<size_t>(g->caps.max_wgs)));
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_linked), 4 * static_cast<size_t>(g->caps.max_wgs)));
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_agg), sizeof(SubStats) * static_cast<size_t>(g->caps.max_wgs)));
-    HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_status), 4 * static_cast<size_t>(g->caps.max_frames)));
+    HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_status), 4 * kMaxScans * static_cast<size_t>(g->caps.max_frames)));
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_coefs), 128 * static_cast<size_t>(g->caps.max_blocks)));
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_raw), g->data_cap()));
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_tiles), 12 * static_cast<size_t>(g->caps.max_tiles)));
@@ -2282,12 +2401,14 @@ int gdec_issue(hjd_gdec* g, void* const* d_outs, const int32_t* pitches, int16_t
             ++i;
             continue;
         }
-        int j = i + 1;                   // host-destuffed: one copy per run of frames
-        size_t hi = p.data_off + len + kDataPad;
+        int j = i + 1;                   // host-destuffed: one copy per run of frames (all their scans)
+        size_t hi = p.data_end();
+        for (const Prepared& q : p.more) host_bytes += static_cast<int64_t>(q.data_bits / 8);
         while (j < n && g->frames[j].destuff == kDestuffHost) {
             const Prepared& q = g->frames[j];
-            hi = q.data_off + q.data_bits / 8 + kDataPad;
+            hi = q.data_end();
             host_bytes += static_cast<int64_t>(q.raw_len) + q.data_bits / 8;
+            for (const Prepared& r : q.more) host_bytes += static_cast<int64_t>(r.data_bits / 8);
             ++j;
         }
         uint8_t* dst = g->d_blob + g->caps.data + p.data_off;
@@ -2315,6 +2436,17 @@ int gdec_issue(hjd_gdec* g, void* const* d_outs, const int32_t* pitches, int16_t
     g->last_host_scan_bytes = host_bytes;
     HJD_HIP(hipEventRecord(g->staged, s));
     g->pending = true;
+    // a multi-scan file's non-interleaved scans leave its MCU-padding blocks
+    // uncoded: they must read as zeros (as the host decoder's)
+    {
+        size_t first = 0;
+        for (int i = 0; i < n; ++i) {
+            const Prepared& p = g->frames[i];
+            if (!p.more.empty())
+                HJD_HIP(hipMemsetAsync(coefs + first * 64, 0, static_cast<size_t>(p.out_blocks) * 128, s));
+            first += static_cast<size_t>(p.out_blocks);
+        }
+    }
     rc = launch_entropy(g, b, s);
     if (rc) return rc;
     if (d_outs) {
@@ -2339,7 +2471,7 @@ int gdec_issue(hjd_gdec* g, void* const* d_outs, const int32_t* pitches, int16_t
                                      static_cast<size_t>(host[i].height), hipMemcpyDeviceToHost, s));
         }
     }
-    HJD_HIP(hipMemcpyAsync(g->h_status, g->d_status, 4 * static_cast<size_t>(n), hipMemcpyDeviceToHost, s));
+    HJD_HIP(hipMemcpyAsync(g->h_status, g->d_status, 4 * static_cast<size_t>(b.nframes), hipMemcpyDeviceToHost, s));
     HJD_HIP(hipEventRecord(g->done, s));
     g->nframes_issued = n;
     return HJD_OK;
@@ -2506,6 +2638,8 @@ int hjd_gdec_sync(hjd_gdec* g, int32_t* status)
     if (!g->pending) return HJD_OK;
     HJD_HIP(hipSetDevice(g->device));
     HJD_HIP(hipEventSynchronize(g->done));
+    for (size_t e = 0; e < g->scan_file.size(); ++e)   // a JPEG's further scans
+        g->h_status[g->scan_file[e]] |= g->h_status[g->nframes_issued + e];
     int bad = 0;
     for (int i = 0; i < g->nframes_issued; ++i) {
         const uint32_t s = g->h_status[i] & ~kStatusFallback;
@@ -2682,13 +2816,13 @@ int hjd_debug_entropy_emulate(const uint8_t* data, size_t size, int sub_bits, in
     const size_t sizes[1] = {size};
     rc = g.stage_frames(datas, sizes, 1);
     if (rc) return rc;
-    if (g.frames[0].nblocks > capacity_blocks)
+    if (g.frames[0].out_blocks > capacity_blocks)
         return set_error(HJD_E_INVALID, "capacity %lld < %lld blocks", static_cast<long long>(capacity_blocks),
-                         static_cast<long long>(g.frames[0].nblocks));
+                         static_cast<long long>(g.frames[0].out_blocks));
     EntBatchDev b;
     rc = g.assemble(g.h_stage, coefs, nullptr, nullptr, nullptr, b);
     if (rc) return rc;
-    const int64_t total = g.frames[0].nblocks;
+    const int64_t total = g.frames[0].out_blocks;
     g.e_entries.assign(static_cast<size_t>(g.caps.max_subs), 0);
     g.e_stats.assign(static_cast<size_t>(g.caps.max_subs), stats_identity());
     g.e_mids.assign(static_cast<size_t>(g.caps.max_subs), 0);
@@ -2696,7 +2830,7 @@ int hjd_debug_entropy_emulate(const uint8_t* data, size_t size, int sub_bits, in
     g.e_wentries.assign(static_cast<size_t>(g.caps.max_wgs) * kWarm, 0);
     g.e_linked.assign(static_cast<size_t>(g.caps.max_wgs), 0);
     g.e_agg.assign(static_cast<size_t>(g.caps.max_wgs), stats_identity());
-    g.e_status.assign(1, 0);
+    g.e_status.assign(b.nframes, 0);
     if (g.spec) {
         const size_t n = static_cast<size_t>(g.caps.max_subs);
         g.e_spec.assign(n * kMaxBpm, SpecRec());
@@ -2719,6 +2853,7 @@ int hjd_debug_entropy_emulate(const uint8_t* data, size_t size, int sub_bits, in
     b.status = g.e_status.data();
     memset(coefs, 0, static_cast<size_t>(total) * 128);
     emulate(b);
+    for (uint32_t e = 1; e < b.nframes; ++e) g.e_status[0] |= g.e_status[e];   // the JPEG's further scans
     if (status) *status = static_cast<int32_t>(g.e_status[0]);
     if (g.e_status[0] & ~kStatusFallback) return set_error(HJD_E_INVALID, "corrupt entropy data (status %u)", g.e_status[0]);
     return HJD_OK;
@@ -2853,7 +2988,7 @@ void hjd_gstream::issue_locked(GBatch* b)
     for (int i = 0; i < b->nframes; ++i) {
         Prepared& p = g->frames[i];
         if (p.rc != HJD_OK) continue;
-        used = std::max(used, align_up(p.data_off + p.data_bits / 8 + kDataPad, 16));
+        used = std::max(used, align_up(p.data_end(), 16));
         images++;
         pixels += static_cast<int64_t>(p.width) * p.height;
         if (b->host_outs[i]) {
@@ -2974,7 +3109,7 @@ static int gstream_submit(hjd_gstream* st, const uint8_t* data, size_t size, voi
     if (rc) return rc;
     if (out_pitch < hjd_internal::out_format_bytes(st->out_format) * h.width)
         return set_error(HJD_E_INVALID, "output pitch too small");
-    const size_t need = align_up(size + kDataPad, 16);
+    const size_t need = h.extra_scans > 0 ? data_need(size) : align_up(size + kDataPad, 16);
     std::lock_guard<std::mutex> api(st->api_mu);
     std::unique_lock<std::mutex> lk(st->mu);
     hjd_gdec* g0 = st->slots[0];

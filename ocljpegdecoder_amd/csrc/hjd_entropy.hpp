@@ -92,12 +92,28 @@ struct EntFrame {
     uint32_t nseg;        // restart intervals (1 without DRI)
     uint32_t nblocks;     // blocks the scan must produce
     uint32_t tab_base;    // first HuffLut of this frame
-    uint8_t ntab, bpm, sampling, pad0;
+    uint8_t ntab, bpm, sampling;
+    uint8_t layout;       // kLayoutMcu / kLayoutRaster (where the scan's blocks go, see block_dest)
     uint16_t jinfo[6];    // per bitstream block j of an MCU: dc slot | ac slot << 3 | comp << 6 | out slot << 8
     uint32_t seg_blocks;  // blocks of a full restart interval (DRI MCUs x bpm); 0 without restarts
-    uint32_t pad1[3];
+    uint32_t geo;         // out_bpm | comp_lh << 4 | comp_lv << 6 | comp_bw << 8 (geo_make)
+    uint32_t mcu_w;       // MCUs per row of the image
+    uint32_t nout;        // blocks of the image (= nblocks for a single scan)
 };
 static_assert(sizeof(EntFrame) == 80, "EntFrame layout");
+
+// Scan layouts.  A "frame" of the entropy kernels is one scan: the reference's
+// single interleaved scan, or one scan of a sequential file with several
+// (an extension; its scans write into the same coefficient frame).
+//   kLayoutMcu:    the scan's MCUs are the image's, holding bpm <= out_bpm of
+//                  its blocks (all of them for the single scan);
+//   kLayoutRaster: one component's blocks in raster order over its own block
+//                  grid (comp_bw wide; T.81 A.2.2), one block per "MCU".
+constexpr uint32_t kLayoutMcu = 0, kLayoutRaster = 1;
+__host__ __device__ __forceinline__ uint32_t geo_make(uint32_t out_bpm, uint32_t lh, uint32_t lv, uint32_t bw)
+{
+    return out_bpm | (lh << 4) | (lv << 6) | (bw << 8);
+}
 
 // Per-subsequence statistics of a run; combined with an ordered, segmented
 // operator to get each subsequence's block index and DC predictors.
@@ -229,7 +245,20 @@ struct RunCtx {
     int bpm;
     uint32_t seg_blocks;       // EntFrame::seg_blocks
     const uint8_t* steps;      // [table][1 << kStepBits] AC step entries (LDS), or null: one unit per step
+    uint32_t layout, geo, mcu_w;   // EntFrame: where the scan's blocks go (block_dest)
 };
+
+// Write mode: where the scan's block lands in the image's MCU-major
+// coefficients.  (u, v): kLayoutMcu -- the scan MCU and the block's j in it;
+// kLayoutRaster -- the block's column and row in the component's grid.
+__host__ __device__ __forceinline__ uint32_t block_dest(const RunCtx& c, uint32_t u, uint32_t v, uint32_t slot)
+{
+    const uint32_t out_bpm = c.geo & 15;
+    if (c.layout == kLayoutMcu) return u * out_bpm + slot;
+    const uint32_t lh = (c.geo >> 4) & 3, lv = (c.geo >> 6) & 3;
+    const uint32_t mcu = (v >> lv) * c.mcu_w + (u >> lh);
+    return mcu * out_bpm + slot + ((v & ((1u << lv) - 1)) << lh) + (u & ((1u << lh) - 1));
+}
 
 // AC step entry (sync mode): the AC units that a kStepBits-bit peek decodes
 // completely, taken in one step, since a sync run needs no AC values --
@@ -294,8 +323,9 @@ __host__ __device__ __forceinline__ int32_t mad24(int32_t a, int32_t b, int32_t 
 struct RunOut {
     int16_t* coefs;        // frame's first block
     int16_t* stage;        // this lane's 64-coefficient staging slot (LDS on the device)
-    uint32_t blk;          // index of the next block this run owns
-    uint32_t nblocks;
+    uint32_t blk;          // index (in scan order) of the next block this run owns
+    uint32_t nblocks;      // blocks of the scan
+    uint32_t nout;         // blocks of the image (destinations must stay below)
     int32_t pred[3];
 };
 
@@ -423,13 +453,21 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
     int32_t nblk = static_cast<int32_t>(st.nblk), d0 = st.dc[0], d1 = st.dc[1], d2 = st.dc[2];
     uint32_t flags = st.flags;
     int32_t p0 = 0, p1 = 0, p2 = 0;
-    uint32_t blk = 0, blk_j = 0;   // write mode: global block index and blk % bpm (kept incrementally)
+    // write mode, kept incrementally: the scan block index, its j in the scan
+    // MCU (blk % bpm) and its block_dest coordinates (bu, bv)
+    uint32_t blk = 0, blk_j = 0, bu = 0, bv = 0;
     if (kWrite) {
         p0 = out->pred[0];
         p1 = out->pred[1];
         p2 = out->pred[2];
         blk = out->blk;
-        blk_j = blk % static_cast<uint32_t>(c.bpm);
+        if (c.layout == kLayoutMcu) {
+            bu = blk / static_cast<uint32_t>(c.bpm);
+            blk_j = blk - bu * static_cast<uint32_t>(c.bpm);
+        } else {
+            bv = blk / (c.geo >> 8);
+            bu = blk - bv * (c.geo >> 8);
+        }
     }
     uint64_t result;
     if (seg >= c.nseg) {
@@ -570,11 +608,11 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
                     p1 = mad24(v, bi.m1, p1);
                     p2 = mad24(v, bi.m2, p2);
                     // MCU-major destination; on valid data blk % bpm == j.  Blocks past
-                    // the frame's count are ignored (as the host decoder stops there).
-                    const uint32_t dst = blk - j + (bi.ji >> 8);
+                    // the scan's count are ignored (as the host decoder stops there).
+                    const uint32_t dst = block_dest(c, bu, bv, bi.ji >> 8);
                     cur = nullptr;
                     if (blk < out->nblocks) {
-                        if (dst < out->nblocks && blk_j == j) {
+                        if (dst < out->nout && blk_j == j) {
                             cur = out->coefs + static_cast<uint64_t>(dst) * 64;
                             zero_quarter(out->stage);
                             out->stage[0] = static_cast<int16_t>(p0 * bi.m0 + p1 * bi.m1 + p2 * bi.m2);
@@ -597,7 +635,15 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
                 if (kWrite && owned) {
                     if (cur) flush_quarters(cur, out->stage, quarter, 4);   // the rest of the block
                     blk += 1;
-                    blk_j = blk_j + 1 == static_cast<uint32_t>(c.bpm) ? 0 : blk_j + 1;
+                    if (c.layout == kLayoutMcu) {
+                        const bool wrap = blk_j + 1 == static_cast<uint32_t>(c.bpm);
+                        blk_j = wrap ? 0 : blk_j + 1;
+                        bu += wrap ? 1 : 0;
+                    } else {
+                        const bool wrap = bu + 1 == (c.geo >> 8);
+                        bu = wrap ? 0 : bu + 1;
+                        bv += wrap ? 1 : 0;
+                    }
                     owned = false;
                     cur = nullptr;
                 }

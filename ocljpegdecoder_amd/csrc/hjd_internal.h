@@ -61,10 +61,15 @@ inline bool out_vector_ok(int out_format, int64_t pitch, int64_t out_base)
     return out_format == 1 ? ((pitch | out_base) & 3) == 0 : ((pitch | out_base) & 15) == 0;
 }
 
-// Parsed baseline-JPEG header as the GPU entropy path needs it (jpeg_host.cpp).
+// Parsed header of one sequential scan as the GPU entropy path needs it
+// (jpeg_host.cpp).  File-level fields (width .. nblocks, out_bpm, qt) describe
+// the whole image; the rest the scan.
 struct ScanHeader {
-    int width, height, sampling, restart_interval, mcu_w, mcu_h, bpm;
-    int64_t nblocks;
+    int width, height, sampling, restart_interval, mcu_w, mcu_h;
+    int bpm;                     // blocks per MCU of this scan (1 for a non-interleaved scan)
+    int out_bpm;                 // blocks per MCU of the image (the coefficient layout)
+    int64_t nblocks;             // blocks of the image (mcu_w * mcu_h * out_bpm)
+    int64_t scan_blocks;         // blocks this scan codes
     size_t scan_offset;          // first byte of entropy-coded data
     int32_t qt[3][64];           // per frame component, zigzag (file) order
     int jcomp[6], jdc[6], jac[6], jslot[6];   // per bitstream block of an MCU
@@ -72,8 +77,19 @@ struct ScanHeader {
     uint8_t counts[2][4][16];
     uint8_t symbols[2][4][256];
     int nsym[2][4];
+    // Sequential files with several scans (T.81 B.2.3; an extension, the
+    // reference takes one interleaved scan): `extra_scans` > 0 on the first
+    // scan's header says how many more scans the frame can hold (<= 2, one per
+    // component not in the first scan); parse_scan_headers() lists them.
+    int extra_scans;
+    int layout;                  // 0: MCU-interleaved; 1: one component in raster block order (A.2.2)
+    int comp_bw, comp_bh;        // layout 1: the component's block grid
+    int comp_lh, comp_lv;        // layout 1: log2 of its sampling factors
 };
 int parse_scan_header(const uint8_t* data, size_t size, ScanHeader* h);
+// Every scan of a sequential file (hs[0] == what parse_scan_header gives).
+// Progressive files fail.
+int parse_scan_headers(const uint8_t* data, size_t size, std::vector<ScanHeader>* hs);
 
 // hjd_ctx accessors for the other translation units
 int ctx_num_cu(const struct ::hjd_ctx* ctx);

@@ -748,18 +748,16 @@ int decode_one(const uint8_t* data, size_t size, hjd_jpeg_info* info, int16_t* c
 
 }  // namespace
 
-int hjd_internal::parse_scan_header(const uint8_t* data, size_t size, ScanHeader* h)
+namespace {
+
+// The header of the scan parse_segments() stopped at (f.scan), with the
+// frame's state (tables, DRI, quantisation) as of that scan.
+void fill_scan_header(const Frame& f, hjd_internal::ScanHeader* h)
 {
-    if (!data || !h) return set_error(HJD_E_INVALID, "NULL argument");
-    Frame f;
-    int rc = parse(data, size, f);
-    if (rc) return rc;
-    if (!single_scan(f))
-        return set_error(HJD_E_INVALID, "%s JPEG: the GPU entropy decoder takes one interleaved sequential scan "
-                         "(decode it with the host decoder, hjd_jpeg_decode_coefs / hjd_stream)",
-                         f.process == 2 ? "progressive" : "multi-scan");
+    const ScanSpec& sc = f.scan;
     hjd_jpeg_info info;
     fill_info(f, &info);
+    const CoefLayout L(f, info);
     h->width = f.width;
     h->height = f.height;
     h->sampling = f.sampling;
@@ -767,23 +765,34 @@ int hjd_internal::parse_scan_header(const uint8_t* data, size_t size, ScanHeader
     h->mcu_w = info.mcu_w;
     h->mcu_h = info.mcu_h;
     h->nblocks = info.nblocks;
-    h->scan_offset = f.scan_offset;
+    h->out_bpm = L.bpm;
+    h->scan_offset = sc.offset;
     memcpy(h->qt, info.qt, sizeof(h->qt));
+    h->extra_scans = f.ncomp - sc.ns;
     // bitstream block order of one MCU (src/decoder.cpp:308-344): scan components
     // in SOS order, H*V blocks each; output slot = Y blocks, then Cb, then Cr.
-    const int nblk_c[3] = {f.ncomp == 1 ? 1 : f.comp[0].h * f.comp[0].v, 1, 1};
-    const int blk_base[3] = {0, nblk_c[0], nblk_c[0] + 1};
+    // A one-component scan of a multi-component frame is non-interleaved: one
+    // block per MCU, the component's blocks in raster order (T.81 A.2.2).
+    h->layout = sc.ns == 1 && f.ncomp > 1 ? 1 : 0;
     int j = 0;
-    for (int si = 0; si < f.ncomp; ++si) {
-        const int c = f.scan_order[si];
-        for (int b = 0; b < nblk_c[c]; ++b, ++j) {
+    for (int si = 0; si < sc.ns; ++si) {
+        const int c = sc.comp[si];
+        const int nb = h->layout ? 1 : L.hs[c] * L.vs[c];
+        for (int b = 0; b < nb; ++b, ++j) {
             h->jcomp[j] = c;
             h->jdc[j] = f.comp[c].td;
             h->jac[j] = f.comp[c].ta;
-            h->jslot[j] = blk_base[c] + b;
+            h->jslot[j] = L.base[c] + b;
         }
     }
     h->bpm = j;
+    const int c0 = sc.comp[0];
+    h->comp_bw = L.bw[c0];
+    h->comp_bh = L.bh[c0];
+    h->comp_lh = L.hs[c0] >> 1;   // sampling factors 1, 2 or 4
+    h->comp_lv = L.vs[c0] >> 1;
+    h->scan_blocks = h->layout ? static_cast<int64_t>(L.bw[c0]) * L.bh[c0]
+                               : static_cast<int64_t>(info.mcu_w) * info.mcu_h * h->bpm;
     for (int cls = 0; cls < 2; ++cls)
         for (int id = 0; id < 4; ++id) {
             const HuffTable& t = cls ? f.ac[id] : f.dc[id];
@@ -793,6 +802,67 @@ int hjd_internal::parse_scan_header(const uint8_t* data, size_t size, ScanHeader
             memcpy(h->symbols[cls][id], t.vals, static_cast<size_t>(t.nsym));
             h->nsym[cls][id] = t.nsym;
         }
+}
+
+// The byte after a scan's entropy-coded data: the first marker that is not
+// RSTn (stuffed FF00 and fill bytes skipped), or the end of the data.
+size_t scan_end(const uint8_t* d, size_t n, size_t p)
+{
+    while (p < n) {
+        const uint8_t* f = static_cast<const uint8_t*>(memchr(d + p, 0xFF, n - p));
+        if (!f) return n;
+        p = static_cast<size_t>(f - d);
+        if (p + 1 >= n) return n;
+        const uint8_t b = d[p + 1];
+        if (b == 0x00 || (b >= 0xD0 && b <= 0xD7)) p += 2;
+        else if (b == 0xFF) p += 1;
+        else return p;
+    }
+    return n;
+}
+
+}  // namespace
+
+int hjd_internal::parse_scan_header(const uint8_t* data, size_t size, ScanHeader* h)
+{
+    if (!data || !h) return set_error(HJD_E_INVALID, "NULL argument");
+    Frame f;
+    int rc = parse(data, size, f);
+    if (rc) return rc;
+    if (f.process == 2)
+        return set_error(HJD_E_INVALID, "progressive JPEG: the GPU entropy decoder takes sequential scans "
+                         "(decode it with the host decoder, hjd_jpeg_decode_coefs / hjd_stream)");
+    fill_scan_header(f, h);
+    return HJD_OK;
+}
+
+int hjd_internal::parse_scan_headers(const uint8_t* data, size_t size, std::vector<ScanHeader>* hs)
+{
+    if (!data || !hs) return set_error(HJD_E_INVALID, "NULL argument");
+    hs->clear();
+    Frame f;
+    int rc = parse(data, size, f);
+    if (rc) return rc;
+    if (f.process == 2)
+        return set_error(HJD_E_INVALID, "progressive JPEG: the GPU entropy decoder takes sequential scans "
+                         "(decode it with the host decoder, hjd_jpeg_decode_coefs / hjd_stream)");
+    bool seen[3] = {false, false, false};
+    for (;;) {
+        for (int i = 0; i < f.scan.ns; ++i) {
+            if (seen[f.scan.comp[i]])   // T.81 B.2.3: a sequential frame codes each component in one scan
+                return set_error(HJD_E_INVALID, "component %d in two sequential scans", f.scan.comp[i]);
+            seen[f.scan.comp[i]] = true;
+        }
+        hs->emplace_back();
+        fill_scan_header(f, &hs->back());
+        size_t p = scan_end(data, size, f.scan.offset);
+        bool eoi = false;
+        rc = parse_segments(data, size, &p, f, true, &eoi);
+        if (rc) return rc;
+        if (eoi) break;
+    }
+    for (int c = 0; c < f.ncomp; ++c)
+        if (!seen[c]) return set_error(HJD_E_INVALID, "component %d is in no scan", c);
     return HJD_OK;
 }
 

@@ -3,7 +3,8 @@ only the C ABI (include/hjd.h, include/hjd_host.h) and the HIP runtime for
 device buffers -- turns JPEG files into the reference program's 32-bpp BMP
 files.  Pixels must equal the reference's BGRX on its golden sample, and the
 oracle's pixels on the host-decoded coefficients of the other files (GPU
-Huffman path, and the host-Huffman + plan path for a progressive file)."""
+Huffman path for sequential files with one scan or several, and the
+host-Huffman + plan path for a progressive file)."""
 import io
 import os
 import subprocess
@@ -12,6 +13,7 @@ import tempfile
 import numpy as np
 import pytest
 
+import jpeg_writer as JW
 import oracle_py as O
 
 pytestmark = pytest.mark.gpu
@@ -35,6 +37,8 @@ def test_c_program_decodes_to_bmp(hjd):
         b = io.BytesIO()
         Image.fromarray(img).save(b, format="JPEG", **kw)
         files[name] = b.getvalue()
+    base = files["q85_444.jpg"]
+    files["3scan_444.jpg"] = JW.rewrite_scans(base, hjd.decode_coefs(base)[0], [(2,), (0,), (1,)], 4)[0]
     with tempfile.TemporaryDirectory() as d:
         paths = []
         for name, data in files.items():
@@ -51,3 +55,6 @@ def test_c_program_decodes_to_bmp(hjd):
                 np.testing.assert_array_equal(got, O.decode_q16(coefs, np.array(info.qt), info.width, info.height,
                                                                 info.sampling))
         assert "process 2" in p.stdout
+        lines = {ln.split(":")[0].rsplit("/", 1)[-1]: ln for ln in p.stdout.splitlines()}
+        assert "scans several" in lines["3scan_444.jpg"] and "(GPU Huffman)" in lines["3scan_444.jpg"]
+        assert "(host Huffman)" in lines["prog_420.jpg"]

@@ -120,12 +120,62 @@ def test_multiscan_gray_and_sof1(hjd):
     np.testing.assert_array_equal(c1, c0)
 
 
-def test_gpu_entropy_emulation_rejects_multiscan(hjd):
-    """The GPU entropy decoder takes one interleaved sequential scan; other
-    files fail loudly there (and decode on the host path)."""
+def test_gpu_entropy_emulation_rejects_progressive(hjd):
+    """The GPU entropy decoder takes sequential scans; a progressive file fails
+    loudly there (and decodes on the host path)."""
     _, prog = _pair(32, 32, 2, "RGB")
     with pytest.raises(RuntimeError, match="progressive"):
         hjd.emulate_entropy(prog)
+
+
+@pytest.mark.parametrize("scans", [
+    [(0,), (1,), (2,)],
+    [(0,), (1, 2)],
+    [(2,), (0,), (1,)],
+    [(1, 2), (0,)],
+])
+@pytest.mark.parametrize("sub", [0, 1, 2])
+@pytest.mark.parametrize("dri", [0, 4])
+@pytest.mark.parametrize("spec", ["0", "1"])
+def test_gpu_entropy_emulation_multiscan(hjd, monkeypatch, scans, sub, dri, spec):
+    """The GPU entropy algorithm (host emulation of the kernels) on sequential
+    files with several scans: each scan is an entropy frame of its own
+    (kLayoutMcu for interleaved scans, kLayoutRaster for one component) and
+    all of them write the file's MCU-major coefficients -- exactly the host
+    decoder's, padding blocks zero; round-based and speculative sync, short
+    subsequences so that every scan spans several groups."""
+    from PIL import Image
+    monkeypatch.setenv("HJD_SYNC_SPEC", spec)
+    w, h = 181, 97
+    b = io.BytesIO()
+    Image.fromarray(_image(w, h, seed=sub + 3)).save(b, format="JPEG", quality=90, subsampling=sub)
+    base = b.getvalue()
+    c0, _ = hjd.decode_coefs(base)
+    data, expect = JW.rewrite_scans(base, c0, scans, dri)
+    for sub_bits in (48, 0):
+        c1, status = hjd.emulate_entropy(data, sub_bits)
+        np.testing.assert_array_equal(c1, expect, err_msg=f"S={sub_bits}")
+        assert status & ~1 == 0
+
+
+def test_gpu_entropy_emulation_multiscan_damaged(hjd):
+    """A damaged later scan is reported, never decoded silently as valid."""
+    from PIL import Image
+    b = io.BytesIO()
+    Image.fromarray(_image(120, 80)).save(b, format="JPEG", quality=85, subsampling=2)
+    base = b.getvalue()
+    c0, _ = hjd.decode_coefs(base)
+    data, expect = JW.rewrite_scans(base, c0, [(0,), (1,), (2,)], 0)
+    last = data.rindex(b"\xff\xda")
+    bad = bytearray(data)
+    bad[last + 30:last + 50] = b"\x00" * 20
+    try:
+        c1, _ = hjd.emulate_entropy(bytes(bad))
+    except RuntimeError:
+        return                                  # reported as corrupt
+    # accepted: then the host decoder accepts it too, with the same coefficients
+    ref, _ = hjd.decode_coefs(bytes(bad))
+    np.testing.assert_array_equal(c1, ref)
 
 
 @pytest.mark.parametrize("marker", [0xC3, 0xC9, 0xCA])   # lossless, arithmetic
