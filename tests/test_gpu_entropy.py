@@ -335,8 +335,8 @@ def test_progressive_rejected_loudly(hjd, ctx):
 
 
 def _mutants(seeds, n, seed):
-    """Damaged copies of single-scan JPEGs (byte flips, 0xFF / RSTn insertions,
-    truncation) that still parse as single-scan files."""
+    """Damaged copies of sequential JPEGs (byte flips, 0xFF / RSTn insertions,
+    truncation) that still parse as sequential files (one scan or several)."""
     import ocljpegdecoder_amd as hjd
     rng = np.random.default_rng(seed)
     out = []
@@ -357,13 +357,14 @@ def _mutants(seeds, n, seed):
             info = hjd.parse(bytes(d))
         except Exception:
             continue
-        if info.single_scan and 0 < info.nblocks <= 4096:
+        if info.process != 2 and 0 < info.nblocks <= 4096:
             out.append(bytes(d))
     return out
 
 
+@pytest.mark.parametrize("multiscan", [False, True])
 @pytest.mark.parametrize("pinned", [False, True])
-def test_damaged_files_on_device(hjd, ctx, pinned):
+def test_damaged_files_on_device(hjd, ctx, pinned, multiscan):
     """Damaged JPEGs through the device decoder (host destuff for pageable
     bytes, the device destuff kernels for pinned ones) in batches of 8: no
     fault, no write outside the batch's coefficient blocks (guard blocks keep
@@ -373,7 +374,12 @@ def test_damaged_files_on_device(hjd, ctx, pinned):
     import torch
     seeds = [_pil(256, 128, 90, 2, seed=31), _pil(160, 96, 95, 0, seed=32, restart_marker_blocks=5),
              _pil(200, 100, 75, 1, seed=33)]
-    muts = _mutants(seeds, 96, seed=5 + int(pinned))
+    if multiscan:   # the same images as sequential files with several scans
+        import jpeg_writer as JW
+        splits = [[(0,), (1,), (2,)], [(1, 2), (0,)], [(2,), (0, 1)]]
+        seeds = [JW.rewrite_scans(d, hjd.decode_coefs(d)[0], splits[k], 4 if k == 1 else 0)[0]
+                 for k, d in enumerate(seeds)]
+    muts = _mutants(seeds, 96, seed=5 + int(pinned) + 2 * int(multiscan))
     guard = 64
     checked = flagged = staged_out = 0
     # every batch also holds two undamaged files, which must come out clean and

@@ -1,7 +1,7 @@
 // Robustness harness for the GPU entropy decoder's algorithm, run on the CPU
 // with AddressSanitizer + UBSan (tools/fuzz/run_entropy.sh): mutates JPEG
-// files (byte flips, 0xFF runs, truncation) and decodes every single-scan
-// mutant with hjd_debug_entropy_emulate -- the host build of the same
+// files (byte flips, 0xFF runs, truncation) and decodes every sequential
+// mutant (one scan or several) with hjd_debug_entropy_emulate -- the host build of the same
 // destuff, sync/link/repair (round-based and speculative) and write code the
 // gfx950 kernels run, over
 // buffers laid out as on the device (each frame's bit string followed by its
@@ -35,7 +35,7 @@ int main(int argc, char** argv)
         for (int c; (c = fgetc(fp)) != EOF;) src.push_back(static_cast<uint8_t>(c));
         fclose(fp);
         hjd_jpeg_info info;
-        if (hjd_jpeg_parse(src.data(), src.size(), &info) || !info.single_scan) continue;
+        if (hjd_jpeg_parse(src.data(), src.size(), &info) || info.process == 2) continue;
         for (int i = 0; i < iters; ++i) {
             std::vector<uint8_t> d = src;
             const int nflip = 1 + static_cast<int>(rng() % 8);
@@ -50,7 +50,7 @@ int main(int argc, char** argv)
             uint8_t* buf = static_cast<uint8_t*>(malloc(d.size()));
             std::copy(d.begin(), d.end(), buf);
             hjd_jpeg_info mi;
-            if (hjd_jpeg_parse(buf, d.size(), &mi) != HJD_OK || !mi.single_scan || mi.nblocks <= 0 ||
+            if (hjd_jpeg_parse(buf, d.size(), &mi) != HJD_OK || mi.process == 2 || mi.nblocks <= 0 ||
                 mi.nblocks > 1 << 20) {
                 ++rejected;
                 free(buf);

@@ -1,7 +1,7 @@
 #!/bin/bash
 # CPU-only: build the GPU entropy decoder's host emulation (hjd_entropy.hip and
 # what it links against) with host-side AddressSanitizer + UBSan, and fuzz it
-# on damaged single-scan JPEGs (tools/fuzz/entropy_emulate_fuzz.cpp).
+# on damaged sequential JPEGs, one scan or several (tools/fuzz/entropy_emulate_fuzz.cpp).
 set -eu
 R=$(cd "$(dirname "$0")/../.." && pwd)
 O=${TMPDIR:-/tmp}/hjd_efuzz
