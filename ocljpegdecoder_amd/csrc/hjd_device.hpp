@@ -99,6 +99,43 @@ __host__ __device__ __forceinline__ void idct8(int (&v)[8])
     }
 }
 
+// The column pass of idct8<true, kLevel> with each result in the HIGH int16
+// of its word (the low half is junk): the kernel stores it with
+// ds_write_b16_d16_hi, so no output needs its own shift.  Every value from the
+// even part's DC on is carried at 4x scale (r' = 4r, exact in int32: |r| <
+// 2^23 on the legal domain, and the sums are mod 2^32 anyway), so hi16(r') =
+// floor(r' / 2^16) = r >> 14, and the clamp is a med3 against bounds scaled
+// the same way.  The stage-1/2 products keep the reference's (+4) >> 3 at
+// unit scale and are scaled after it (x4 in the final add chains); the
+// stage-3 terms 4 * floor((181 s + 128) / 256) = ((181 s + 128) >> 6) & ~3.
+template <int kLevel = 0>
+__host__ __device__ __forceinline__ void idct8_col_hi(int (&v)[8])
+{
+    int e0 = v[0] * 1024 + (8192 + (kLevel << 14)) * 4;
+    const int e1 = v[4] * 1024;
+    int t = mul24(kC7, v[1] + v[7]) + 4;
+    const int o4 = (t + mul24(kC1 - kC7, v[1])) >> 3;
+    const int o5 = (t - mul24(kC1 + kC7, v[7])) >> 3;
+    t = mul24(kC3, v[5] + v[3]) + 4;
+    const int o6 = (t - mul24(kC3 - kC5, v[5])) >> 3;
+    const int o7 = (t - mul24(kC3 + kC5, v[3])) >> 3;
+    const int e8 = e0 + e1;
+    e0 -= e1;
+    t = mul24(kC6, v[2] + v[6]) + 4;
+    const int e2 = ((t - mul24(kC2 + kC6, v[6])) >> 3) * 4;
+    const int e3 = ((t + mul24(kC2 - kC6, v[2])) >> 3) * 4;
+    const int a1 = (o4 + o6) * 4, a4 = o4 - o6;
+    const int a6 = (o5 + o7) * 4, a5 = o5 - o7;
+    const int f7 = e8 + e3, f8 = e8 - e3;
+    const int f3 = e0 + e2, f0 = e0 - e2;
+    const int g2 = ((mul181(a4 + a5) + 128) >> 6) & ~3;
+    const int g4 = ((mul181(a4 - a5) + 128) >> 6) & ~3;
+    constexpr int lo = (-256 + kLevel) * 65536, hi = (255 + kLevel) * 65536 + 65535;
+    auto clampw = [](int x) { return x < lo ? lo : (x > hi ? hi : x); };
+    v[0] = clampw(f7 + a1); v[1] = clampw(f3 + g2); v[2] = clampw(f0 + g4); v[3] = clampw(f8 + a6);
+    v[4] = clampw(f8 - a6); v[5] = clampw(f0 - g4); v[6] = clampw(f3 - g2); v[7] = clampw(f7 - a1);
+}
+
 // ---- row pass on packed int16 pairs (the pixel kernel's hot form) -----------
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 
@@ -119,6 +156,18 @@ __host__ __device__ __forceinline__ int sdot2(s16x2 a, s16x2 b)
     return r;
 #else
     return static_cast<int>(a.x) * b.x + static_cast<int>(a.y) * b.y + kC;
+#endif
+}
+
+// a.x*b.x + a.y*b.y + c with c in a VGPR (an accumulation chain of dot2s).
+__host__ __device__ __forceinline__ int sdot2acc(s16x2 a, s16x2 b, int c)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    int r;
+    asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(b), "v"(c));
+    return r;
+#else
+    return static_cast<int>(a.x) * b.x + static_cast<int>(a.y) * b.y + c;
 #endif
 }
 
@@ -153,19 +202,19 @@ __host__ __device__ __forceinline__ void idct8_row_pk(const RowPk& p, int (&v)[8
     const s16x2 k4 = const_pair(kC1, kC7), k5 = const_pair(kC7, -kC1);
     const s16x2 k6 = const_pair(kC3, kC5), k7 = const_pair(-kC5, kC3);
     const s16x2 k3 = const_pair(kC2, kC6), k2 = const_pair(kC6, -kC2);
+    const s16x2 k6n = const_pair(-kC3, -kC5), k7n = const_pair(kC5, -kC3);
+    const s16x2 k3n = const_pair(-kC2, -kC6), k2n = const_pair(-kC6, kC2);
     const int e8 = sdot2<128>(p.p04, k0p);   // (b0 << 11) + 128 + (b4 << 11)
     const int e0 = sdot2<128>(p.p04, k0m);   // (b0 << 11) + 128 - (b4 << 11)
     const int o4 = sdot2<0>(p.p17, k4);
     const int o5 = sdot2<0>(p.p17, k5);
-    const int o6 = sdot2<0>(p.p35, k6);
-    const int o7 = sdot2<0>(p.p35, k7);
-    const int e3 = sdot2<0>(p.p26, k3);
-    const int e2 = sdot2<0>(p.p26, k2);
-
-    const int a1 = o4 + o6, a4 = o4 - o6;
-    const int a6 = o5 + o7, a5 = o5 - o7;
-    const int f7 = e8 + e3, f8 = e8 - e3;
-    const int f3 = e0 + e2, f0 = e0 - e2;
+    // the stage-2 sums and differences accumulate onto the stage-1 products:
+    // one dot2 each instead of a dot2 per product plus an add per sum
+    // (o6 = (b3,b5).k6, o7 = (b3,b5).k7, e3 = (b2,b6).k3, e2 = (b2,b6).k2)
+    const int a1 = sdot2acc(p.p35, k6, o4), a4 = sdot2acc(p.p35, k6n, o4);   // o4 +- o6
+    const int a6 = sdot2acc(p.p35, k7, o5), a5 = sdot2acc(p.p35, k7n, o5);   // o5 +- o7
+    const int f7 = sdot2acc(p.p26, k3, e8), f8 = sdot2acc(p.p26, k3n, e8);   // e8 +- e3
+    const int f3 = sdot2acc(p.p26, k2, e0), f0 = sdot2acc(p.p26, k2n, e0);   // e0 +- e2
     const int g2 = (mul181(a4 + a5) + 128) >> 8;
     const int g4 = (mul181(a4 - a5) + 128) >> 8;
     v[0] = (f7 + a1) >> 8; v[1] = (f3 + g2) >> 8; v[2] = (f0 + g4) >> 8; v[3] = (f8 + a6) >> 8;
@@ -189,10 +238,12 @@ __host__ __device__ __forceinline__ void idct8_row_pk(const RowPk& p, int (&v)[8
 //   * every chroma term is produced in the HIGH int16 of a 32-bit word, so
 //     one v_perm per channel assembles the int16 pair of two pixels:
 //       floor(1.402 v)               = hi16(v * 91881)
-//       floor(1.772 u)               = hi16(u * 116130 + 52)
+//       floor(1.772 u)               = hi16(u * 116130), except at u = -250
+//         (one below: -444; Ys + B <= 383 - 443 < 0 there, so B saturates
+//         to 0 either way and the pixel is the same)
 //       floor(-(17207u+35707v)/50000) = hi16(mulhi_i32(128*(-17207u-35707v), 43980466))
-//     (43980466 = ceil(2^48 / 6.4e6)).  The first two are 24-bit multiplies
-//     (R's reads the packed sample through SDWA, no extraction), the third
+//     (43980466 = ceil(2^48 / 6.4e6)).  All four products are 24-bit
+//     multiplies reading the packed sample through SDWA (no extraction); the third
 //     is exact except where the division is exact with a negative quotient:
 //     (U,V) = (-200,200) and (-100,100), the only grid points whose mulhi
 //     has low half 0xffff (every other point's is <= 0xfffe).  There the
@@ -206,7 +257,7 @@ __host__ __device__ __forceinline__ void idct8_row_pk(const RowPk& p, int (&v)[8
 // ---------------------------------------------------------------------------
 constexpr int kLumaLevel = 128;    // Ys = Y + 128, folded into the luma IDCT
 constexpr int kRK = 91881;         // floor(1.402 v) = (v * kRK) >> 16
-constexpr int kBK = 116130, kBBias = 52;   // floor(1.772 u) = (u * kBK + kBBias) >> 16
+constexpr int kBK = 116130;        // floor(1.772 u) = (u * kBK) >> 16 but at u = -250 (saturated)
 constexpr int kGScale = 128;
 constexpr int kGKu = -17207 * kGScale, kGKv = -35707 * kGScale;   // 24-bit signed
 constexpr int kGMagic = 43980466;  // ceil(2^48 / (50000 * kGScale))
@@ -243,23 +294,16 @@ __device__ __forceinline__ int mul24_half(uint32_t w, int k)
     return r;
 }
 
-template <int kHalf>
-__device__ __forceinline__ int half_of(uint32_t w)
-{
-    return kHalf == 0 ? static_cast<short>(w) : static_cast<int>(w) >> 16;
-}
-
 // Chroma terms of the (U,V) sample held in int16 half kHalf of the packed
-// words uw, vw.  V goes through SDWA multiplies only; U is unpacked once for
-// the two 24-bit multiply-adds (B, and G's sum).
+// words uw, vw: four SDWA 24-bit multiplies (no sample is unpacked), one add
+// and G's mulhi.
 template <int kHalf>
 __device__ __forceinline__ ChromaTerms chroma_terms(uint32_t uw, uint32_t vw)
 {
-    const int u = half_of<kHalf>(uw);
     ChromaTerms t;
     t.r = static_cast<uint32_t>(mul24_half<kHalf>(vw, kRK));
-    t.b = static_cast<uint32_t>(mul24(u, kBK) + kBBias);
-    t.g = static_cast<uint32_t>(g_mulhi(mul24(u, kGKu) + mul24_half<kHalf>(vw, kGKv)));
+    t.b = static_cast<uint32_t>(mul24_half<kHalf>(uw, kBK));
+    t.g = static_cast<uint32_t>(g_mulhi(mul24_half<kHalf>(uw, kGKu) + mul24_half<kHalf>(vw, kGKv)));
     return t;
 }
 

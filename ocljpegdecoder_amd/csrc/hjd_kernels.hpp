@@ -674,13 +674,14 @@ __device__ __forceinline__ void idct_stage(char* __restrict__ slots, char* __res
                 load_round_i32<kSampling>(lane, i + 1, src32, nblk, v);
         }
         if (round_component<kSampling>(i) == 0)
-            idct8<true, kLumaLevel>(c8);   // luma leaves the IDCT level-shifted (Ys = Y + 128)
+            idct8_col_hi<kLumaLevel>(c8);   // luma leaves the IDCT level-shifted (Ys = Y + 128)
         else
-            idct8<true>(c8);
+            idct8_col_hi(c8);
         {
-            char* blk = slots + b * kSlotBytes + r * 2;   // column r
+            char* blk = slots + b * kSlotBytes + r * 2;   // column r; the samples are the words' high halves
 #pragma unroll
-            for (int k = 0; k < 8; ++k) *reinterpret_cast<short*>(blk + k * 16) = static_cast<short>(c8[k]);
+            for (int k = 0; k < 8; ++k)
+                *reinterpret_cast<short*>(blk + k * 16) = static_cast<short>(static_cast<uint32_t>(c8[k]) >> 16);
         }
         wave_lds_sync();
     }
@@ -929,13 +930,14 @@ __global__ __launch_bounds__(kLatThreads) void decode_kernel_lat(const void* __r
         for (int k = 0; k < 8; ++k) c8[k] = *reinterpret_cast<const int*>(col + k * kRowStride);
     }
     if (round_is_luma<kSampling>(wave))
-        idct8<true, kLumaLevel>(c8);
+        idct8_col_hi<kLumaLevel>(c8);
     else
-        idct8<true>(c8);
+        idct8_col_hi(c8);
     {
-        char* blk = slots + b * kSlotBytes + r * 2;   // column r
+        char* blk = slots + b * kSlotBytes + r * 2;   // column r; the samples are the words' high halves
 #pragma unroll
-        for (int k = 0; k < 8; ++k) *reinterpret_cast<short*>(blk + k * 16) = static_cast<short>(c8[k]);
+        for (int k = 0; k < 8; ++k)
+            *reinterpret_cast<short*>(blk + k * 16) = static_cast<short>(static_cast<uint32_t>(c8[k]) >> 16);
     }
     __syncthreads();   // all 48 blocks' samples are in the slots
 

@@ -97,7 +97,7 @@ def test_oracle_csc_exhaustive_hash():
 # Constants of the device formulation (csrc/hjd_device.hpp colour block).
 LEVEL = 128                      # luma leaves the IDCT as Ys = Y + 128
 RK = 91881                       # floor(1.402 v) = (v * RK) >> 16
-BK, BBIAS = 116130, 52           # floor(1.772 u) = (u * BK + BBIAS) >> 16
+BK = 116130                      # floor(1.772 u) = (u * BK) >> 16, except u = -250 (one below; B saturates to 0 there)
 GSCALE = 128
 GKU, GKV = -17207 * GSCALE, -35707 * GSCALE
 GMAGIC = 43980466                # ceil(2^48 / (50000 * GSCALE))
@@ -111,7 +111,7 @@ def integer_csc(y, u, v):
     y = y.astype(np.int64); u = u.astype(np.int64); v = v.astype(np.int64)
     ys = y + LEVEL
     r = (v * RK) >> 16
-    b = (u * BK + BBIAS) >> 16
+    b = (u * BK) >> 16
     hi = ((u * GKU + v * GKV) * GMAGIC) >> 32       # v_mul_hi_i32
     g = hi >> 16
     flagged = (hi & 0xFFFF) == 0xFFFF
@@ -127,7 +127,11 @@ def test_fixed_point_colour_terms():
     """The constants of the device formulation, exhaustively on their domains."""
     x = np.arange(-256, 256, dtype=np.int64)
     assert ((x * RK) >> 16 == np.floor_divide(701 * x, 500)).all()
-    assert ((x * BK + BBIAS) >> 16 == np.floor_divide(443 * x, 250)).all()
+    b = (x * BK) >> 16
+    exact = np.floor_divide(443 * x, 250)
+    assert (b[x != -250] == exact[x != -250]).all() and b[x == -250] == exact[x == -250] - 1
+    # ... where Ys + B <= (255 + LEVEL) - 443 < 0: the blue channel saturates to 0 either way
+    assert (255 + LEVEL) + exact[x == -250] < 0
     assert max(RK, BK, -GKU, -GKV) < 2 ** 23        # 24-bit signed multiplies
     assert GMAGIC < 2 ** 31 and GMAGIC == -(-(1 << 48) // (50000 * GSCALE))
     u, v = np.meshgrid(x, x, indexing="ij")
