@@ -1016,17 +1016,12 @@ __device__ __forceinline__ SlotRow row_load(const uint32_t* p)
 }
 
 // f then g: (g . f)(s) = g(f(s)), kNoCand absorbing; bytes past kChainSlots stay kNoCand
+// (slot_compose, hjd_entropy.hpp: byte permutes, no per-slot selects)
+static_assert(kRowWords == 5 && kNoCand == 0xFF, "slot_compose's row format");
 __device__ __forceinline__ SlotRow row_compose(const SlotRow& f, const SlotRow& g)
 {
     SlotRow r;
-#pragma unroll
-    for (int i = 0; i < kRowWords; ++i) r.w[i] = 0xFFFFFFFFu;
-#pragma unroll
-    for (int s = 0; s < kChainSlots; ++s) {
-        const uint32_t a = row_get(f, static_cast<uint32_t>(s));
-        const uint32_t v = a == kNoCand ? kNoCand : row_get(g, a);
-        r.w[s >> 2] = (r.w[s >> 2] & ~(0xFFu << ((s & 3) * 8))) | (v << ((s & 3) * 8));
-    }
+    slot_compose(f.w, g.w, r.w);
     return r;
 }
 

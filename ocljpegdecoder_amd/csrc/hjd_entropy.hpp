@@ -670,5 +670,51 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
     return result;
 }
 
+// ---- slot maps of the speculative sync's chain kernel ----------------------
+// A slot map is 20 bytes (5 dwords): byte s = the slot of the next
+// subsequence that slot s leads to, < 20, or 0xFF (none; absorbing).
+// Composition r = g . f, r[s] = g[f[s]], as three byte permutes per dword
+// (v_perm_b32 picks 4 bytes out of 8 by the selector bytes 0..7; selector
+// bytes >= 13 give 0xFF) and a per-byte select on bits 3 and 4 of f's bytes:
+// bytes 0-7 of g from (g0, g1), 8-15 from (g2, g3) with the selector's bit 3
+// flipped, 16-19 from g4 with bit 4 flipped; a 0xFF selector has bit 4 set and
+// flips to 0xEF, which the permute turns into 0xFF.
+__host__ __device__ __forceinline__ uint32_t byte_perm(uint32_t hi, uint32_t lo, uint32_t sel)
+{
+#ifdef __HIP_DEVICE_COMPILE__
+    return __builtin_amdgcn_perm(hi, lo, sel);
+#else
+    uint32_t r = 0;
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t k = (sel >> (8 * i)) & 0xFF;
+        uint32_t b;
+        if (k < 4) b = (lo >> (8 * k)) & 0xFF;
+        else if (k < 8) b = (hi >> (8 * (k - 4))) & 0xFF;
+        else if (k == 12) b = 0;
+        else if (k >= 13) b = 0xFF;
+        else {   // 8..11: sign of a 16-bit half (unused here)
+            const uint32_t w = k < 10 ? lo : hi;
+            b = ((w >> ((k & 1) ? 31 : 15)) & 1) ? 0xFF : 0;
+        }
+        r |= b << (8 * i);
+    }
+    return r;
+#endif
+}
+
+__host__ __device__ __forceinline__ void slot_compose(const uint32_t (&f)[5], const uint32_t (&g)[5], uint32_t (&r)[5])
+{
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        const uint32_t idx = f[i];
+        const uint32_t lo = byte_perm(g[1], g[0], idx);
+        const uint32_t mid = byte_perm(g[3], g[2], idx ^ 0x08080808u);
+        const uint32_t hi = byte_perm(g[4], g[4], idx ^ 0x10101010u);
+        const uint32_t m3 = ((idx >> 3) & 0x01010101u) * 0xFFu;   // bytes >= 8 (bit 3)
+        const uint32_t m4 = ((idx >> 4) & 0x01010101u) * 0xFFu;   // bytes >= 16 and 0xFF (bit 4)
+        r[i] = (hi & m4) | (~m4 & ((mid & m3) | (lo & ~m3)));
+    }
+}
+
 }  // namespace ent
 }  // namespace hjd
