@@ -443,6 +443,8 @@ struct EntBatchDev {
     uint32_t* status;
     int16_t* coefs;
     uint32_t nframes, nwg, sub_bits, ntab_max;   // ntab_max: tables of the largest frame (dynamic LDS)
+    uint32_t ntab_total;                         // tables of the batch
+    uint8_t* steps_g;                            // [table][1 << kStepBits] AC step entries (ent_steps_kernel)
     uint32_t nsub_total;                         // subsequences of the batch
     // device destuff (ntiles == 0: every frame of the batch was destuffed on the host)
     const uint8_t* raw;          // raw scan bytes, frame f at frames[f].data_off
@@ -485,6 +487,15 @@ __host__ __device__ __forceinline__ void fill_steps(uint8_t* steps, const HuffLu
 {
     for (int i = tid; i < (ntab << kStepBits); i += nthreads)
         steps[i] = step_entry(tabs[i >> kStepBits], static_cast<uint32_t>(i) & ((1u << kStepBits) - 1));
+}
+
+// A frame's step tables from the batch's (ent_steps_kernel) into LDS.
+__device__ __forceinline__ void copy_steps(uint8_t* steps, const EntBatchDev& b, const EntFrame& F, int tid,
+                                           int nthreads)
+{
+    const uint4* src = reinterpret_cast<const uint4*>(b.steps_g + (static_cast<size_t>(F.tab_base) << kStepBits));
+    uint4* dst = reinterpret_cast<uint4*>(steps);
+    for (int i = tid; i < (F.ntab << kStepBits) / 16; i += nthreads) dst[i] = src[i];
 }
 
 // Host side of the block records (the kernels fill their LDS copy per thread).
@@ -775,9 +786,8 @@ __global__ __launch_bounds__(kGroupSubs) void ent_sync_kernel(EntBatchDev b)
     __shared__ BlockInfo blocks[kMaxBpm];
     const RunCtx c = make_ctx(b, F, tabs, blocks, HJD_STEPS ? steps : nullptr);
     load_tables(tabs, blocks, b.tabs + F.tab_base, F, b.frames + f, tid, kGroupSubs);
+    copy_steps(steps, b, F, tid, kGroupSubs);
     if (tid < 2) L.nlist[tid] = 0;
-    __syncthreads();
-    fill_steps(steps, tabs, F.ntab, tid, kGroupSubs);
     __syncthreads();
     const int64_t k0 = group_sub(gl, 0);
     const int64_t k = k0 + tid;
@@ -912,6 +922,29 @@ __global__ __launch_bounds__(kGroupSubs) void ent_sync_kernel(EntBatchDev b)
     }
 }
 
+// The AC step tables of every Huffman table of the batch, once per batch (the
+// sync / spec / cand kernels copy their frame's from here instead of each
+// workgroup deriving them from the LUTs).  One group per table, 4 entries
+// (one dword) per thread and pass.
+constexpr int kStepsThreads = 256;
+__global__ __launch_bounds__(kStepsThreads) void ent_steps_kernel(EntBatchDev b)
+{
+    __shared__ HuffLut t;
+    const uint32_t ti = blockIdx.x;
+    const int tid = threadIdx.x;
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(b.tabs + ti);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&t);
+    for (int i = tid; i < static_cast<int>(sizeof(HuffLut) / 4); i += kStepsThreads) dst[i] = src[i];
+    __syncthreads();
+    uint32_t* out = reinterpret_cast<uint32_t*>(b.steps_g + (static_cast<size_t>(ti) << kStepBits));
+    for (int q = tid; q < (1 << kStepBits) / 4; q += kStepsThreads) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w |= static_cast<uint32_t>(step_entry(t, static_cast<uint32_t>(4 * q + e))) << (8 * e);
+        out[q] = w;
+    }
+}
+
 // ---- speculative sync (latency decoders) ------------------------------------
 // Grid (groups, kMaxBpm): block (w, j) runs guess j of group w's owned
 // subsequences (the warm-up ones belong to the previous group).
@@ -928,8 +961,7 @@ __global__ __launch_bounds__(kGroupSubs) void ent_spec_kernel(EntBatchDev b)
     const uint32_t gl = w - F.wg_base;
     if (gl >= frame_groups(F.nsub) || j >= F.bpm) return;
     load_tables(tabs, blocks, b.tabs + F.tab_base, F, b.frames + f, tid, kGroupSubs);
-    __syncthreads();
-    fill_steps(steps, tabs, F.ntab, tid, kGroupSubs);
+    copy_steps(steps, b, F, tid, kGroupSubs);
     __syncthreads();
     const int64_t k = group_sub(gl, tid);
     if (tid < kWarm || k >= static_cast<int64_t>(F.nsub)) return;
@@ -958,8 +990,7 @@ __global__ __launch_bounds__(kGroupSubs) void ent_cand_kernel(EntBatchDev b)
     const uint32_t gl = w - F.wg_base;
     if (gl >= frame_groups(F.nsub) || i >= F.bpm) return;
     load_tables(tabs, blocks, b.tabs + F.tab_base, F, b.frames + f, tid, kGroupSubs);
-    __syncthreads();
-    fill_steps(steps, tabs, F.ntab, tid, kGroupSubs);
+    copy_steps(steps, b, F, tid, kGroupSubs);
     __syncthreads();
     const int64_t k = group_sub(gl, tid);
     if (tid < kWarm || k >= static_cast<int64_t>(F.nsub)) return;
@@ -1901,6 +1932,7 @@ struct hjd_gdec {
     CandRec* d_cand = nullptr;
     uint8_t* d_cmap = nullptr;
     uint8_t* d_cslot = nullptr;
+    uint8_t* d_steps = nullptr;         // [table][1 << kStepBits] (ent_steps_kernel)
     hipEvent_t staged = nullptr, done = nullptr;
     int64_t last_h2d = 0;               // bytes the last issue moved host -> device
     int64_t last_host_scan_bytes = 0;   // scan bytes the host CPU read + wrote for the staged frames
@@ -2243,6 +2275,8 @@ int hjd_gdec::assemble(uint8_t* blob, int16_t* coefs, int64_t* block_offsets, vo
     d.sub_bits = S;
     d.ntab_max = 1;
     for (const Prepared* p : ents) d.ntab_max = std::max<uint32_t>(d.ntab_max, static_cast<uint32_t>(p->ntab));
+    d.ntab_total = tab_base;
+    d.steps_g = nullptr;
     return HJD_OK;
 }
 
@@ -2272,6 +2306,8 @@ int gdec_alloc(hjd_gdec* g)
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_coefs), 128 * static_cast<size_t>(g->caps.max_blocks)));
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_raw), g->data_cap()));
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_tiles), 12 * static_cast<size_t>(g->caps.max_tiles)));
+    HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_steps),
+                      (static_cast<size_t>(kMaxTables) * kMaxScans * static_cast<size_t>(g->caps.max_frames)) << kStepBits));
     if (g->spec) {
         const size_t n = static_cast<size_t>(g->caps.max_subs);
         HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_spec), sizeof(SpecRec) * kMaxBpm * n));
@@ -2297,6 +2333,8 @@ int launch_entropy(hjd_gdec* g, const EntBatchDev& b, hipStream_t s)
         hipLaunchKernelGGL(destuff_write_kernel, dim3(b.ntiles), dim3(kTileThreads), 0, s, b);
         HJD_HIP(hipGetLastError());
     }
+    hipLaunchKernelGGL(ent_steps_kernel, dim3(b.ntab_total), dim3(kStepsThreads), 0, s, b);
+    HJD_HIP(hipGetLastError());
     if (b.spec) {   // speculative sync: latency decoders
         const size_t tl = (sizeof(HuffLut) + (1u << kStepBits)) * b.ntab_max;
         hipLaunchKernelGGL(ent_spec_kernel, dim3(b.nwg, kMaxBpm), dim3(kGroupSubs), tl, s, b);
@@ -2349,6 +2387,7 @@ int gdec_issue(hjd_gdec* g, void* const* d_outs, const int32_t* pitches, int16_t
     b.status = g->d_status;
     b.raw = g->d_raw;
     b.tiles = g->d_tiles;
+    b.steps_g = g->d_steps;
     if (g->spec) {
         b.spec = g->d_spec;
         b.cand = g->d_cand;
@@ -2587,7 +2626,8 @@ int hjd_gdec_destroy(hjd_gdec* g)
     if (g->h_stage) (void)hipHostFree(g->h_stage);
     if (g->h_status) (void)hipHostFree(g->h_status);
     void* dev[] = {g->d_blob, g->d_entries, g->d_stats, g->d_mids, g->d_stats1, g->d_wentries, g->d_linked, g->d_agg,
-                   g->d_status, g->d_coefs, g->d_raw, g->d_tiles, g->d_spec, g->d_cand, g->d_cmap, g->d_cslot};
+                   g->d_status, g->d_coefs, g->d_raw, g->d_tiles, g->d_spec, g->d_cand, g->d_cmap, g->d_cslot,
+                   g->d_steps};
     for (void* p : dev)
         if (p) (void)hipFree(p);
     if (g->staged) (void)hipEventDestroy(g->staged);
