@@ -924,9 +924,11 @@ __global__ __launch_bounds__(kGroupSubs) void ent_sync_kernel(EntBatchDev b)
 
 // The AC step tables of every Huffman table of the batch, once per batch (the
 // sync / spec / cand kernels copy their frame's from here instead of each
-// workgroup deriving them from the LUTs).  One group per table, 4 entries
-// (one dword) per thread and pass.
+// workgroup deriving them from the LUTs).  Grid (tables, kStepGroups): one
+// entry per thread, so the serial chain is one entry's few LUT lookups.
 constexpr int kStepsThreads = 256;
+constexpr int kStepGroups = (1 << kStepBits) / kStepsThreads;
+static_assert(kStepGroups * kStepsThreads == (1 << kStepBits), "step groups");
 __global__ __launch_bounds__(kStepsThreads) void ent_steps_kernel(EntBatchDev b)
 {
     __shared__ HuffLut t;
@@ -934,15 +936,10 @@ __global__ __launch_bounds__(kStepsThreads) void ent_steps_kernel(EntBatchDev b)
     const int tid = threadIdx.x;
     const uint32_t* src = reinterpret_cast<const uint32_t*>(b.tabs + ti);
     uint32_t* dst = reinterpret_cast<uint32_t*>(&t);
-    for (int i = tid; i < static_cast<int>(sizeof(HuffLut) / 4); i += kStepsThreads) dst[i] = src[i];
+    for (int i = tid; i < static_cast<int>(sizeof(t.lut) / 4); i += kStepsThreads) dst[i] = src[i];   // the LUT is all step_entry reads
     __syncthreads();
-    uint32_t* out = reinterpret_cast<uint32_t*>(b.steps_g + (static_cast<size_t>(ti) << kStepBits));
-    for (int q = tid; q < (1 << kStepBits) / 4; q += kStepsThreads) {
-        uint32_t w = 0;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) w |= static_cast<uint32_t>(step_entry(t, static_cast<uint32_t>(4 * q + e))) << (8 * e);
-        out[q] = w;
-    }
+    const uint32_t e = blockIdx.y * kStepsThreads + static_cast<uint32_t>(tid);
+    b.steps_g[(static_cast<size_t>(ti) << kStepBits) + e] = step_entry(t, e);
 }
 
 // ---- speculative sync (latency decoders) ------------------------------------
@@ -2333,7 +2330,7 @@ int launch_entropy(hjd_gdec* g, const EntBatchDev& b, hipStream_t s)
         hipLaunchKernelGGL(destuff_write_kernel, dim3(b.ntiles), dim3(kTileThreads), 0, s, b);
         HJD_HIP(hipGetLastError());
     }
-    hipLaunchKernelGGL(ent_steps_kernel, dim3(b.ntab_total), dim3(kStepsThreads), 0, s, b);
+    hipLaunchKernelGGL(ent_steps_kernel, dim3(b.ntab_total, kStepGroups), dim3(kStepsThreads), 0, s, b);
     HJD_HIP(hipGetLastError());
     if (b.spec) {   // speculative sync: latency decoders
         const size_t tl = (sizeof(HuffLut) + (1u << kStepBits)) * b.ntab_max;
