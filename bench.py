@@ -954,6 +954,9 @@ def main():
             "workload": wl4["desc"], "frames_per_gpu": wl4["frames"], "sampling": "4:4:4",
             "output_checked_vs_oracle": r4["output_check"]["ok"], "output_check": r4["output_check"],
             "roofline": roofline_obj(r4["_achieved"], r4["_bytes_per_launch"], r4["_kernel_ms"], traffic4, trace4),
+            "binding_limit": "VALU issue, not HBM: removing either the IDCT or the colour math leaves the "
+                             "kernel at its memory time, ~9 % faster (ablation, "
+                             "profiles/r03_ablation_4k444_4k420.json; DESIGN.md s3)",
             "reference_path": "src/idct8x8.cl:168-192 (batch_idct_csc_444), src/decoder.cpp:457-471"}
         checked_all_ok = checked["ok"] and r4["output_check"]["ok"]
     else:
