@@ -208,6 +208,11 @@ int hjd_debug_destuff_gpu(hjd_ctx* ctx, const uint8_t* scan, size_t n, int nseg,
                           uint32_t* seg_end, int64_t* out_bytes, uint32_t* status);
 int hjd_debug_entropy_emulate(const uint8_t* data, size_t size, int sub_bits, int16_t* coefs, int64_t capacity_blocks,
                               int32_t* status);
+/* Test hook (no GPU): the sync kernels' step decode (AC step tables, several
+ * units per lookup) against the unit-by-unit decode, from guessed and true
+ * entries of the first scan; *runs compared, *mismatches in exit state or
+ * statistics. */
+int hjd_debug_entropy_sync_check(const uint8_t* data, size_t size, int sub_bits, int64_t* runs, int64_t* mismatches);
 
 #ifdef __cplusplus
 }

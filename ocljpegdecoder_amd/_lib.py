@@ -165,6 +165,8 @@ def _bind_host(lib):
         "hjd_gstream_sync": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int64)]),
         "hjd_debug_entropy_emulate": (ctypes.c_int, [u8p, ctypes.c_size_t, ctypes.c_int,
                                                      ctypes.POINTER(ctypes.c_int16), ctypes.c_int64, c_i32p]),
+        "hjd_debug_entropy_sync_check": (ctypes.c_int, [u8p, ctypes.c_size_t, ctypes.c_int,
+                                                        ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
     })
     for name, (res, args) in sigs.items():
         fn = getattr(lib, name, None)

@@ -2751,6 +2751,68 @@ int hjd_debug_entropy_syncstats(const uint8_t* data, size_t size, int sub_bits, 
     return HJD_OK;
 }
 
+// Test hook for the sync-mode step decode: every run a sync kernel makes uses
+// the AC step tables (several units per lookup) and must give exactly the
+// state and statistics of the unit-by-unit decode.  Runs the first scan from
+// guessed entries (k*S - o, j, 0) for every block-in-MCU j and a few offsets o,
+// and from true unit boundaries, to stops S bits on, both ways; counts runs
+// and mismatches (exit state, block count, flags or DC sums).
+int hjd_debug_entropy_sync_check(const uint8_t* data, size_t size, int sub_bits, int64_t* runs, int64_t* mismatches)
+{
+    if (!data || !runs || !mismatches || sub_bits < 16) return set_error(HJD_E_INVALID, "invalid arguments");
+    std::vector<uint8_t> buf(size + 256);
+    Prepared p;
+    int rc = prepare(data, size, buf.data(), size + 64, p);
+    if (rc) return rc;
+    EntFrame F;
+    memset(&F, 0, sizeof(F));
+    F.data_bits = p.data_bits;
+    F.nseg = static_cast<uint32_t>(p.seg_end.size());
+    F.bpm = static_cast<uint8_t>(p.bpm);
+    F.ntab = static_cast<uint8_t>(p.ntab);
+    memcpy(F.jinfo, p.jinfo, sizeof(F.jinfo));
+    EntBatchDev b;
+    memset(&b, 0, sizeof(b));
+    b.data = buf.data();
+    b.seg_end = p.seg_end.data();
+    BlockInfo blocks[kMaxBpm];
+    fill_blocks(blocks, F);
+    std::vector<uint8_t> steps(static_cast<size_t>(F.ntab) << kStepBits);
+    fill_steps(steps.data(), p.tabs, F.ntab, 0, 1);
+    const RunCtx cs = make_ctx(b, F, p.tabs, blocks, steps.data());
+    const RunCtx cu = make_ctx(b, F, p.tabs, blocks);
+    const uint32_t S = static_cast<uint32_t>(sub_bits);
+    int64_t n = 0, bad = 0;
+    auto check = [&](uint64_t entry, uint32_t stop) {
+        SubStats a = stats_identity(), u = stats_identity();
+        const uint64_t xa = run<false>(cs, entry, stop, a, nullptr);
+        const uint64_t xu = run<false>(cu, entry, stop, u, nullptr);
+        ++n;
+        if (xa != xu || a.nblk != u.nblk || a.flags != u.flags || a.dc[0] != u.dc[0] || a.dc[1] != u.dc[1] ||
+            a.dc[2] != u.dc[2])
+            ++bad;
+    };
+    static const uint32_t kOffs[] = {0, 5, 19, 61, 200};
+    for (uint32_t k = 0; static_cast<uint64_t>(k) * S < p.data_bits; ++k)
+        for (uint32_t o : kOffs) {
+            if (o > k * S) continue;
+            const uint64_t g = guess_entry(cu, k * S - o);
+            for (uint32_t j = 0; j < F.bpm; ++j) check(pack_state(st_pos(g), j, 0, st_seg(g)), k * S + S);
+        }
+    // true unit boundaries, sampled
+    uint64_t cur = pack_state(0, 0, 0, 0);
+    for (uint32_t i = 0; st_seg(cur) < F.nseg; ++i) {
+        if (i % 7 == 0) check(cur, st_pos(cur) + S / 2 + (i % 5) * 37);
+        SubStats st = stats_identity();
+        const uint64_t nx = run<false>(cu, cur, st_pos(cur) + 1, st, nullptr);
+        if (st_pos(nx) <= st_pos(cur) && st_seg(nx) == st_seg(cur)) break;
+        cur = nx;
+    }
+    *runs = n;
+    *mismatches = bad;
+    return HJD_OK;
+}
+
 // Test hooks for the destuff step alone: the host routine (destuff()) and the
 // three device kernels on one raw scan, so arbitrary byte strings (stuffing,
 // fill bytes, RSTn in and out of order, truncation) can be compared directly.

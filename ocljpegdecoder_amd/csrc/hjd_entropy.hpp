@@ -438,6 +438,28 @@ __host__ __device__ __forceinline__ uint32_t funnel(uint32_t w0, uint32_t w1, ui
     return static_cast<uint32_t>(((static_cast<uint64_t>(w0) << 32) | w1) >> (32 - off));
 }
 
+// Unit entry of a code longer than the LUT (T.81 F.2.2.3): the length is the
+// first l with code_l <= MAXCODE[l]; the six compares use independent loads
+// and selects instead of a dependent loop.  An invalid code sets kError and
+// consumes 16 bits as a zero symbol.
+__host__ __device__ __forceinline__ uint32_t long_code_entry(const HuffLut& t, uint32_t peek, bool dc, uint32_t& flags)
+{
+    static_assert(kLutBits == 10, "long-code lengths 11..16");
+    const int32_t c11 = static_cast<int32_t>(peek >> 21), c12 = static_cast<int32_t>(peek >> 20);
+    const int32_t c13 = static_cast<int32_t>(peek >> 19), c14 = static_cast<int32_t>(peek >> 18);
+    const int32_t c15 = static_cast<int32_t>(peek >> 17), c16 = static_cast<int32_t>(peek >> 16);
+    const bool p11 = c11 <= t.maxcode[11], p12 = c12 <= t.maxcode[12], p13 = c13 <= t.maxcode[13];
+    const bool p14 = c14 <= t.maxcode[14], p15 = c15 <= t.maxcode[15], p16 = c16 <= t.maxcode[16];
+    const uint32_t len = p11 ? 11u : p12 ? 12u : p13 ? 13u : p14 ? 14u : p15 ? 15u : 16u;
+    const int32_t code = static_cast<int32_t>(peek >> (32 - len));
+    uint32_t sym = t.vals[(code + t.delta[len]) & 255];
+    if (!(p11 || p12 || p13 || p14 || p15 || p16)) {
+        flags |= kError;
+        sym = 0;
+    }
+    return unit_entry(len, sym, dc);
+}
+
 // Decode one run: from `entry` until the first unit boundary >= stop (write
 // mode: and until the block this run owns is complete).  Accumulates `st`
 // (must start as the identity).  Returns the exit state.  Per-component sums
@@ -542,6 +564,8 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
             // Taken only where single units would give the same state: all of
             // them end at or before `stop`, >= 8 bits before the segment end (no pad
             // check in between), and z stays <= 63 (no index-63 error case).
+            // (A branch-free form that computes the step and the unit outcome in
+            // every lane and selects measured slower: DESIGN.md s10.1.)
             if (!kWrite && c.steps && !dc) {
                 const uint32_t se = c.steps[bi.sac + (peek >> (32 - kStepBits))];
                 const uint32_t nb = step_bits(se), za = step_zadv(se);
@@ -563,25 +587,7 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
             const HuffLut& t = *reinterpret_cast<const HuffLut*>(reinterpret_cast<const char*>(c.tabs) +
                                                                  (dc ? bi.tdc : bi.tac));
             uint32_t e = t.lut[peek >> (32 - kLutBits)];
-            if (e == 0) {
-                // Codes longer than the LUT (T.81 F.2.2.3): the length is the first
-                // l with code_l <= MAXCODE[l]; the six compares use independent
-                // loads and selects instead of a dependent loop.
-                static_assert(kLutBits == 10, "long-code lengths 11..16");
-                const int32_t c11 = static_cast<int32_t>(peek >> 21), c12 = static_cast<int32_t>(peek >> 20);
-                const int32_t c13 = static_cast<int32_t>(peek >> 19), c14 = static_cast<int32_t>(peek >> 18);
-                const int32_t c15 = static_cast<int32_t>(peek >> 17), c16 = static_cast<int32_t>(peek >> 16);
-                const bool p11 = c11 <= t.maxcode[11], p12 = c12 <= t.maxcode[12], p13 = c13 <= t.maxcode[13];
-                const bool p14 = c14 <= t.maxcode[14], p15 = c15 <= t.maxcode[15], p16 = c16 <= t.maxcode[16];
-                const uint32_t len = p11 ? 11u : p12 ? 12u : p13 ? 13u : p14 ? 14u : p15 ? 15u : 16u;
-                const int32_t code = static_cast<int32_t>(peek >> (32 - len));
-                uint32_t sym = t.vals[(code + t.delta[len]) & 255];
-                if (!(p11 || p12 || p13 || p14 || p15 || p16)) {
-                    flags |= kError;   // consumes 16 bits as a zero symbol
-                    sym = 0;
-                }
-                e = unit_entry(len, sym, dc);
-            }
+            if (e == 0) e = long_code_entry(t, peek, dc, flags);
             const uint32_t total = e & 31, s = (e >> 5) & 15;
             uint32_t zk = e >> 9;
             if (zk == kZkDcError) {   // DC symbol > 11

@@ -176,3 +176,32 @@ def test_damaged_files_match_host_decoder(hjd):
             np.testing.assert_array_equal(got, ref, err_msg=f"round {rnd} mutant {i}")
             clean += 1
     assert clean > 20
+
+
+@pytest.mark.parametrize("case", ["golden", "fhd_q90", "q100_444", "dri1", "q40", "optimized", "multiscan_first"])
+def test_sync_step_decode_equals_unit_decode(hjd, case):
+    """The sync kernels' run (AC step tables, several units per lookup, both
+    lookups computed by every lane and selected) gives exactly the exit state
+    and statistics of the unit-by-unit decode, from guessed entries at every
+    block-in-MCU phase and a few bit offsets, and from true unit boundaries
+    (hjd_debug_entropy_sync_check)."""
+    import ctypes
+    import oracle_py as O
+    if case == "golden":
+        data = open(os.path.join(O.GOLDEN, "JPEG_example_JPG_RIP_050.jpg"), "rb").read()
+    elif case == "multiscan_first":
+        import jpeg_writer as JW
+        base = _pil(200, 120, 90, 2, seed=4)
+        data = JW.rewrite_scans(base, hjd.decode_coefs(base)[0], [(1, 2), (0,)], 3)[0]
+    else:
+        kw = {"fhd_q90": dict(w=640, h=360, q=90, sub=2), "q100_444": dict(w=320, h=200, q=100, sub=0),
+              "dri1": dict(w=300, h=180, q=90, sub=2, restart_marker_blocks=1),
+              "q40": dict(w=400, h=300, q=40, sub=2), "optimized": dict(w=400, h=240, q=85, sub=1, optimize=True)}[case]
+        kw = dict(kw)
+        data = _pil(kw.pop("w"), kw.pop("h"), kw.pop("q"), kw.pop("sub"), seed=11, **kw)
+    lib = hjd._lib.load()
+    runs, bad = ctypes.c_int64(0), ctypes.c_int64(0)
+    buf = (ctypes.c_uint8 * len(data)).from_buffer_copy(data)
+    for S in (64, 512, 2048):
+        assert lib.hjd_debug_entropy_sync_check(buf, len(data), S, ctypes.byref(runs), ctypes.byref(bad)) == 0
+        assert runs.value > 0 and bad.value == 0, (case, S, runs.value, bad.value)
