@@ -486,19 +486,28 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
         o = outs_mid if k == mid_step else outs
         for i, fid in enumerate(stream_step_ids(k, nf, rank, world)):
             st.submit(pool_c[fid % npool], o[i])
-        return st.sync()
 
+    # Steps are submitted back to back: the stream does not drain between
+    # steps (a drain idles the DMA engine for the last batch's kernels, ~6 % of
+    # a 1024-frame step).  One sync before the last step makes its writes the
+    # only ones in flight into `outs` (consecutive steps reuse those buffers on
+    # different slot streams), so the checked outputs are the last step's.
     for k in range(args.warmup):
         step(k)
+    st.sync()
     stats = {}
+    last_step = args.warmup + args.steps - 1
+    step_sync = os.environ.get("HJD_BENCH_STEP_SYNC") == "1"   # A/B knob: drain after every step (round-2/3 behaviour)
 
     def body():
         stats["before"] = st.sync()                 # stats are cumulative
-        stats["after"] = stats["before"]
         for k in range(args.warmup, args.warmup + args.steps):
-            stats["after"] = step(k)
+            if step_sync or (k == last_step and k != args.warmup):
+                st.sync()
+            step(k)
             if (k - args.warmup) % 16 == 15:
-                log(f"stream step {k - args.warmup + 1}/{args.steps}")
+                log(f"stream step {k - args.warmup + 1}/{args.steps} submitted")
+        stats["after"] = st.sync()
 
     wall, wall_max = timed_region(dist, world, body, torch.cuda.synchronize)   # max over ranks
     before, after = stats["before"], stats["after"]
