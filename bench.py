@@ -496,18 +496,17 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
         step(k)
     st.sync()
     stats = {}
-    last_step = args.warmup + args.steps - 1
     step_sync = os.environ.get("HJD_BENCH_STEP_SYNC") == "1"   # A/B knob: drain after every step (round-2/3 behaviour)
 
     def body():
         stats["before"] = st.sync()                 # stats are cumulative
-        for k in range(args.warmup, args.warmup + args.steps):
-            if step_sync or (k == last_step and k != args.warmup):
-                st.sync()
+        for act, k in stream_schedule(args.warmup, args.steps, step_sync):
+            if act == "sync":
+                stats["after"] = st.sync()
+                continue
             step(k)
             if (k - args.warmup) % 16 == 15:
                 log(f"stream step {k - args.warmup + 1}/{args.steps} submitted")
-        stats["after"] = st.sync()
 
     wall, wall_max = timed_region(dist, world, body, torch.cuda.synchronize)   # max over ranks
     before, after = stats["before"], stats["after"]
@@ -705,6 +704,21 @@ def timed_region(dist, world, body, sync):
         dist.barrier()
     wall = time.perf_counter() - t0
     return wall, shard.aggregate({"seconds": wall})["seconds"]
+
+
+def stream_schedule(warmup, steps, step_sync=False):
+    """The stream leg's timed region as actions ("step", k) / ("sync", None).
+    Steps are submitted back to back; the only drains are one before the last
+    step (consecutive steps write the same output buffers from different slot
+    streams, so the checked last step must be the only writer in flight) and
+    the final one.  step_sync=True drains after every step (A/B knob)."""
+    acts, last = [], warmup + steps - 1
+    for k in range(warmup, warmup + steps):
+        if step_sync or (k == last and k != warmup):
+            acts.append(("sync", None))
+        acts.append(("step", k))
+    acts.append(("sync", None))
+    return acts
 
 
 def stream_step_ids(k, frames_per_gpu, rank, world):

@@ -87,6 +87,27 @@ def test_stream_step_ids_match_one_rank():
             assert allids == list(range(k * 1024 * world, (k + 1) * 1024 * world))
 
 
+@pytest.mark.parametrize("warmup,steps", [(1, 98), (1, 13), (3, 2), (1, 1), (0, 5)])
+def test_stream_schedule(warmup, steps):
+    """The stream leg submits steps back to back: every timed step exactly
+    once in order, a drain right before the last step (its output buffers are
+    then written by it alone) and at the end, and no other drain."""
+    sys.path.insert(0, ROOT)
+    import bench
+    acts = bench.stream_schedule(warmup, steps)
+    assert [k for a, k in acts if a == "step"] == list(range(warmup, warmup + steps))
+    assert acts[-1] == ("sync", None)
+    syncs = [i for i, (a, _) in enumerate(acts) if a == "sync"]
+    last = acts.index(("step", warmup + steps - 1))
+    if steps > 1:
+        assert syncs == [last - 1, len(acts) - 1]
+    else:
+        assert syncs == [len(acts) - 1]
+    # the A/B knob: a drain before every step after the first and at the end
+    per = bench.stream_schedule(warmup, steps, step_sync=True)
+    assert [a for a, _ in per] == ["sync", "step"] * steps + ["sync"]
+
+
 @pytest.mark.parametrize("world", [1, 2, 8])
 def test_stream_leg_command(world):
     sys.path.insert(0, ROOT)
