@@ -412,7 +412,11 @@ int64_t hjd_plan_coef_bytes(const hjd_plan* plan) { return plan ? plan->coef_byt
 // batch (4:2:0 +12 %, 4:4:4 +13 % over one persistent wave per slot).  With
 // the XCD-contiguous group order (hjd_kernels.hpp group_order) the best chunk
 // is 2 tasks per wave at 4:2:0 (+3.9 % over 1 on 1024-frame batches) and 16 at
-// the heavier samplings (+1.3 % over 8; profiles/r02_tune_tasks_per_wave.json).
+// the VALU-heavier samplings 4:4:4, 4:2:2 and 4:4:0 (+1.3 % over 8 at 4:4:4;
+// profiles/r02_tune_tasks_per_wave.json).  The lighter, memory-bound shapes
+// want one task per wave: grayscale (0.69 -> 0.80 of 8 TB/s), 4:1:1 (0.65-0.71
+// -> 0.76) and both int32 (idct.h) formats (4:2:0 0.67 -> 0.76-0.78, 4:4:4
+// 0.74-0.75 -> 0.765-0.77), same box (profiles/r03_tune_tasks_per_wave_ext.json).
 // HJD_TASKS_PER_WAVE overrides it (tuning).
 static int decode_grid(int sampling, int fmt, int64_t tasks)
 {
@@ -422,7 +426,12 @@ static int decode_grid(int sampling, int fmt, int64_t tasks)
     }();
     // ... but never fewer than ~4 waves per SIMD (256 CUs x 4 SIMDs): a single
     // 4:4:4 frame at 16 tasks per wave would leave most of the chip idle.
-    int64_t per_wave = env > 0 ? env : (sampling == HJD_YUV420 && fmt == 0) ? 2 : 16;
+    int64_t per_wave = 16;
+    if (fmt != 0 || sampling == HJD_GRAY || sampling == HJD_YUV411_H4V1)
+        per_wave = 1;
+    else if (sampling == HJD_YUV420)
+        per_wave = 2;
+    if (env > 0) per_wave = env;
     per_wave = std::max<int64_t>(1, std::min<int64_t>(per_wave, tasks / (4 * 1024)));
     const int64_t waves = (tasks + per_wave - 1) / per_wave;
     const int64_t groups = (waves + hjd::kWavesPerGroup - 1) / hjd::kWavesPerGroup;
