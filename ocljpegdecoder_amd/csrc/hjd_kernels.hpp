@@ -434,21 +434,25 @@ __device__ __forceinline__ void colour_stage(const char* __restrict__ slots, int
         }
     } else if constexpr (kSampling == 5) {
         // 4:4:0 (extension, Y H1V2): 96x16 strip of 12 MCUs (Y0 above Y1, Cb,
-        // Cr; 8x16 px); units of 4 px x 1 row, 24 per row, 6 per lane; each
-        // chroma row serves 2 vertically adjacent pixel rows.
+        // Cr; 8x16 px); units of 4 px x 2 rows (pixel rows 2p, 2p+1 share
+        // chroma row p: nearest vertical replication), 24 per row pair, 3 per
+        // lane.  The chroma terms are computed once per chroma sample, as at
+        // 4:2:0 (round 2 computed them for each pixel row: 6 units per lane).
         (void)loff;
-#pragma unroll 2
-        for (int k = 0; k < (6 + kStride - 1) / kStride; ++k) {
+#pragma unroll 1
+        for (int k = 0; k < (3 + kStride - 1) / kStride; ++k) {
             const int it = u0 + k * kStride;
-            if (kStride > 1 && it >= 6) break;
+            if (kStride > 1 && it >= 3) break;
             const int u = it * 64 + lane;
-            const int y = u / 24;
-            const int cu4 = u - y * 24;       // unit within the row
+            const int p = u / 24;              // chroma row = pixel rows 2p, 2p+1
+            const int cu4 = u - p * 24;        // unit within the row pair
             const int m = cu4 >> 1;
-            const int xm = (cu4 & 1) * 4;     // x within MCU: 0 or 4
-            const int2 sy = *reinterpret_cast<const int2*>(slots + (4 * m + (y >> 3)) * kSlotBytes + (y & 7) * 16 +
-                                                           xm * 2);
-            const int coff = (y >> 1) * 16 + xm * 2;
+            const int xm = (cu4 & 1) * 4;      // x within MCU: 0 or 4
+            const int y0 = 2 * p;
+            const char* yblk = slots + (4 * m + (y0 >> 3)) * kSlotBytes + (y0 & 7) * 16 + xm * 2;
+            const int2 sya = *reinterpret_cast<const int2*>(yblk);
+            const int2 syb = *reinterpret_cast<const int2*>(yblk + 16);   // row y0 + 1 (same block: y0 even)
+            const int coff = p * 16 + xm * 2;
             const uint2 su = *reinterpret_cast<const uint2*>(slots + (4 * m + 2) * kSlotBytes + coff);
             const uint2 sv = *reinterpret_cast<const uint2*>(slots + (4 * m + 3) * kSlotBytes + coff);
             const ChromaTerms c0 = chroma_terms<0>(su.x, sv.x);
@@ -456,15 +460,23 @@ __device__ __forceinline__ void colour_stage(const char* __restrict__ slots, int
             const ChromaTerms c2 = chroma_terms<0>(su.y, sv.y);
             const ChromaTerms c3 = chroma_terms<1>(su.y, sv.y);
             const ChromaPair p01 = pair_of(c0, c1), p23 = pair_of(c2, c3);
-            const uint32_t lo = static_cast<uint32_t>(y) * static_cast<uint32_t>(pitch) +
+            const uint32_t lo = static_cast<uint32_t>(y0) * static_cast<uint32_t>(pitch) +
                                 static_cast<uint32_t>(cu4 * 4 * kPx);
             const int xu = x_base + cu4 * 4;
-            if (kFull || y_base + y < height) {
-                if (__builtin_amdgcn_ballot_w64((p01.flagged | p23.flagged) != 0))
-                    emit_row4<true, kVariant, kFull>(strip, lo, xu, width, sy.x, sy.y, p01, p23, &c0, &c1, &c2, &c3);
-                else
-                    emit_row4<false, kVariant, kFull>(strip, lo, xu, width, sy.x, sy.y, p01, p23, &c0, &c1, &c2,
+            const int ya = y_base + y0;
+            if (__builtin_amdgcn_ballot_w64((p01.flagged | p23.flagged) != 0)) {   // wave-uniform, rare
+                if (kFull || ya < height)
+                    emit_row4<true, kVariant, kFull>(strip, lo, xu, width, sya.x, sya.y, p01, p23, &c0, &c1, &c2, &c3);
+                if (kFull || ya + 1 < height)
+                    emit_row4<true, kVariant, kFull>(strip, lo + static_cast<uint32_t>(pitch), xu, width, syb.x,
+                                                     syb.y, p01, p23, &c0, &c1, &c2, &c3);
+            } else {
+                if (kFull || ya < height)
+                    emit_row4<false, kVariant, kFull>(strip, lo, xu, width, sya.x, sya.y, p01, p23, &c0, &c1, &c2,
                                                       &c3);
+                if (kFull || ya + 1 < height)
+                    emit_row4<false, kVariant, kFull>(strip, lo + static_cast<uint32_t>(pitch), xu, width, syb.x,
+                                                      syb.y, p01, p23, &c0, &c1, &c2, &c3);
             }
         }
     } else {
