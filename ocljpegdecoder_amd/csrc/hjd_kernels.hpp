@@ -504,6 +504,45 @@ __device__ __forceinline__ void colour_stage(const char* __restrict__ slots, int
     }
 }
 
+#ifndef HJD_SPLIT444
+#define HJD_SPLIT444 0   // tuning: 4:4:4 colour of each 64-px half right after its IDCT rounds
+#endif
+
+// 4:4:4 colour of one 64x8 half of a full strip (HJD_SPLIT444): lane = (4-px
+// column group cg = lane & 15, row lane >> 4); unit u covers rows 4u..4u+3, so
+// each wave store instruction writes four 256-byte row segments.
+template <int kVariant>
+__device__ __forceinline__ void colour_half444(const char* __restrict__ slots, int lane, uint8_t* __restrict__ out,
+                                               int pitch, int width, int y_base, int x_base, int half)
+{
+    constexpr int kPx = kOutBytes<kVariant>;
+    const int cg = lane & 15;
+    const int x0 = cg * 4;
+    const int m = half * 8 + (cg >> 1);
+    const int xm = x0 & 7;
+    const int rsub = lane >> 4;
+    const uint32_t loff = static_cast<uint32_t>(x0 * kPx) + static_cast<uint32_t>(rsub) * static_cast<uint32_t>(pitch);
+    uint8_t* const strip = out + static_cast<int64_t>(y_base) * pitch + static_cast<int64_t>(x_base + 64 * half) * kPx;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int y = 4 * u + rsub;
+        const char* base = slots + m * 3 * kSlotBytes + y * 16 + xm * 2;
+        const int2 sy = *reinterpret_cast<const int2*>(base);
+        const uint2 su = *reinterpret_cast<const uint2*>(base + kSlotBytes);
+        const uint2 sv = *reinterpret_cast<const uint2*>(base + 2 * kSlotBytes);
+        const ChromaTerms c0 = chroma_terms<0>(su.x, sv.x);
+        const ChromaTerms c1 = chroma_terms<1>(su.x, sv.x);
+        const ChromaTerms c2 = chroma_terms<0>(su.y, sv.y);
+        const ChromaTerms c3 = chroma_terms<1>(su.y, sv.y);
+        const ChromaPair p01 = pair_of(c0, c1), p23 = pair_of(c2, c3);
+        uint8_t* row = strip + static_cast<int64_t>(4 * u) * pitch;   // wave-uniform
+        if (__builtin_amdgcn_ballot_w64((p01.flagged | p23.flagged) != 0))
+            emit_row4<true, kVariant, true>(row, loff, x_base, width, sy.x, sy.y, p01, p23, &c0, &c1, &c2, &c3);
+        else
+            emit_row4<false, kVariant, true>(row, loff, x_base, width, sy.x, sy.y, p01, p23, &c0, &c1, &c2, &c3);
+    }
+}
+
 // Task-local block (= LDS slot) transformed by lane group g in round i.  The
 // mapping keeps each round's component uniform across the wave (dequant table
 // and luma level shift): 4:4:4 / 4:2:0 / gray blocks are MCU-interleaved with
@@ -524,6 +563,10 @@ __device__ __forceinline__ int round_block(int i, int g)
         }
         const int idx = (i - 3) * 8 + g;        // 0-11 Cb, 12-23 Cr
         return idx < 12 ? 4 * idx + 2 : 4 * (idx - 12) + 3;
+    } else if constexpr (kSampling == 0 && HJD_SPLIT444 != 0) {
+        // MCUs 0-7 (the strip's left 64 px) in rounds 0-2, MCUs 8-15 in rounds
+        // 3-5, so the left half's colour can run before rounds 3-5
+        return i < 3 ? 3 * g + i : 24 + 3 * g + (i - 3);
     } else {
         return 6 * g + i;
     }
@@ -630,10 +673,13 @@ __device__ __forceinline__ void load_qrow_pk(const int* __restrict__ qt_pool, in
 // Samples end up as int16 row-major in the block slots (luma as Y + 128).  The next round's
 // coefficient gathers are issued before this round's column math, so their
 // LDS latency overlaps it.
-template <int kSampling, int kFmt>
+struct NoHook {
+    __device__ __forceinline__ void operator()(int) const {}
+};
+template <int kSampling, int kFmt, typename AfterRound = NoHook>
 __device__ __forceinline__ void idct_stage(char* __restrict__ slots, char* __restrict__ rowbuf, int lane,
                                            const int (&zoff)[8], const uint32_t (&q)[3][4], const char* __restrict__ qlds,
-                                           const int* __restrict__ src32, int nblk)
+                                           const int* __restrict__ src32, int nblk, AfterRound after_round = {})
 {
     const int g = lane >> 3, r = lane & 7;
     RowPk pk;
@@ -696,6 +742,7 @@ __device__ __forceinline__ void idct_stage(char* __restrict__ slots, char* __res
                 *reinterpret_cast<short*>(blk + k * 16) = static_cast<short>(static_cast<uint32_t>(c8[k]) >> 16);
         }
         wave_lds_sync();
+        after_round(i);
     }
 }
 
@@ -704,6 +751,9 @@ __device__ __forceinline__ void idct_stage(char* __restrict__ slots, char* __res
 #endif
 #ifndef HJD_XCD
 #define HJD_XCD 1
+#endif
+#ifndef HJD_PREFETCH_AT
+#define HJD_PREFETCH_AT -1   // tuning: issue the next task's loads after IDCT round N (-1: before round 0)
 #endif
 #ifndef HJD_XCD_CHUNK
 #define HJD_XCD_CHUNK 0
@@ -836,7 +886,7 @@ __global__ __launch_bounds__(kGroupThreads, KLayout<kSampling>::min_waves) void 
                 *reinterpret_cast<int4*>(slots + (j >> 3) * kSlotBytes + (j & 7) * 16) = pre[k];
             }
             wave_lds_sync();
-            if (task + t_step < t_end) {
+            if (HJD_PREFETCH_AT < 0 && task + t_step < t_end) {
                 while (task + t_step >= pc.end) cursor_load(pc, frames, nframes, total_tasks, pc.idx + 1);
                 prefetch(task_geom<kSampling>(pc, task + t_step));
             }
@@ -845,16 +895,36 @@ __global__ __launch_bounds__(kGroupThreads, KLayout<kSampling>::min_waves) void 
                 while (task + t_step >= pc.end) cursor_load(pc, frames, nframes, total_tasks, pc.idx + 1);
         }
 
-        if constexpr ((kVariant & kAblNoIdct) == 0)
-            idct_stage<kSampling, kFmt>(slots, rowbuf, lane, zoff, q, qlds,
-                                        static_cast<const int*>(coefs) + tg.blk0 * 64, tg.nblk);
-
+        // HJD_PREFETCH_AT >= 0 (tuning): the next task's loads are issued after
+        // IDCT round HJD_PREFETCH_AT instead of before round 0
         constexpr int kRows = KGeom<kSampling>::kMcuH;
         constexpr int kStripW = KGeom<kSampling>::kStripW;
         uint8_t* fout = out + cc.out_base;
+        const bool full = cc.vec_ok && tg.x_base + kStripW <= cc.width && tg.y_base + kRows <= cc.height;
+        constexpr bool kSplit = HJD_SPLIT444 != 0 && kSampling == 0 && (kVariant & (kAblNoColour | kAblNoIdct)) == 0;
+        auto late_prefetch = [&](int i) {
+            if constexpr (kFmt == 0 && HJD_PREFETCH_AT >= 0) {
+                if (i == HJD_PREFETCH_AT && task + t_step < t_end) {
+                    while (task + t_step >= pc.end) cursor_load(pc, frames, nframes, total_tasks, pc.idx + 1);
+                    prefetch(task_geom<kSampling>(pc, task + t_step));
+                }
+            }
+            if constexpr (kSplit) {
+                if (full && (i == 2 || i == 5))
+                    colour_half444<kVariant>(slots, lane, fout, cc.pitch, cc.width, tg.y_base, tg.x_base, i == 5 ? 1 : 0);
+            }
+        };
+        if constexpr ((kVariant & kAblNoIdct) == 0)
+            idct_stage<kSampling, kFmt>(slots, rowbuf, lane, zoff, q, qlds,
+                                        static_cast<const int*>(coefs) + tg.blk0 * 64, tg.nblk, late_prefetch);
+        else
+            late_prefetch(HJD_PREFETCH_AT);
+
         if constexpr ((kVariant & kAblNoColour) != 0) {
             (void)fout;
-        } else if (cc.vec_ok && tg.x_base + kStripW <= cc.width && tg.y_base + kRows <= cc.height)
+        } else if (kSplit && full) {
+            // converted inside the IDCT stage (late_prefetch hook)
+        } else if (full)
             colour_stage<kSampling, true, kVariant>(slots, lane, fout, cc.pitch, cc.width, cc.height, tg.y_base, tg.x_base);
         else {
             colour_stage<kSampling, false, kVariant>(slots, lane, fout, cc.pitch, cc.width, cc.height, tg.y_base, tg.x_base);

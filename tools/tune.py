@@ -73,7 +73,7 @@ def main():
                 sig = int(out[:, ::97, ::89].sum().item())
                 ref = sig if ref is None else ref
                 assert sig == ref, f"kernel {k} variant {v} grid {g} output differs"
-    res = {"workload": args.workload, "frames": nf, "bytes_per_launch": nbytes, "results": []}
+    res = {"workload": args.workload, "frames": nf, "bytes_per_launch": nbytes, "signature": ref, "results": []}
     for (k, v, g), ts in times.items():
         med = statistics.median(ts)
         res["results"].append({"kernel": k, "variant": v, "grid": g, "median_ms": round(med, 4),
