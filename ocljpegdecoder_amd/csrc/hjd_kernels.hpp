@@ -191,9 +191,6 @@ constexpr int kAblNoCsc = 64;
 // Output format bit (include/hjd.h HJD_OUT_BGR24): 3-byte B,G,R pixels
 // instead of 4-byte BGRX words.
 constexpr int kOutBgr24 = 32;
-#ifndef HJD_STORE_ASM
-#define HJD_STORE_ASM 0   // tuning: full-strip BGRX store cache policy (0: nt via the builtin)
-#endif
 template <int kVariant>
 constexpr int kOutBytes = (kVariant & kOutBgr24) != 0 ? 3 : 4;
 
@@ -250,12 +247,6 @@ __device__ __forceinline__ void store4(uint8_t* __restrict__ row, uint32_t loff,
         typedef __attribute__((address_space(1))) u32x4 gvec;
         if constexpr (kVariant & kVarPlainStores)
             *(gvec*)dst = v;
-        else if constexpr (HJD_STORE_ASM == 1)   // tuning: write-through, line dropped from L2
-            asm volatile("global_store_dwordx4 %0, %1, %2 sc0 sc1" ::"v"(loff), "v"(v), "s"(grow) : "memory");
-        else if constexpr (HJD_STORE_ASM == 2)
-            asm volatile("global_store_dwordx4 %0, %1, %2 sc1" ::"v"(loff), "v"(v), "s"(grow) : "memory");
-        else if constexpr (HJD_STORE_ASM == 3)
-            asm volatile("global_store_dwordx4 %0, %1, %2 sc1 nt" ::"v"(loff), "v"(v), "s"(grow) : "memory");
         else
             __builtin_nontemporal_store(v, (gvec*)dst);
     } else {
