@@ -41,6 +41,16 @@ def aggregate(stats: Dict[str, float], reduce_max=("seconds",)) -> Dict[str, flo
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return dict(stats)
+    return allreduce_stats(stats, reduce_max)
+
+
+def allreduce_stats(stats: Dict[str, float], reduce_max=("seconds",)) -> Dict[str, float]:
+    """aggregate's collective part: one SUM and one MAX all-reduce of float64
+    vectors (on the device for RCCL, on the host for gloo).  Split out so a
+    one-rank RCCL group on a single GPU can run the exact calls an N-GPU run
+    makes (tests/test_gpu_rccl.py)."""
+    import torch
+    import torch.distributed as dist
     keys = sorted(stats)
     dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
     sums = torch.tensor([0.0 if k in reduce_max else float(stats[k]) for k in keys], dtype=torch.float64,
