@@ -191,6 +191,9 @@ constexpr int kAblNoCsc = 64;
 // Output format bit (include/hjd.h HJD_OUT_BGR24): 3-byte B,G,R pixels
 // instead of 4-byte BGRX words.
 constexpr int kOutBgr24 = 32;
+// Gather pairs as ds_read_u16 | ds_read_u16_d16_hi (load_round_pk_d16): only
+// valid where d16 loads zero the other half (sramecc+), chosen at launch.
+constexpr int kVarD16 = 128;
 template <int kVariant>
 constexpr int kOutBytes = (kVariant & kOutBgr24) != 0 ? 3 : 4;
 
@@ -640,6 +643,64 @@ __device__ __forceinline__ RowPk load_round_pk(const char* __restrict__ slots, i
     return p;
 }
 
+// kVarD16 kernels (the runtime launches them on sramecc+ devices only, where
+// d16 LDS loads zero the other half): shapes whose round blocks are 6g + i
+// with a wave-uniform component (4:4:4, 4:2:0, 4:1:1, grayscale), staged
+// int16 (kFmt 0), default layout.  Instantiated for 4:4:4 (hjd_runtime.hip).
+template <int kSampling, int kFmt, int kVariant>
+constexpr bool kD16Gather = (kVariant & kVarD16) != 0 && kFmt == 0 && !KLayout<kSampling>::t2 &&
+                            (round_class(kSampling) == 0 || round_class(kSampling) == 1 || round_class(kSampling) == 3) &&
+                            !(kSampling == 0 && HJD_SPLIT444 != 0);
+
+// load_round_pk for kD16Gather shapes, round kI: each pair's second
+// coefficient is loaded straight into the high half of its word with
+// ds_read_u16_d16_hi, which on MI355X (sramecc+) zeroes the low half
+// (profiles/r03_d16_probe.txt), so the pair is (first | second): one v_or_b32
+// (a full-rate op on gfx950) instead of a v_perm_b32.  LLVM does not emit the
+// d16 LDS loads for this target, so they are inline asm: all four are issued
+// before the four compiler-visible ds_read_u16 of the same round, and DS
+// operations of a wave complete in order, so the compiler's own wait for
+// each low-half load also covers the high-half load issued before it.
+template <int kSampling, int kI>
+__device__ __forceinline__ RowPk load_round_pk_d16(const char* __restrict__ slots, uint32_t slots_lds, int lane,
+                                                   const int (&zoff)[8], const uint32_t (&q)[3][4])
+{
+    constexpr int comp = round_component<kSampling>(kI);
+    static_assert(comp >= 0, "wave-uniform component");
+    constexpr int kOff = kI * kSlotBytes;
+    const int blk_off = 6 * (lane >> 3) * kSlotBytes;   // round_block = 6g + kI
+    constexpr int kHi[4] = {4, 7, 5, 6}, kLo[4] = {0, 1, 3, 2};
+    uint32_t w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t a = slots_lds + static_cast<uint32_t>(blk_off + zoff[kHi[k]]);
+        asm volatile("ds_read_u16_d16_hi %0, %1 offset:%2" : "=v"(w[k]) : "v"(a), "i"(kOff) : "memory");
+    }
+    const char* blk = slots + blk_off + kOff;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) w[k] |= *reinterpret_cast<const unsigned short*>(blk + zoff[kLo[k]]);
+    RowPk p;   // dequant (src/decoder.cpp:340)
+    p.p04 = __builtin_bit_cast(s16x2, w[0]) * __builtin_bit_cast(s16x2, q[comp][0]);
+    p.p17 = __builtin_bit_cast(s16x2, w[1]) * __builtin_bit_cast(s16x2, q[comp][1]);
+    p.p35 = __builtin_bit_cast(s16x2, w[2]) * __builtin_bit_cast(s16x2, q[comp][2]);
+    p.p26 = __builtin_bit_cast(s16x2, w[3]) * __builtin_bit_cast(s16x2, q[comp][3]);
+    return p;
+}
+
+template <int kSampling>
+__device__ __forceinline__ RowPk load_round_pk_d16_at(int i, const char* __restrict__ slots, uint32_t slots_lds,
+                                                      int lane, const int (&zoff)[8], const uint32_t (&q)[3][4])
+{
+    switch (i) {   // i is a constant in the unrolled round loop
+    case 0: return load_round_pk_d16<kSampling, 0>(slots, slots_lds, lane, zoff, q);
+    case 1: return load_round_pk_d16<kSampling, 1>(slots, slots_lds, lane, zoff, q);
+    case 2: return load_round_pk_d16<kSampling, 2>(slots, slots_lds, lane, zoff, q);
+    case 3: return load_round_pk_d16<kSampling, 3>(slots, slots_lds, lane, zoff, q);
+    case 4: return load_round_pk_d16<kSampling, 4>(slots, slots_lds, lane, zoff, q);
+    default: return load_round_pk_d16<kSampling, 5>(slots, slots_lds, lane, zoff, q);
+    }
+}
+
 // One round's row-pass inputs, kFmt 1: int32 natural rows (already
 // dequantised: the idct.h format) read straight from global memory.
 template <int kSampling>
@@ -676,15 +737,18 @@ __device__ __forceinline__ void load_qrow_pk(const int* __restrict__ qt_pool, in
 struct NoHook {
     __device__ __forceinline__ void operator()(int) const {}
 };
-template <int kSampling, int kFmt, typename AfterRound = NoHook>
+template <int kSampling, int kFmt, int kVariant = 0, typename AfterRound = NoHook>
 __device__ __forceinline__ void idct_stage(char* __restrict__ slots, char* __restrict__ rowbuf, int lane,
                                            const int (&zoff)[8], const uint32_t (&q)[3][4], const char* __restrict__ qlds,
-                                           const int* __restrict__ src32, int nblk, AfterRound after_round = {})
+                                           const int* __restrict__ src32, int nblk, AfterRound after_round = {},
+                                           uint32_t slots_lds = 0)
 {
     const int g = lane >> 3, r = lane & 7;
     RowPk pk;
     int v[8];
-    if constexpr (kFmt == 0)
+    if constexpr (kD16Gather<kSampling, kFmt, kVariant>)
+        pk = load_round_pk_d16_at<kSampling>(0, slots, slots_lds, lane, zoff, q);
+    else if constexpr (kFmt == 0)
         pk = load_round_pk<kSampling>(slots, lane, 0, zoff, q, qlds);
     else
         load_round_i32<kSampling>(lane, 0, src32, nblk, v);
@@ -726,7 +790,9 @@ __device__ __forceinline__ void idct_stage(char* __restrict__ slots, char* __res
             for (int k = 0; k < 8; ++k) c8[k] = *reinterpret_cast<const int*>(col + k * kRowStride);
         }
         if (i + 1 < 6) {
-            if constexpr (kFmt == 0)
+            if constexpr (kD16Gather<kSampling, kFmt, kVariant>)
+                pk = load_round_pk_d16_at<kSampling>(i + 1, slots, slots_lds, lane, zoff, q);
+            else if constexpr (kFmt == 0)
                 pk = load_round_pk<kSampling>(slots, lane, i + 1, zoff, q, qlds);
             else
                 load_round_i32<kSampling>(lane, i + 1, src32, nblk, v);
@@ -795,6 +861,8 @@ __global__ __launch_bounds__(kGroupThreads, KLayout<kSampling>::min_waves) void 
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     char* slots = lds + wave * L::wave_lds;
+    // LDS byte address of this wave's slots (inline-asm DS loads, kVarD16)
+    const uint32_t slots_lds = static_cast<uint32_t>(reinterpret_cast<size_t>(lds)) + wave * L::wave_lds;
     char* rowbuf = slots + kTaskBlocks * kSlotBytes;   // transpose buffer (default) or table rows (t2)
     char* qlds = rowbuf;
     const int r = lane & 7;
@@ -915,8 +983,9 @@ __global__ __launch_bounds__(kGroupThreads, KLayout<kSampling>::min_waves) void 
             }
         };
         if constexpr ((kVariant & kAblNoIdct) == 0)
-            idct_stage<kSampling, kFmt>(slots, rowbuf, lane, zoff, q, qlds,
-                                        static_cast<const int*>(coefs) + tg.blk0 * 64, tg.nblk, late_prefetch);
+            idct_stage<kSampling, kFmt, kVariant>(slots, rowbuf, lane, zoff, q, qlds,
+                                        static_cast<const int*>(coefs) + tg.blk0 * 64, tg.nblk, late_prefetch,
+                                        slots_lds);
         else
             late_prefetch(HJD_PREFETCH_AT);
 

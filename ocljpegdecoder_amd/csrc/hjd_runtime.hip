@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <string>
 #include <vector>
@@ -99,6 +100,29 @@ static int64_t latency_max_tasks()
     return v;
 }
 
+// The 4:4:4 kernels gather coefficient pairs with ds_read_u16_d16_hi
+// (hjd::kVarD16), which relies on d16 LDS loads zeroing the other half of
+// the register.  That is the sramecc+ behaviour (MI355X as deployed,
+// profiles/r03_d16_probe.txt); on a sramecc- device they keep it, so the
+// variant is taken only when the device's ISA name says sramecc+.
+// HJD_D16=0 / 1 overrides the default (kD16Default) for A/B and tests.
+constexpr bool kD16Default = false;
+static bool device_d16_gather(int device)
+{
+    const char* e = getenv("HJD_D16");
+    if (e ? e[0] == '0' : !kD16Default) return false;
+    static std::mutex mu;
+    static std::vector<int> known;   // -1 unknown, 0 / 1
+    std::lock_guard<std::mutex> lock(mu);
+    if (device < 0) return false;
+    if (static_cast<size_t>(device) >= known.size()) known.resize(device + 1, -1);
+    if (known[device] < 0) {
+        hipDeviceProp_t p;
+        known[device] = hipGetDeviceProperties(&p, device) == hipSuccess && strstr(p.gcnArchName, "sramecc+") != nullptr;
+    }
+    return known[device] == 1;
+}
+
 static int geometry(int width, int height, int sampling, int& mcu_w, int& mcu_h, int& bpm, int& tasks_mcus);
 static int decode_grid(int sampling, int fmt, int64_t tasks);
 
@@ -170,7 +194,10 @@ int hjd_internal::launch_decode(int device, int num_cu, int sampling, int input_
             hjd::decode_kernel<4, 0, hjd::kOutBgr24>, hjd::decode_kernel<4, 1, hjd::kOutBgr24>,
             hjd::decode_kernel<5, 0, hjd::kOutBgr24>, hjd::decode_kernel<5, 1, hjd::kOutBgr24>};
         if (variant != 0) return set_error(HJD_E_INVALID, "kernel variants are BGRX-only");
-        hipLaunchKernelGGL(kTable24[(sg.index << 1) | fmt], dim3(grid), dim3(hjd::kGroupThreads), 0,
+        K k24 = kTable24[(sg.index << 1) | fmt];
+        if (sampling == HJD_YUV444 && fmt == 0 && device_d16_gather(device))
+            k24 = hjd::decode_kernel<0, 0, hjd::kOutBgr24 | hjd::kVarD16>;
+        hipLaunchKernelGGL(k24, dim3(grid), dim3(hjd::kGroupThreads), 0,
                            static_cast<hipStream_t>(stream), d_coefs, d_qt_nat,
                            reinterpret_cast<const FrameDev*>(d_frames), nframes, tasks, static_cast<uint8_t*>(d_out));
         HJD_HIP(hipGetLastError());
@@ -206,7 +233,10 @@ int hjd_internal::launch_decode(int device, int num_cu, int sampling, int input_
                                  HJD_K4(2, 0), HJD_K4(2, 1), HJD_K4(3, 0), HJD_K4(3, 1),
                                  HJD_K4(4, 0), HJD_K4(4, 1), HJD_K4(5, 0), HJD_K4(5, 1)};
 #undef HJD_K4
-    hipLaunchKernelGGL(kTable[key], dim3(grid), dim3(hjd::kGroupThreads), 0, static_cast<hipStream_t>(stream),
+    K k = kTable[key];
+    if (sampling == HJD_YUV444 && fmt == 0 && (variant & 3) == 0 && device_d16_gather(device))
+        k = hjd::decode_kernel<0, 0, hjd::kVarD16>;
+    hipLaunchKernelGGL(k, dim3(grid), dim3(hjd::kGroupThreads), 0, static_cast<hipStream_t>(stream),
                        d_coefs, d_qt_nat, reinterpret_cast<const FrameDev*>(d_frames), nframes, tasks,
                        static_cast<uint8_t*>(d_out));
     HJD_HIP(hipGetLastError());

@@ -110,3 +110,20 @@ def test_16bit_quantisation_tables(hjd, ctx, mode, s):
     assert peak < 480, peak   # premise: legal domain, with margin for the integer IDCT's rounding
     got = _run(hjd, ctx, coefs, qt, w, h, s, mode)
     np.testing.assert_array_equal(got, _expect(O.decode_q16(coefs, qt, w, h, s), 0))
+
+
+@pytest.mark.parametrize("d16", ["0", "1"])
+def test_444_gather_forms_vs_oracle(hjd, ctx, monkeypatch, d16):
+    """4:4:4 persistent kernel with both coefficient-pair gathers: the
+    ds_read_u16_d16_hi | ds_read_u16 form (hjd::kVarD16, taken on sramecc+
+    devices) and the v_perm form (HJD_D16=0, and sramecc- devices)."""
+    import torch
+    monkeypatch.setenv("HJD_D16", d16)
+    arch = torch.cuda.get_device_properties(0).gcnArchName
+    print("device", arch, "d16 gather", d16 == "1" and "sramecc+" in arch)
+    for (w, h) in SIZES + [(3840, 64)]:
+        coefs, qt = O.synthetic_coefs(w, h, 0, seed=7 * w + h)
+        exp = O.decode_q16(coefs, qt, w, h, 0)
+        for out_format in (0, 1):
+            got = _run(hjd, ctx, coefs, qt, w, h, 0, 1, out_format=out_format)
+            np.testing.assert_array_equal(got, _expect(exp, out_format), err_msg=f"{w}x{h} fmt={out_format}")
