@@ -106,7 +106,7 @@ static int64_t latency_max_tasks()
 // profiles/r03_d16_probe.txt); on a sramecc- device they keep it, so the
 // variant is taken only when the device's ISA name says sramecc+.
 // HJD_D16=0 / 1 overrides the default (kD16Default) for A/B and tests.
-constexpr bool kD16Default = false;
+constexpr bool kD16Default = true;   // same-box A/B: profiles/r03_444_d16_gather_ab.json
 static bool device_d16_gather(int device)
 {
     const char* e = getenv("HJD_D16");
