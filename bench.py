@@ -31,6 +31,7 @@ import ctypes
 import glob
 import json
 import os
+import socket
 import sys
 import tempfile
 import time
@@ -248,13 +249,65 @@ def cpu_baseline(coef_pool_host, qt, wl, frames_done_gpu_rate):
                     t_sum += time.perf_counter() - t0
             finally:
                 os.chdir(cwd)
-            res["reference"] = {"value": round(reps * w * h / t_sum / 1e6, 2), "unit": "Mpixels/s", "cores": 1,
-                                "kind": "reference",
-                                "sample": f"{reps} x decode_mcu_data (src/decoder.cpp:397, USE_CPU_ONLY, incl. its "
-                                          f"BMP fwrite to a temp dir) on one {w}x{h} frame"}
+            one = {"value": round(reps * w * h / t_sum / 1e6, 2), "unit": "Mpixels/s", "cores": 1,
+                   "sample": f"{reps} x decode_mcu_data (src/decoder.cpp:397, USE_CPU_ONLY, incl. its "
+                             f"BMP fwrite to a temp dir) on one {w}x{h} frame, 1 thread"}
+            res["reference"] = reference_multicore(O, pool, q, w, h, s, nthreads)
+            res["reference"]["one_thread"] = one
         except Exception as e:  # pragma: no cover
             res["reference"] = {"error": str(e)}
     return res
+
+
+def reference_multicore(O, pool, q, w, h, s, nworkers, reps=8):
+    """The REFERENCE CPU path on all of this process's cores: `nworkers`
+    processes (tests/ref_cpu_worker.py), one per core, each running the
+    reference's own decode_mcu_data (oracle/_ref/libref.so) on its own pool
+    frame in its own temp dir (the reference keeps global state and writes
+    its BMP into the cwd, src/decoder.cpp:420).  All workers load their frame
+    copies, then start together; Mpx/s = all frames / wall time until the last
+    one finishes."""
+    import shutil
+    import subprocess
+    worker = os.path.join(REPO, "tests", "ref_cpu_worker.py")
+    tmp = tempfile.mkdtemp(prefix="hjd_refmc_")
+    procs = []
+    try:
+        paths = []
+        for i in range(min(pool.shape[0], nworkers)):
+            pth = os.path.join(tmp, f"frame{i}.npy")
+            np.save(pth, O.dequant_natural(pool[i], q, s))
+            paths.append(pth)
+        for k in range(nworkers):
+            wd = os.path.join(tmp, f"w{k}")
+            os.makedirs(wd)
+            procs.append(subprocess.Popen([sys.executable, worker, paths[k % len(paths)], str(w), str(h), str(s),
+                                           str(reps), wd], stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True))
+        for p in procs:
+            if p.stdout.readline().strip() != "ready":
+                raise RuntimeError("reference worker failed to start")
+        t0 = time.perf_counter()
+        for p in procs:
+            p.stdin.write("go\n")
+            p.stdin.flush()
+        outs = [json.loads(p.stdout.readline()) for p in procs]
+        wall = time.perf_counter() - t0
+        for p in procs:
+            p.wait(timeout=60)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        shutil.rmtree(tmp, ignore_errors=True)
+    if any("error" in o for o in outs):
+        return {"error": [o for o in outs if "error" in o][:2]}
+    frames = sum(o["frames"] for o in outs)
+    return {"value": round(frames * w * h / wall / 1e6, 2), "unit": "Mpixels/s", "cores": nworkers,
+            "kind": "reference", "processes": nworkers,
+            "sample": f"{nworkers} processes x {reps} frames {w}x{h} {SAMPLING_NAMES[s]} (pool of {pool.shape[0]}): "
+                      f"the reference's own decode_mcu_data (src/decoder.cpp:397-523, USE_CPU_ONLY, incl. its BMP "
+                      f"fwrite to each process's temp dir), started together, {wall:.2f} s wall",
+            "mean_s_per_frame_per_process": round(sum(o["seconds"] for o in outs) / frames, 4)}
 
 
 def _cpu_model():
@@ -301,7 +354,7 @@ def committed_traffic(workload, frames):
             continue
         if (d.get("workload") == workload and d.get("hbm_bytes_per_launch") and
                 d.get("frames_per_launch") == frames):
-            best = (d["hbm_bytes_per_launch"], os.path.relpath(p, REPO))
+            best = (d["hbm_bytes_per_launch"], os.path.relpath(p, REPO), d.get("box", "not recorded"))
     return best
 
 
@@ -336,13 +389,14 @@ def frame_checksum(torch, t, weights):
     return int(((x * weights[:x.numel()]) % CHECK_PRIME).sum().item() % CHECK_PRIME)
 
 
-def run_jpeg_single(args, wl, hjd, torch, dist, world, rank, dev):
+def jpeg_single_latency(args, wl, hjd, torch, dist, world, dev, steps, warmup):
     """Config 1 end to end, one image at a time (the reference program's use:
-    decode one file, src/main.cpp): JPEG bytes in host memory -> BGRX in HBM,
-    each step = submit + sync of ONE image.  Three paths on the same file:
-    GPU Huffman from pageable bytes (host destuff; `value`), GPU Huffman from
-    pinned bytes (device destuff), and host Huffman + the fused kernel."""
-    from ocljpegdecoder_amd import shard
+    decode one file, src/main.cpp + src/decoder.cpp:397-416): JPEG bytes in
+    host memory -> BGRX in HBM, each step = submit + sync of ONE image.  Three
+    paths on the same file: GPU Huffman from pageable bytes (host destuff; the
+    headline), GPU Huffman from pinned bytes (device destuff), and host
+    Huffman + the fused kernel.  The last timed step's output of the first
+    path is checked against the oracle on the host decoder's coefficients."""
     w, h, s = wl["width"], wl["height"], wl["sampling"]
     data = encode_pool(w, h, s, 1, seed0=4242)[0]
     info = hjd.parse(data)
@@ -371,7 +425,7 @@ def run_jpeg_single(args, wl, hjd, torch, dist, world, rank, dev):
         torch.cuda.synchronize()
 
     def timed(fn, k):
-        for _ in range(args.warmup):
+        for _ in range(warmup):
             fn()
 
         def body():
@@ -379,15 +433,26 @@ def run_jpeg_single(args, wl, hjd, torch, dist, world, rank, dev):
                 fn()
         return timed_region(dist, world, body, torch.cuda.synchronize)[1] / k
 
-    t_gpu = timed(gpu_pageable, args.steps)
-    # the output of the last timed step vs the oracle on the host decoder's coefficients
+    t_gpu = timed(gpu_pageable, steps)
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_py as O
     ref, rinfo = hjd.decode_coefs(data)
-    ok = bool(np.array_equal(out.cpu().numpy().view(np.uint32),
-                             O.decode_q16(ref, rinfo.qt, w, h, s)))
-    t_pin = timed(gpu_pinned, args.steps)
-    t_host = timed(host_huffman, args.steps)
+    ok = bool(np.array_equal(out.cpu().numpy().view(np.uint32), O.decode_q16(ref, rinfo.qt, w, h, s)))
+    t_pin = timed(gpu_pinned, steps)
+    t_host = timed(host_huffman, steps)
+    gd.close()
+    plan.close()
+    return {"t_gpu": t_gpu, "ok": ok, "jpeg_bytes": len(data),
+            "latency_ms_per_image": {"gpu_huffman_pageable_bytes": round(t_gpu * 1e3, 4),
+                                     "gpu_huffman_pinned_bytes_device_destuff": round(t_pin * 1e3, 4),
+                                     "host_huffman_then_kernel": round(t_host * 1e3, 4)}}
+
+
+def run_jpeg_single(args, wl, hjd, torch, dist, world, rank, dev):
+    """--workload fhd420_jpeg: jpeg_single_latency as its own line."""
+    w, h, s = wl["width"], wl["height"], wl["sampling"]
+    r = jpeg_single_latency(args, wl, hjd, torch, dist, world, dev, args.steps, args.warmup)
+    t_gpu, ok = r["t_gpu"], r["ok"]
     px = w * h
     if rank == 0:
         res = {
@@ -395,22 +460,48 @@ def run_jpeg_single(args, wl, hjd, torch, dist, world, rank, dev):
             "value": round(px * world / t_gpu / 1e6, 1), "unit": "Mpixels/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(t_gpu * 1e3, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "int32",
-            "data": f"synthetic JPEG (Pillow q90, gradient + sigma-20 noise), {len(data)} bytes",
+            "data": f"synthetic JPEG (Pillow q90, gradient + sigma-20 noise), {r['jpeg_bytes']} bytes",
             "config": {"workload": wl["desc"], "width": w, "height": h, "sampling": SAMPLING_NAMES[s],
                        "images_per_step_per_gpu": 1, "parallelism": f"image-parallel x{world} (no collective)"},
-            "latency_ms_per_image": {"gpu_huffman_pageable_bytes": round(t_gpu * 1e3, 4),
-                                     "gpu_huffman_pinned_bytes_device_destuff": round(t_pin * 1e3, 4),
-                                     "host_huffman_then_kernel": round(t_host * 1e3, 4)},
+            "latency_ms_per_image": r["latency_ms_per_image"],
             "output_checked_vs_oracle": ok,
             "roofline": None,
         }
         print(json.dumps(res), flush=True)
-    gd.close()
     if world > 1 and dist.is_initialized():
         dist.destroy_process_group()
     if not ok:
         log("FATAL: the decoded image differs from the oracle")
         sys.exit(1)
+
+
+def configs1_legs(args, hjd, torch, dist, world, rank, dev, qt):
+    """BASELINE configs[1] in the default line: one 1920x1080 4:2:0 frame per
+    launch (`fhd420`: resident coefficients -> BGRX, the single-image kernel
+    launch, src/decoder.cpp:402-409 + src/oclDCT8x8.cpp:275-304) and one FHD
+    JPEG end to end per step (`fhd420_jpeg`: bytes in host memory -> BGRX in
+    HBM with the GPU Huffman decode).  Both are latency-bound (the frame is
+    cache-resident), so they report time per launch / per image, not a
+    roofline fraction; both are checked against the oracle."""
+    wl = dict(WORKLOADS["fhd420"])
+    k = max(args.steps, 200)
+    r = pixel_batch(args, wl, hjd, torch, dist, world, rank, dev, qt, k, max(args.warmup, 10), measure=False)
+    r.pop("_pool_host")
+    fhd = {"value": r["value"], "unit": "Mpixels/s", "n_gpus": world, "launches": k,
+           "us_per_launch_kernel": round(r["_kernel_ms"] * 1e3, 3),
+           "us_per_launch_wall": round(r["_wall_max"] / k * 1e6, 3),
+           "workload": wl["desc"], "output_checked_vs_oracle": r["output_check"]["ok"],
+           "how": f"{k} back-to-back launches of one plan over one resident FHD frame; kernel time from HIP events "
+                  f"on the launch stream, wall time over the timed region (barrier + synchronize on both sides)",
+           "reference_path": "src/decoder.cpp:402-409 + src/oclDCT8x8.cpp:275-304 (clidct_run of one image)"}
+    wj = dict(WORKLOADS["fhd420_jpeg"])
+    j = jpeg_single_latency(args, wj, hjd, torch, dist, world, dev, args.steps, args.warmup)
+    fj = {"value": round(wj["width"] * wj["height"] * world / j["t_gpu"] / 1e6, 1), "unit": "Mpixels/s",
+          "n_gpus": world, "images": args.steps, "ms_per_image": round(j["t_gpu"] * 1e3, 4),
+          "latency_ms_per_image": j["latency_ms_per_image"], "jpeg_bytes": j["jpeg_bytes"],
+          "workload": wj["desc"], "output_checked_vs_oracle": j["ok"],
+          "reference_path": "src/decoder.cpp:262-416 (decode_huffman_data + decode_mcu_data of one file)"}
+    return fhd, fj
 
 
 def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
@@ -547,7 +638,10 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
             nchecked += 1
     # sums of < 2^31 values over <= 2^21 frames are exact in float64 (shard.aggregate's dtype)
     agg, ok = stream_check_totals(got, exp, id_sum, nchecked)
-    h2d = h2d_ceiling(torch, dev) if gpu_entropy and not d2h else None
+    # PCIe ceilings measured the way the stream moves bytes (concurrent slot streams, batch-sized pieces)
+    jpeg_mean = float(np.mean([len(d) for d in pool]))
+    h2d = pcie_ceiling(torch, dev, "h2d", per_batch * jpeg_mean, sorted({2, 4, nslots})) if gpu_entropy else None
+    d2h_c = pcie_ceiling(torch, dev, "d2h", h * pitch, sorted({2, 4, nslots})) if d2h else None
     if rank == 0:
         jpeg_bytes = int(np.mean([len(d) for d in pool]))
         res = {
@@ -574,10 +668,22 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
                            if gpu_entropy else "n/a (host Huffman)",
                 "host_scan_bytes_per_frame": round(host_scan / (nf * args.steps), 1) if gpu_entropy else None,
                 "h2d_ceiling": None if h2d is None else {
-                    "pinned_h2d_GBps": h2d, "jpeg_GBps_in_per_gpu": round(nf * args.steps * jpeg_bytes / wall_max / 1e9, 2),
-                    "frac": round(nf * args.steps * jpeg_bytes / wall_max / 1e9 / h2d, 3),
-                    "how": "pinned host -> device copy of 256 MiB buffers on this GPU after the timed region "
-                           "(tools/h2d_bw.py); the JPEG bytes are what crosses PCIe"},
+                    "pinned_h2d_GBps": h2d["GBps"],
+                    "jpeg_GBps_in_per_gpu": round(nf * args.steps * jpeg_bytes / wall_max / 1e9, 2),
+                    "frac": round(nf * args.steps * jpeg_bytes / wall_max / 1e9 / h2d["GBps"], 3),
+                    "rows": h2d["rows"],
+                    "how": "pinned host -> device copies on this GPU after the timed region, as the stream moves "
+                           "its JPEG scans: 2, 4 and the stream's slot count of concurrent streams, each copying "
+                           "one batch's bytes at a time (plus one stream of 256 MiB copies); the best rate is "
+                           "the ceiling"},
+                "d2h_ceiling": None if d2h_c is None else {
+                    "pinned_d2h_GBps": d2h_c["GBps"],
+                    "bgrx_GBps_out_per_gpu": round(nf * args.steps * h * pitch / wall_max / 1e9, 2),
+                    "frac": round(nf * args.steps * h * pitch / wall_max / 1e9 / d2h_c["GBps"], 3),
+                    "rows": d2h_c["rows"],
+                    "how": "device -> pinned host copies on this GPU after the timed region, as the stream "
+                           "returns frames: 2, 4 and the stream's slot count of concurrent streams, one frame's "
+                           "output per copy (plus one stream of 256 MiB copies); the best rate is the ceiling"},
                 "output_checked_vs_oracle": bool(ok)},
             "timed_seconds": round(wall_max, 3),
             "stream_check": {"frames_checked": int(agg["frames_checked"]), "checksum": int(agg["checksum"]),
@@ -598,22 +704,43 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
         sys.exit(1)
 
 
-def h2d_ceiling(torch, dev, mb=256, reps=8):
-    """Pinned host -> device copy rate on this GPU (GB/s), the PCIe ceiling of
-    the JPEG stream (the same measurement as tools/h2d_bw.py)."""
-    n = mb << 20
-    hbuf = torch.empty(n, dtype=torch.uint8).pin_memory()
-    dbuf = torch.empty(n, dtype=torch.uint8, device=dev)
-    s = torch.cuda.Stream(dev)
-    with torch.cuda.stream(s):
-        dbuf.copy_(hbuf, non_blocking=True)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    with torch.cuda.stream(s):
-        for _ in range(reps):
-            dbuf.copy_(hbuf, non_blocking=True)
-    torch.cuda.synchronize()
-    return round(n * reps / (time.perf_counter() - t0) / 1e9, 2)
+def pcie_ceiling(torch, dev, direction, chunk_bytes, stream_counts, total_bytes=4 << 30):
+    """Pinned host <-> device copy rate on this GPU (GB/s) the way the stream
+    uses PCIe: `n` concurrent HIP streams, each copying `chunk_bytes` pieces
+    (one batch's JPEG scans for H2D, one frame's BGRX for D2H) round-robin,
+    for every n in stream_counts, plus one stream of 256 MiB copies (the
+    round-3 measurement).  Returns {"GBps": best, "rows": [...]} -- the best
+    of these is the ceiling the stream's rate is divided by."""
+    chunk = max(1 << 20, int(chunk_bytes) // 4096 * 4096)
+    nmax = max(stream_counts)
+    span = max(256 << 20, chunk * nmax)
+    host = torch.empty(span, dtype=torch.uint8).pin_memory()
+    devb = torch.empty(span, dtype=torch.uint8, device=dev)
+    rows = []
+    for n, size in [(1, 256 << 20)] + [(n, chunk) for n in stream_counts]:
+        streams = [torch.cuda.Stream(dev) for _ in range(n)]
+        ncopies = max(n, int(total_bytes // size))
+        pieces = max(1, span // size)
+
+        def issue(k):
+            st = streams[k % n]
+            off = (k % pieces) * size
+            with torch.cuda.stream(st):
+                if direction == "h2d":
+                    devb[off:off + size].copy_(host[off:off + size], non_blocking=True)
+                else:
+                    host[off:off + size].copy_(devb[off:off + size], non_blocking=True)
+        for k in range(n):
+            issue(k)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(ncopies):
+            issue(k)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        rows.append({"streams": n, "copy_bytes": size, "GBps": round(ncopies * size / dt / 1e9, 2)})
+    del host, devb
+    return {"GBps": max(r["GBps"] for r in rows), "rows": rows}
 
 
 def numa_nodes():
@@ -743,14 +870,14 @@ _TORCHRUN_VARS = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP
                   "TORCHELASTIC_ENABLED")
 
 
-def stream_leg_command(world, dist_backend, frame_ids, per_gpu, port, environ):
+def stream_leg_command(world, dist_backend, frame_ids, per_gpu, port, environ, workload="stream4k420"):
     """The config-5 child run rank 0 starts: (argv, env, steps).  N=1: plain
     python; N>1: torch.distributed.run over the same N GPUs on `port` at
     127.0.0.1.  Enough steps of per_gpu frames per GPU to cover frame_ids
     global ids (>= 3).  The env drops this rank's torchrun variables, so the
     child agent sets its own."""
     steps = max(3, -(-frame_ids // (per_gpu * world)))
-    args = [os.path.abspath(__file__), "--gpus", str(world), "--workload", "stream4k420", "--steps", str(steps),
+    args = [os.path.abspath(__file__), "--gpus", str(world), "--workload", workload, "--steps", str(steps),
             "--warmup", "1", "--no-cpu", "--dist-backend", dist_backend, "--frames", str(per_gpu)]
     if world == 1:
         cmd = [sys.executable] + args
@@ -761,43 +888,138 @@ def stream_leg_command(world, dist_backend, frame_ids, per_gpu, port, environ):
     return cmd, env, steps
 
 
-def roofline_obj(achieved, bytes_per_launch, kernel_ms, traffic, trace):
-    """The line's roofline object: achieved = algorithmic bytes per launch / the
-    mean launch time measured with HIP events on the launch stream in this run;
-    traffic (PMC HBM bytes per launch) and the kernel-trace dispatch split come
-    from the committed profiles of the same command (profiles/)."""
+def roofline_obj(achieved, bytes_per_launch, kernel_ms, traffic, box=None):
+    """The line's roofline object.  Measured in THIS run: achieved =
+    algorithmic bytes per launch / the mean launch time from HIP events on the
+    launch stream; box_ceiling_GBps / frac_of_box_ceiling = the same bytes
+    against this box's own streaming rate for the kernel's read:write mix
+    (hjd_debug_rw_mix, same process, same buffers).  From ANOTHER run, and
+    labelled so: traffic = per-launch HBM bytes of the committed rocprofv3 PMC
+    passes of the same command (profiles/*pmc*.json), with their path and box."""
     r = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
          "frac": round(achieved / HBM_PEAK_GBPS, 4),
          "traffic": traffic[0] if traffic else None,
-         "traffic_source": traffic[1] if traffic else None,
          "algorithmic_bytes_per_launch": bytes_per_launch,
-         "kernel_ms_per_launch": round(kernel_ms, 4)}
-    if trace:
-        d, path = trace
-        r["kernel_trace_source"] = path
-        r["timed_dispatch_mean_ms"] = d["timed_mean_ms"]
-        r["frac_from_trace"] = round(bytes_per_launch / (d["timed_mean_ms"] / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)
+         "kernel_ms_per_launch": round(kernel_ms, 4),
+         "kernel_ms_source": "this run: HIP events on the launch stream around the timed launches"}
+    if traffic:
+        r["traffic_other_run"] = {"path": traffic[1], "box": traffic[2],
+                                  "what": "committed rocprofv3 PMC passes of the same command (FETCH_SIZE x2 + "
+                                          "WRITE_SIZE per launch), not measured in this run"}
+    if box:
+        r["box_ceiling_GBps"] = box["ceiling_GBps"]
+        r["frac_of_box_ceiling"] = round(achieved / box["ceiling_GBps"], 4)
+        r["box_ceiling_source"] = "this run: " + box["how"]
     return r
 
 
-def committed_dispatch_trace(workload, frames):
-    """The committed rocprofv3 kernel trace of the bench command, split into
-    warmup and timed dispatches (tools/ktrace_dispatch.py writes
-    profiles/*dispatch*.json); the latest file that covers this workload at this
-    launch size, or None."""
-    best = None
-    for p in sorted(glob.glob(os.path.join(REPO, "profiles", "*dispatch*.json"))):
-        try:
-            d = json.load(open(p))
-        except Exception:
-            continue
-        e = d.get("workloads", {}).get(workload) if isinstance(d, dict) else None
-        if e and e.get("frames_per_launch") == frames and e.get("timed_mean_ms"):
-            best = (e, os.path.relpath(p, REPO))
-    return best
+def box_ceiling(torch, ctx, src, dst, stream, mix, reps=5):
+    """This box's streaming rate for the fused kernel's read:write mix (KiB
+    per task: 6:8 at 4:2:0, 6:4 at 4:4:4), measured on the bench's own buffers
+    after the output check: hjd_debug_rw_mix with the kernel's launch shape
+    (nt, XCD order), the next unit's loads issued before this unit's stores
+    (the kernel's prefetch) at 1/2/4/8 units per wave, and one un-pipelined
+    shape; the best is the ceiling.  Read-only and write-only rates of the
+    same buffers are reported beside it."""
+    r, w = mix
+
+    def rate(rk, wk, upw, flags):
+        nbytes = ctx.debug_rw_mix(src, dst, rk, wk, upw, flags, stream)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            ctx.debug_rw_mix(src, dst, rk, wk, upw, flags, stream)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return round(nbytes / (e0.elapsed_time(e1) / reps) / 1e6, 1)
+    rows = [{"units_per_wave": upw, "pipelined": True, "GBps": rate(r, w, upw, 7)} for upw in (1, 2, 4, 8)]
+    rows.append({"units_per_wave": 1, "pipelined": False, "GBps": rate(r, w, 1, 3)})
+    best = max(rows, key=lambda x: x["GBps"])
+    return {"ceiling_GBps": best["GBps"], "mix_kib": f"{r}:{w}", "rows": rows,
+            "read_only_GBps": rate(6, 0, 4, 3), "write_only_GBps": rate(0, 8, 4, 3),
+            "how": f"hjd_debug_rw_mix {r}:{w} KiB read:write per wave-unit (the kernel's per-task bytes), 16 B per "
+                   f"lane, nt, XCD-contiguous in-order grid; pipelined at 1/2/4/8 units per wave and un-pipelined at "
+                   f"1; best of these; {reps} launches each on the bench's own coefficient and output buffers"}
 
 
-def pixel_batch(args, wl, hjd, torch, dist, world, rank, dev, qt, steps, warmup):
+def box_identity(torch):
+    """Which GPU this line was measured on (the container hostname is not
+    unique): the device's unique id and serial from rocm-smi, when readable."""
+    import subprocess
+    ident = {"hostname": socket.gethostname(), "device": torch.cuda.get_device_name(0)}
+    try:
+        r = subprocess.run(["rocm-smi", "--showserial", "--showuniqueid", "--json"], capture_output=True, text=True,
+                           timeout=20)
+        card = next(iter(json.loads(r.stdout).values()))
+        ident["unique_id"] = card.get("Unique ID")
+        ident["serial"] = card.get("Serial Number")
+    except Exception:
+        pass
+    return ident
+
+
+def clock_under_load(torch, ctx, dev, stream, launch, steps, kernel_ms):
+    """The shader clock the chip holds while `launch` runs (MI355X lowers it
+    under load, and devices differ: MI355X_MICROARCH.md 'DVFS give-back'):
+    hjd_debug_clock_probe samples s_memtime / s_memrealtime every 20 us on a
+    side stream beside `steps` more launches (untimed, after the timed region).
+    Returns the median / p10 / p90 of the per-interval clock, first 10 % of the
+    samples dropped (ramp)."""
+    interval = 2000                                   # 100-MHz ticks = 20 us
+    n = int(max(32, min(100000, steps * kernel_ms * 1e-3 * 1e8 * 0.9 // interval)))
+    buf = torch.zeros(2 * n, dtype=torch.int64, device=dev)
+    side = torch.cuda.Stream(dev)
+    torch.cuda.synchronize()
+    ctx.clock_probe(buf, n, interval, side)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(steps):
+        launch()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    smp = buf.cpu().numpy().reshape(n, 2).astype(np.float64)
+    f = np.diff(smp[:, 1]) / np.maximum(np.diff(smp[:, 0]), 1) * 0.1    # GHz (real-time ticks are 10 ns)
+    f = f[len(f) // 10:]
+    return {"sclk_GHz_median": round(float(np.median(f)), 3), "sclk_GHz_p10": round(float(np.percentile(f, 10)), 3),
+            "sclk_GHz_p90": round(float(np.percentile(f, 90)), 3), "samples": int(len(f)),
+            "kernel_ms_beside_probe": round(e0.elapsed_time(e1) / steps, 4),
+            "how": "hjd_debug_clock_probe: one wave on a side stream samples (s_memtime, s_memrealtime) every 20 us "
+                   f"while {steps} more launches run (after the timed region); clock = d(cycles) / d(10-ns ticks)"}
+
+
+STAGE_VARIANTS = {80: "memory_only", 4: "no_stores"}
+
+
+def stage_times(torch, plan, coefs, out, stream, product_ms, reps):
+    """Same-run ablation of the fused kernel on the bench's own plan and
+    buffers (after the output check; outputs are wrong by design): the
+    memory-only variant (loads, staging, LDS reads, stores; no IDCT, no colour
+    math) and the no-store variant.  What binds the kernel in THIS run is read
+    off these times, not asserted."""
+    res = {"product_ms": round(product_ms, 4)}
+    for st, name in STAGE_VARIANTS.items():
+        plan.launch_stages(st, coefs, out, stream)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            plan.launch_stages(st, coefs, out, stream)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        res[name + "_ms"] = round(e0.elapsed_time(e1) / reps, 4)
+    over = product_ms / res["memory_only_ms"] - 1
+    res["product_over_memory_only_pct"] = round(100 * over, 2)
+    if over <= 0.02:
+        res["binding"] = ("memory: the product runs within 2 % of its own memory-only variant (same loads, LDS "
+                          "traffic and stores, no IDCT or colour math)")
+    else:
+        res["binding"] = (f"instruction issue on top of memory: the product takes {100 * over:.1f} % longer than its "
+                          f"memory-only variant (same loads, LDS traffic and stores)")
+    res["how"] = (f"hjd_debug_plan_launch_stages on this run's plan and buffers, {reps} launches each after one warmup, "
+                  f"HIP events; timing-only variants with wrong outputs by design")
+    return res
+
+
+def pixel_batch(args, wl, hjd, torch, dist, world, rank, dev, qt, steps, warmup, measure=True):
     """One pixel workload on this rank: inputs resident in HBM, W untimed + K
     timed launches of one plan over the whole batch (barrier + synchronize on
     both sides, max over ranks), then every frame of the last launch checked
@@ -880,12 +1102,20 @@ def pixel_batch(args, wl, hjd, torch, dist, world, rank, dev, qt, steps, warmup)
     # every frame of the timed launch's output vs the oracle (outside the timed region)
     pool_host = pool16.cpu().numpy()
     checked = check_batch_vs_oracle(torch, out, pool_host, qt, wl, ofmt)
+    # same-run measurements on the same buffers (they overwrite `out`, so after the check)
+    stages = box = clock = None
+    if measure and not i32 and ofmt == hjd.OUT_BGRX and s in (0, 1) and not args.no_stages:
+        clock = clock_under_load(torch, ctx, dev, stream, lambda: plan.launch(coefs, out, stream, grid_blocks=args.grid),
+                                 steps, kernel_ms)
+        stages = stage_times(torch, plan, coefs, out, stream, kernel_ms, min(steps, 10))
+        box = box_ceiling(torch, ctx, coefs, out, stream, (6, 8) if s == 1 else (6, 4))
     tasks = plan.tasks
     plan.close()
     del coefs, out, pool16, plan
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
     return {"value": round(value, 1), "output_check": checked, "device_copy_GBps": copy_gbps,
+            "stages": stages, "box": box, "clock": clock,
             "_pool_host": pool_host, "_wall_max": wall_max, "_kernel_ms": kernel_ms, "_achieved": achieved,
             "_bytes_per_launch": bytes_per_launch, "_tasks": tasks}
 
@@ -899,6 +1129,12 @@ def main():
     ap.add_argument("--frames", type=int, default=0, help="override batch size")
     ap.add_argument("--grid", type=int, default=0, help="persistent grid (workgroups), 0 = default")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-stages", action="store_true",
+                    help="skip the same-run stage ablation and box-ceiling measurements of the pixel batches")
+    ap.add_argument("--no-fhd", action="store_true",
+                    help="4k420: skip the configs[1] legs (single FHD launch, one FHD JPEG end to end)")
+    ap.add_argument("--no-d2h", action="store_true",
+                    help="skip the D2H-on config-5 stream leg (config5_stream_d2h)")
     ap.add_argument("--no-444", action="store_true",
                     help="4k420: skip the configs[3] 4:4:4 batch reported under config4_444")
     ap.add_argument("--stream-frame-ids", type=int, default=100000,
@@ -969,36 +1205,40 @@ def main():
         r4 = pixel_batch(args, wl4, hjd, torch, dist, world, rank, dev, qt, args.steps, args.warmup)
         r4.pop("_pool_host")
         traffic4 = committed_traffic("4k444", wl4["frames"])
-        trace4 = committed_dispatch_trace("4k444", wl4["frames"])
         config4 = {
             "metric": "Mpixels/s decoded (dequant+IDCT+colour)", "value": r4["value"], "unit": "Mpixels/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(r4["_wall_max"] / args.steps * 1e3, 4),
             "workload": wl4["desc"], "frames_per_gpu": wl4["frames"], "sampling": "4:4:4",
             "output_checked_vs_oracle": r4["output_check"]["ok"], "output_check": r4["output_check"],
-            "roofline": roofline_obj(r4["_achieved"], r4["_bytes_per_launch"], r4["_kernel_ms"], traffic4, trace4),
-            "binding_limit": "VALU issue, not HBM: removing either the IDCT or the colour math leaves the "
-                             "kernel at its memory time, ~9 % faster (ablation, "
-                             "profiles/r03_ablation_4k444_4k420.json; DESIGN.md s3)",
+            "roofline": roofline_obj(r4["_achieved"], r4["_bytes_per_launch"], r4["_kernel_ms"], traffic4, r4["box"]),
+            "stages": r4["stages"], "box_ceiling": r4["box"], "clock_under_load": r4["clock"],
             "reference_path": "src/idct8x8.cl:168-192 (batch_idct_csc_444), src/decoder.cpp:457-471"}
         checked_all_ok = checked["ok"] and r4["output_check"]["ok"]
     else:
         checked_all_ok = checked["ok"]
+    # configs[1] (single FHD 4:2:0 launch; one FHD JPEG end to end) in the same default run
+    fhd = fhd_jpeg = None
+    if args.workload == "4k420" and not args.no_fhd:
+        fhd, fhd_jpeg = configs1_legs(args, hjd, torch, dist, world, rank, dev, qt)
+        checked_all_ok = checked_all_ok and fhd["output_checked_vs_oracle"] and fhd_jpeg["output_checked_vs_oracle"]
 
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu:
             log("running CPU baseline leg ...")
             cpu = cpu_baseline(pool_host, qt, wl, value)
-        stream5 = None
+        stream5 = stream5_d2h = None
         if not args.no_stream and args.workload == "4k420":
             torch.cuda.synchronize()
             torch.cuda.empty_cache()
             if world > 1:
                 dist.destroy_process_group()   # the other ranks are leaving; the child run has its own group
             stream5 = config5_stream_leg(world, args.dist_backend, args.stream_frame_ids)
+            if not args.no_d2h:
+                stream5_d2h = config5_stream_leg(world, args.dist_backend, args.stream_frame_ids,
+                                                 workload="stream4k420_d2h")
         traffic = committed_traffic(args.workload, nf)
-        trace = committed_dispatch_trace(args.workload, nf)
         res = {
             "metric": "Mpixels/s decoded (dequant+IDCT+colour) at 1/2/4/8 GPUs; % HBM roofline",
             "value": round(value, 1),
@@ -1022,11 +1262,16 @@ def main():
                        "tasks_per_launch": tasks},
             "output_checked_vs_oracle": checked["ok"],
             "output_check": checked,
-            "roofline": roofline_obj(achieved, bytes_per_launch, kernel_ms, traffic, trace),
+            "roofline": roofline_obj(achieved, bytes_per_launch, kernel_ms, traffic, res_px["box"]),
+            "stages": res_px["stages"], "box_ceiling": res_px["box"], "clock_under_load": res_px["clock"],
+            "box": box_identity(torch),
             "cpu_baseline": cpu,
             "device_copy_GBps": res_px["device_copy_GBps"],
             "config4_444": config4,
             "config5_stream": stream5,
+            "config5_stream_d2h": stream5_d2h,
+            "fhd420": fhd,
+            "fhd420_jpeg": fhd_jpeg,
         }
         if cpu and "reference" in cpu:
             res["cpu_reference"] = cpu.pop("reference")
@@ -1061,7 +1306,7 @@ def _wait_sibling_ranks_exit(timeout_s=60.0):
         time.sleep(0.5)
 
 
-def config5_stream_leg(world, dist_backend, frame_ids=100000):
+def config5_stream_leg(world, dist_backend, frame_ids=100000, workload="stream4k420"):
     """BASELINE configs[4] on the same GPUs, measured in the same default run:
     rank 0 starts a child `bench.py --workload stream4k420` (N=1: plain python;
     N>1: torch.distributed.run over the same N GPUs on a fresh port, the frame
@@ -1075,14 +1320,14 @@ def config5_stream_leg(world, dist_backend, frame_ids=100000):
     import subprocess
     # BASELINE configs[4] is a 100k-image stream: enough steps of 1024 frames per
     # GPU (G = 1024 * world ids per step) to cover `frame_ids` global ids
-    per_gpu = int(os.environ.get("HJD_BENCH_STREAM_FRAMES", WORKLOADS["stream4k420"]["frames"]))  # tests: smaller
+    per_gpu = int(os.environ.get("HJD_BENCH_STREAM_FRAMES", WORKLOADS[workload]["frames"]))  # tests: smaller
     port = 0
     if world > 1:
         sk = socket.socket()
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
         sk.close()
-    cmd, env, _ = stream_leg_command(world, dist_backend, frame_ids, per_gpu, port, os.environ)
+    cmd, env, _ = stream_leg_command(world, dist_backend, frame_ids, per_gpu, port, os.environ, workload)
     if world > 1:
         _wait_sibling_ranks_exit()
     log("running config-5 stream leg:", " ".join(cmd[1:]))
@@ -1105,6 +1350,8 @@ def config5_stream_leg(world, dist_backend, frame_ids=100000):
             "value_per_gpu": round(d["value"] / d["n_gpus"], 1),
             "jpeg_GBps_in": d["end_to_end"]["jpeg_GBps_in"], "destuff": d["end_to_end"]["destuff"],
             "h2d_ceiling": d["end_to_end"].get("h2d_ceiling"),
+            "d2h_ceiling": d["end_to_end"].get("d2h_ceiling"),
+            "output": d["config"]["output"],
             "output_checked_vs_oracle": d["end_to_end"]["output_checked_vs_oracle"],
             "steps_checked": d["stream_check"]["steps_checked"],
             "command": " ".join(["python"] + [os.path.basename(c) if c.endswith("bench.py") else c

@@ -165,6 +165,42 @@ int hjd_debug_csc(hjd_ctx* ctx, const int32_t* d_y, const int32_t* d_u, const in
  * device and writes the 2^27 BGRX words to d_out (512 MiB). */
 int hjd_debug_csc_exhaustive(hjd_ctx* ctx, uint32_t* d_out, int mode, void* stream);
 
+/* Same-run measurement of the fused kernel's stages (bench.py): launch the
+ * plan's persistent kernel with stages skipped.  Outputs are WRONG by design
+ * (timing only).  stages: 80 = memory only (coefficient loads, staging, LDS
+ * reads and BGRX stores kept; no IDCT, no colour math), 4 = no stores,
+ * 16 = no IDCT, 64 = no colour math, 20 = no IDCT and no stores, 8 = no colour
+ * stage, 24 = neither IDCT nor colour stage.  4:2:0 / 4:4:4, int16 zigzag
+ * input, BGRX output only. */
+int hjd_debug_plan_launch_stages(hjd_plan* plan, int stages, const void* d_coefs, void* d_out, void* stream);
+
+/* The box's streaming ceiling for a read:write byte mix (bench.py's
+ * frac_of_box_ceiling): units of read_kib KiB read + write_kib KiB written
+ * (16 B per lane, coalesced), units_per_wave consecutive units per wave, one
+ * launch over min(src_bytes / read_kib KiB, dst_bytes / write_kib KiB) units.
+ * flags bit 0: non-temporal loads and stores; bit 1: XCD-contiguous group
+ * order (the fused kernel's); bit 2: pipelined (the next unit's loads issued
+ * before this unit's stores, as the fused kernel prefetches its next task).  Mixes (KiB): 6:8 (4:2:0 task), 6:4 (4:4:4
+ * task), 0:8, 6:0, 4:4, 3:4.  *units_out = units moved (bytes = units *
+ * (read_kib + write_kib) KiB).  dst_bytes >= 1 KiB. */
+int hjd_debug_rw_mix(hjd_ctx* ctx, const void* d_src, void* d_dst, int64_t src_bytes, int64_t dst_bytes,
+                     int read_kib, int write_kib, int units_per_wave, int flags, void* stream, int64_t* units_out);
+
+/* Clock probe: one wave on `stream` samples the shader clock counter and the
+ * 100-MHz real-time counter every interval_ticks (>= 100) real-time ticks,
+ * nsamples times: d_out[2i] = real-time ticks, d_out[2i+1] = shader cycles
+ * (2 * nsamples uint64 words).  Launched beside a kernel on another stream,
+ * consecutive samples give the clock the chip holds under that load
+ * (delta cycles / delta ticks * 100 MHz).  Ends after nsamples intervals. */
+int hjd_debug_clock_probe(hjd_ctx* ctx, uint64_t* d_out, int nsamples, int interval_ticks, void* stream);
+
+/* The 4:4:4 kernels' d16 gather (ds_read_u16_d16_hi) is valid only where that
+ * load zeroes the low half of its destination.  *probe_zeroes: the one-wave
+ * hardware probe's answer for `device` (run once per device at first use;
+ * HJD_D16_PROBE=fail forces 0); *selected: whether the 4:4:4 launches take
+ * the d16 kernels (the probe, unless HJD_D16=0/1 overrides it). */
+int hjd_debug_d16_gather(int device, int* probe_zeroes, int* selected);
+
 #ifdef __cplusplus
 }
 #endif

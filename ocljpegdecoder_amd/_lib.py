@@ -75,6 +75,14 @@ SIGNATURES = {
     "hjd_debug_csc": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                      ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]),
     "hjd_debug_csc_exhaustive": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
+    "hjd_debug_plan_launch_stages": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                                    ctypes.c_void_p]),
+    "hjd_debug_rw_mix": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                        ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                        ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)]),
+    "hjd_debug_d16_gather": (ctypes.c_int, [ctypes.c_int, c_i32p, c_i32p]),
+    "hjd_debug_clock_probe": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                             ctypes.c_void_p]),
 }
 
 _lib = None

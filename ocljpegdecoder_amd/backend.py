@@ -118,6 +118,34 @@ class Context:
         check(self.lib.hjd_debug_csc_exhaustive(self.handle, out.data_ptr(), mode, _stream_ptr(stream)),
               "hjd_debug_csc_exhaustive")
 
+    def debug_rw_mix(self, src, dst, read_kib: int, write_kib: int, units_per_wave: int = 2, flags: int = 3,
+                     stream=None) -> int:
+        """The box's streaming ceiling kernel (hjd_debug_rw_mix): one launch;
+        returns the bytes it moves (read + written)."""
+        for t in (src, dst):
+            if not (t.is_cuda and t.is_contiguous()):
+                raise ValueError("debug_rw_mix needs contiguous device tensors")
+        units = ctypes.c_int64(0)
+        check(self.lib.hjd_debug_rw_mix(self.handle, src.data_ptr(), dst.data_ptr(), src.numel() * src.element_size(),
+                                        dst.numel() * dst.element_size(), int(read_kib), int(write_kib),
+                                        int(units_per_wave), int(flags), _stream_ptr(stream), ctypes.byref(units)),
+              "hjd_debug_rw_mix")
+        return units.value * (read_kib + write_kib) * 1024
+
+    def clock_probe(self, out, nsamples: int, interval_ticks: int, stream=None):
+        """Launch the clock probe (hjd_debug_clock_probe) writing 2*nsamples
+        int64 words into `out` (a device tensor); see clock_summary()."""
+        if not (out.is_cuda and out.is_contiguous() and out.element_size() == 8 and out.numel() >= 2 * nsamples):
+            raise ValueError("clock_probe needs a contiguous int64 device tensor of >= 2*nsamples elements")
+        check(self.lib.hjd_debug_clock_probe(self.handle, out.data_ptr(), int(nsamples), int(interval_ticks),
+                                             _stream_ptr(stream)), "hjd_debug_clock_probe")
+
+    def d16_gather(self):
+        """(probe_zeroes, selected) of hjd_debug_d16_gather for this device."""
+        a, b = ctypes.c_int32(-1), ctypes.c_int32(-1)
+        check(self.lib.hjd_debug_d16_gather(self.device, ctypes.byref(a), ctypes.byref(b)), "hjd_debug_d16_gather")
+        return bool(a.value), bool(b.value)
+
 
 @dataclass
 class FrameSpec:
@@ -205,6 +233,14 @@ class Plan:
         cp = self._check_tensor(coefs, "coefs", self.coef_elem_bytes, self.coef_elems_needed * self.coef_elem_bytes)
         op = self._check_tensor(out, "out", 0, self.out_bytes_needed)
         check(self.lib.hjd_plan_launch(self.handle, cp, op, _stream_ptr(stream), grid_blocks), "hjd_plan_launch")
+
+    def launch_stages(self, stages: int, coefs, out, stream=None):
+        """Timing-only launch with kernel stages skipped (hjd_debug_plan_launch_stages;
+        80 memory only, 4 no stores, ...): the output is WRONG by design."""
+        cp = self._check_tensor(coefs, "coefs", self.coef_elem_bytes, self.coef_elems_needed * self.coef_elem_bytes)
+        op = self._check_tensor(out, "out", 0, self.out_bytes_needed)
+        check(self.lib.hjd_debug_plan_launch_stages(self.handle, int(stages), cp, op, _stream_ptr(stream)),
+              "hjd_debug_plan_launch_stages")
 
     def close(self):
         if self.handle:

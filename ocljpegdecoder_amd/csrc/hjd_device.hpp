@@ -108,6 +108,15 @@ __host__ __device__ __forceinline__ void idct8(int (&v)[8])
 // the same way.  The stage-1/2 products keep the reference's (+4) >> 3 at
 // unit scale and are scaled after it (x4 in the final add chains); the
 // stage-3 terms 4 * floor((181 s + 128) / 256) = ((181 s + 128) >> 6) & ~3.
+// Outside the legal domain the reference itself is undefined (iclp is read
+// out of bounds once (r >> 14) leaves [-512, 511], and its int math can
+// overflow), so no output is specified there.  This form's own limit: the 4x
+// sums wrap once |r| > 2^29 (an unclamped sample beyond about +-32768, far
+// outside [-512, 511]), where idct8<true> wrapped only past 2^31; such a
+// sample may then clamp to the opposite bound.  Likewise the int16 path
+// dequantises with 16-bit products (v_pk_mul_lo_u16) and the row pass takes
+// 24-bit operands.  The kernel is bit-exact wherever the reference is defined
+// (tests/test_idct_forms.py, the clamp-edge vectors of test_gpu_parity.py).
 template <int kLevel = 0>
 __host__ __device__ __forceinline__ void idct8_col_hi(int (&v)[8])
 {

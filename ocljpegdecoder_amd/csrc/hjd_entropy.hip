@@ -412,7 +412,9 @@ Caps make_caps(int max_frames, int64_t max_scan_bytes, int64_t max_blocks, int s
     const int64_t ef = static_cast<int64_t>(max_frames) * kMaxScans;
     c.max_subs = (max_scan_bytes * 8 + sub_bits - 1) / sub_bits + ef;
     c.max_wgs = (c.max_subs + kOwn - 1) / kOwn + ef;
-    c.max_segs = max_blocks / 3 + ef;
+    // restart segments: one per restart interval; a non-interleaved scan (or a
+    // gray file) with Ri = 1 has one per block, so blocks + one per entropy frame
+    c.max_segs = max_blocks + ef;
     c.max_tiles = max_scan_bytes / kTileBytes + max_frames;
     const size_t per_frame = (sizeof(EntFrame) + sizeof(HuffLut) * kMaxTables) * kMaxScans + sizeof(FrameRecord) +
                              192 * 4 + sizeof(RawFrame);
@@ -2076,11 +2078,20 @@ int hjd_gdec::stage_frames(const uint8_t* const* datas, const size_t* sizes, int
     data_used = 0;
     int64_t blocks = 0;
     RawCursor cur;
-    // what the frames after i may need in either area, whichever path they
-    // take: a frame with a device-destuffed scan is placed only if the rest
-    // still fit, so a batch sized by its file bytes never fails on placement
+    // what the frames after i need at least in the data area, whichever path
+    // they take: a frame with a device-destuffed scan is placed only if the
+    // rest still fit, so a batch sized by its file bytes never fails on
+    // placement.  A single-scan file needs its entropy-coded bytes plus pad
+    // (destuffed or raw), a multi-scan file data_need() of its size; so a
+    // batch sized by its scan bytes (hjd_gdec_create) keeps the device destuff
+    // for its pinned files wherever their raw scans fit.
     std::vector<uint64_t> tail(static_cast<size_t>(n) + 1, 0);
-    for (int i = n - 1; i >= 0; --i) tail[i] = tail[i + 1] + data_need(sizes[i]);
+    for (int i = n - 1; i >= 0; --i) {
+        hjd_internal::ScanHeader h;
+        const bool one_scan = datas[i] && hjd_internal::parse_scan_header(datas[i], sizes[i], &h) == HJD_OK &&
+                              h.extra_scans == 0 && h.scan_offset <= sizes[i];
+        tail[i] = tail[i + 1] + (one_scan ? align_up(sizes[i] - h.scan_offset + kDataPad, 16) : data_need(sizes[i]));
+    }
     for (int i = 0; i < n; ++i) {
         if (data_used >= data_cap()) return set_error(HJD_E_INVALID, "scan bytes exceed the batch capacity");
         int mode;

@@ -94,6 +94,13 @@ int parse_scan_headers(const uint8_t* data, size_t size, std::vector<ScanHeader>
 // hjd_ctx accessors for the other translation units
 int ctx_num_cu(const struct ::hjd_ctx* ctx);
 
+// d16 gather (hjd_probe.hip): 1 if ds_read_u16_d16_hi zeroes the low half of
+// its destination on `device` (one-wave probe, run once per device and
+// cached; HJD_D16_PROBE=fail forces 0).  d16_gather_selected(): whether the
+// 4:4:4 launches take the kVarD16 kernels (the probe, or HJD_D16=0/1).
+int d16_probe(int device);
+bool d16_gather_selected(int device);
+
 }  // namespace hjd_internal
 
 namespace hjd_internal {

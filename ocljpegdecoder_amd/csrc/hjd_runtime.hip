@@ -102,26 +102,20 @@ static int64_t latency_max_tasks()
 
 // The 4:4:4 kernels gather coefficient pairs with ds_read_u16_d16_hi
 // (hjd::kVarD16), which relies on d16 LDS loads zeroing the other half of
-// the register.  That is the sramecc+ behaviour (MI355X as deployed,
-// profiles/r03_d16_probe.txt); on a sramecc- device they keep it, so the
-// variant is taken only when the device's ISA name says sramecc+.
-// HJD_D16=0 / 1 overrides the default (kD16Default) for A/B and tests.
+// the register.  MI355X as deployed (sramecc+) does that
+// (profiles/r03_d16_probe.txt); a half-preserving part would corrupt the
+// pairs.  So the variant is taken only where the one-wave hardware probe
+// (hjd_probe.hip, once per device) saw every lane's low half zeroed; the
+// v_perm kernels are the fallback.  HJD_D16=0 / 1 overrides the probe (A/B).
 constexpr bool kD16Default = true;   // same-box A/B: profiles/r03_444_d16_gather_ab.json
-static bool device_d16_gather(int device)
+bool hjd_internal::d16_gather_selected(int device)
 {
     const char* e = getenv("HJD_D16");
-    if (e ? e[0] == '0' : !kD16Default) return false;
-    static std::mutex mu;
-    static std::vector<int> known;   // -1 unknown, 0 / 1
-    std::lock_guard<std::mutex> lock(mu);
-    if (device < 0) return false;
-    if (static_cast<size_t>(device) >= known.size()) known.resize(device + 1, -1);
-    if (known[device] < 0) {
-        hipDeviceProp_t p;
-        known[device] = hipGetDeviceProperties(&p, device) == hipSuccess && strstr(p.gcnArchName, "sramecc+") != nullptr;
-    }
-    return known[device] == 1;
+    if (e) return e[0] != '0';
+    if (!kD16Default || device < 0) return false;
+    return hjd_internal::d16_probe(device) == 1;
 }
+static bool device_d16_gather(int device) { return hjd_internal::d16_gather_selected(device); }
 
 static int geometry(int width, int height, int sampling, int& mcu_w, int& mcu_h, int& bpm, int& tasks_mcus);
 static int decode_grid(int sampling, int fmt, int64_t tasks);
@@ -203,18 +197,20 @@ int hjd_internal::launch_decode(int device, int num_cu, int sampling, int input_
         HJD_HIP(hipGetLastError());
         return HJD_OK;
     }
-#ifdef HJD_ABLATION
-    if (fmt == 0 && variant > 1) {
+    if (fmt == 0 && variant > 3) {   // stage-skipping measurement variants (hjd_debug_plan_launch_stages)
         if (sg.index > 1) return hjd_internal::set_error(HJD_E_INVALID, "ablation variants are 4:4:4/4:2:0 only");
         K k = nullptr;
         const bool s420 = sampling == HJD_YUV420;
+        const bool d16 = !s420 && device_d16_gather(device);   // as the product 4:4:4 kernel gathers
         switch (variant) {
-        case 4: k = s420 ? hjd::decode_kernel<1, 0, 4> : hjd::decode_kernel<0, 0, 4>; break;
+        case 4: k = s420 ? hjd::decode_kernel<1, 0, 4> : d16 ? hjd::decode_kernel<0, 0, 4 | hjd::kVarD16>
+                                                             : hjd::decode_kernel<0, 0, 4>; break;
         case 8: k = s420 ? hjd::decode_kernel<1, 0, 8> : hjd::decode_kernel<0, 0, 8>; break;
         case 16: k = s420 ? hjd::decode_kernel<1, 0, 16> : hjd::decode_kernel<0, 0, 16>; break;
         case 20: k = s420 ? hjd::decode_kernel<1, 0, 20> : hjd::decode_kernel<0, 0, 20>; break;
         case 24: k = s420 ? hjd::decode_kernel<1, 0, 24> : hjd::decode_kernel<0, 0, 24>; break;
-        case 64: k = s420 ? hjd::decode_kernel<1, 0, 64> : hjd::decode_kernel<0, 0, 64>; break;
+        case 64: k = s420 ? hjd::decode_kernel<1, 0, 64> : d16 ? hjd::decode_kernel<0, 0, 64 | hjd::kVarD16>
+                                                               : hjd::decode_kernel<0, 0, 64>; break;
         case 80: k = s420 ? hjd::decode_kernel<1, 0, 80> : hjd::decode_kernel<0, 0, 80>; break;
         default: return hjd_internal::set_error(HJD_E_INVALID, "unknown ablation variant %d", variant);
         }
@@ -224,7 +220,6 @@ int hjd_internal::launch_decode(int device, int num_cu, int sampling, int input_
         HJD_HIP(hipGetLastError());
         return HJD_OK;
     }
-#endif
     // [sampling index][input format][variant bits 0-1]
     const int key = (sg.index << 3) | (fmt << 2) | (variant & 3);
 #define HJD_K4(S, F) hjd::decode_kernel<S, F, 0>, hjd::decode_kernel<S, F, 1>, hjd::decode_kernel<S, F, 2>, \
@@ -488,6 +483,24 @@ int hjd_plan_launch(hjd_plan* plan, const void* d_coefs, void* d_out, void* stre
                                        reinterpret_cast<const hjd_internal::FrameRecord*>(plan->d_frames),
                                        plan->nframes, plan->tasks, d_out, stream, grid_blocks, plan->out_format,
                                        plan->kernel_mode);
+}
+
+int hjd_debug_plan_launch_stages(hjd_plan* plan, int stages, const void* d_coefs, void* d_out, void* stream)
+{
+    if (!plan) return fail(HJD_E_INVALID, "plan is NULL");
+    if (stages != 4 && stages != 16 && stages != 20 && stages != 64 && stages != 80 && stages != 8 && stages != 24)
+        return fail(HJD_E_INVALID, "unknown stage variant %d", stages);
+    if (plan->input_format != HJD_IN_Q16_ZIGZAG || plan->out_format != HJD_OUT_BGRX ||
+        (plan->sampling != HJD_YUV420 && plan->sampling != HJD_YUV444))
+        return fail(HJD_E_INVALID, "stage variants: 4:2:0 / 4:4:4, int16 zigzag in, BGRX out");
+    if (plan->tasks == 0) return HJD_OK;
+    if (!d_coefs || !d_out || ((reinterpret_cast<uintptr_t>(d_coefs) | reinterpret_cast<uintptr_t>(d_out)) & 15))
+        return fail(HJD_E_INVALID, "NULL or unaligned device buffer");
+    return hjd_internal::launch_decode(plan->ctx->device, plan->ctx->num_cu, plan->sampling, plan->input_format, stages,
+                                       d_coefs, plan->d_qt,
+                                       reinterpret_cast<const hjd_internal::FrameRecord*>(plan->d_frames),
+                                       plan->nframes, plan->tasks, d_out, stream, 0, plan->out_format,
+                                       HJD_KERNEL_PERSISTENT);
 }
 
 int hjd_idct_blocks(hjd_ctx* ctx, const int32_t* d_in, int32_t* d_out, int64_t nblocks, void* stream)

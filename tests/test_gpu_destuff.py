@@ -318,6 +318,30 @@ def test_pinned_capacity_by_entropy_bytes_falls_back_to_host(hjd, ctx, monkeypat
             gd.decode_coefs(pinned, coefs)
 
 
+def test_pinned_capacity_by_raw_scan_bytes_stays_on_device(hjd, ctx, monkeypatch):
+    """sized by the files' entropy-coded bytes as they lie in
+    the file (stuffing and markers included: size - scan_offset), every pinned
+    frame's raw scan fits, so none may fall back to the host destuff -- the
+    placement must not reserve whole file sizes for the frames still to come."""
+    import torch
+    datas = _pil_files()
+    raw = sum(len(d) - hjd.parse(d).scan_offset for d in datas)
+    pinned = [hjd.pinned_bytes(d) for d in datas]
+    infos = [hjd.parse(d) for d in datas]
+    total = sum(i.nblocks for i in infos)
+    coefs = torch.full((total, 64), 0x5A5A, dtype=torch.int16, device="cuda")
+    monkeypatch.setenv("HJD_DESTUFF", "auto")
+    with hjd.GpuDecoder(ctx, len(datas), raw, total) as gd:
+        offs = gd.decode_coefs(pinned, coefs)
+        assert gd.last_bytes()["host_scan_bytes"] == 0
+        status = gd.sync()
+        host = coefs.cpu().numpy()
+        for d, o, i, s in zip(datas, offs, infos, status):
+            ref, _ = hjd.decode_coefs(d)
+            np.testing.assert_array_equal(host[o:o + i.nblocks], ref)
+            assert s & ~1 == 0
+
+
 def test_pinned_input_reusable_on_return(hjd, ctx, monkeypatch):
     """hjd_gdec_decode* may return before the kernels run, but
     not before the DMA has read the caller's pinned bytes; overwriting them

@@ -127,3 +127,43 @@ def test_444_gather_forms_vs_oracle(hjd, ctx, monkeypatch, d16):
         for out_format in (0, 1):
             got = _run(hjd, ctx, coefs, qt, w, h, 0, 1, out_format=out_format)
             np.testing.assert_array_equal(got, _expect(exp, out_format), err_msg=f"{w}x{h} fmt={out_format}")
+
+
+def test_d16_probe_selects_gather(hjd, ctx, monkeypatch):
+    """Without an override the 4:4:4 gather form follows the one-wave hardware
+    probe (hjd_probe.hip), not the device's ISA name; MI355X as deployed
+    (sramecc+) zeroes the d16 load's low half, so the probe passes there."""
+    import torch
+    monkeypatch.delenv("HJD_D16", raising=False)
+    zeroes, selected = ctx.d16_gather()
+    arch = torch.cuda.get_device_properties(0).gcnArchName
+    print("device", arch, "probe zeroes low half", zeroes, "d16 selected", selected)
+    assert selected == zeroes
+    if "sramecc+" in arch:
+        assert zeroes, "sramecc+ part did not zero the d16 load's low half"
+
+
+def test_d16_probe_failure_falls_back_to_perm_gather():
+    """HJD_D16_PROBE=fail makes the probe report a half-preserving part: the
+    runtime must then take the v_perm kernels, and 4:4:4 stays bit-exact.  A
+    child process, because the probe result is cached per process."""
+    import os
+    import subprocess
+    import sys
+    code = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, REPO); sys.path.insert(0, REPO + "/tests")
+import ocljpegdecoder_amd as hjd, oracle_py as O
+ctx = hjd.Context(0)
+assert ctx.d16_gather() == (False, False), ctx.d16_gather()
+w, h = 1920, 1080
+coefs, qt = O.synthetic_coefs(w, h, 0, seed=5)
+out, plan = hjd.decode_frame(ctx, torch.from_numpy(coefs).cuda(), qt, w, h, 0)
+torch.cuda.synchronize()
+assert np.array_equal(out.cpu().numpy().view(np.uint32), O.decode_q16(coefs, qt, w, h, 0))
+print("fallback ok")
+""".replace("REPO", repr(O.REPO))
+    env = {k: v for k, v in os.environ.items() if k != "HJD_D16"}
+    env["HJD_D16_PROBE"] = "fail"
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "fallback ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]

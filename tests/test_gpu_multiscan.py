@@ -65,6 +65,21 @@ def test_multiscan_coefficients(hjd, ctx, sub_bits):
         assert s & ~1 == 0, (i, s)
 
 
+def test_restart_every_block_fits_exact_capacity(hjd, ctx):
+    """a non-interleaved scan with Ri = 1 (and a gray file with
+    Ri = 1) has one restart interval per BLOCK; a decoder sized by the
+    batch's exact block count (what hjd_gdec_create documents as enough) must
+    take it."""
+    data, expect = _multiscan(200, 120, 1, SPLITS[0], 1, seed=123)
+    gray = _pil(96, 40, 90, 0, seed=124, gray=True, restart_marker_blocks=1)
+    datas = [data, gray]
+    expects = [expect, hjd.decode_coefs(gray)[0]]
+    got, status = _decode_coefs(hjd, ctx, datas)
+    for i, (g, e, st) in enumerate(zip(got, expects, status)):
+        np.testing.assert_array_equal(g, e, err_msg=f"file {i}")
+        assert st & ~1 == 0, (i, st)
+
+
 def test_multiscan_pinned_inputs_take_host_destuff(hjd, ctx):
     """Pinned inputs normally reach the GPU raw; a multi-scan file's scans are
     found and destuffed on the host instead, in the same batch."""

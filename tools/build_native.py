@@ -26,7 +26,8 @@ OBJDIR = os.path.join(REPO, "build", "obj")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("HJD_ARCH", "gfx950")
 
-HIP_SOURCES = ["hjd_runtime.hip", "idct_compat.hip", "stream_pipeline.hip", "hjd_entropy.hip", "numa_affinity.hip"]
+HIP_SOURCES = ["hjd_runtime.hip", "idct_compat.hip", "stream_pipeline.hip", "hjd_entropy.hip", "numa_affinity.hip",
+               "hjd_probe.hip"]
 CXX_SOURCES = ["jpeg_host.cpp"]
 
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", f"-I{INCLUDE}", f"-I{CSRC}"]

@@ -11,7 +11,7 @@ FLAGS="-std=c++17 -O1 -g -fno-omit-frame-pointer -I$R/include -I$R/ocljpegdecode
 C=$R/ocljpegdecoder_amd/csrc
 pids=()
 newest_hdr=$(ls -t $C/*.hpp $C/*.h $R/include/*.h | head -1)
-for f in hjd_entropy hjd_runtime idct_compat stream_pipeline numa_affinity; do
+for f in hjd_entropy hjd_runtime idct_compat stream_pipeline numa_affinity hjd_probe; do
   [ $O/$f.o -nt $C/$f.hip ] && [ $O/$f.o -nt $newest_hdr ] || { /opt/rocm/bin/hipcc --offload-arch=gfx950 $FLAGS $SAN -c $C/$f.hip -o $O/$f.o & pids+=($!); }
 done
 [ $O/jpeg_host.o -nt $C/jpeg_host.cpp ] && [ $O/jpeg_host.o -nt $newest_hdr ] || { /opt/rocm/bin/hipcc -x c++ $FLAGS $SAN -c $C/jpeg_host.cpp -o $O/jpeg_host.o & pids+=($!); }

@@ -36,10 +36,12 @@ def main():
     ap.add_argument("--workload", default="4k420")
     ap.add_argument("--kernel", default="decode_kernel")
     ap.add_argument("--note", default="")
+    ap.add_argument("--box", default="", help="box identity of the profiled run (e.g. GPU serial), recorded for "
+                                              "bench.py's traffic_other_run")
     ap.add_argument("--frames", type=int, default=1024, help="frames per launch of the profiled command (bench.py)")
     args = ap.parse_args()
     out = {"name": args.name, "workload": args.workload, "kernel_match": args.kernel, "note": args.note,
-           "frames_per_launch": args.frames,
+           "frames_per_launch": args.frames, "box": args.box or "not recorded",
            "source_dir": os.path.relpath(args.dir, REPO)}
 
     stats = sorted(glob.glob(os.path.join(args.dir, "**", "*kernel_stats.csv"), recursive=True))
