@@ -171,8 +171,9 @@ int hjd_debug_csc_exhaustive(hjd_ctx* ctx, uint32_t* d_out, int mode, void* stre
  * reads and BGRX stores kept; no IDCT, no colour math), 4 = no stores,
  * 16 = no IDCT, 64 = no colour math, 20 = no IDCT and no stores, 8 = no colour
  * stage, 24 = neither IDCT nor colour stage.  4:2:0 / 4:4:4, int16 zigzag
- * input, BGRX output only. */
-int hjd_debug_plan_launch_stages(hjd_plan* plan, int stages, const void* d_coefs, void* d_out, void* stream);
+ * input, BGRX output only.  grid_blocks as hjd_plan_launch (0 = default). */
+int hjd_debug_plan_launch_stages(hjd_plan* plan, int stages, const void* d_coefs, void* d_out, void* stream,
+                                 int grid_blocks);
 
 /* The box's streaming ceiling for a read:write byte mix (bench.py's
  * frac_of_box_ceiling): units of read_kib KiB read + write_kib KiB written
@@ -180,7 +181,10 @@ int hjd_debug_plan_launch_stages(hjd_plan* plan, int stages, const void* d_coefs
  * launch over min(src_bytes / read_kib KiB, dst_bytes / write_kib KiB) units.
  * flags bit 0: non-temporal loads and stores; bit 1: XCD-contiguous group
  * order (the fused kernel's); bit 2: pipelined (the next unit's loads issued
- * before this unit's stores, as the fused kernel prefetches its next task).  Mixes (KiB): 6:8 (4:2:0 task), 6:4 (4:4:4
+ * before this unit's stores, as the fused kernel prefetches its next task);
+ * bit 3: image-row stores (the fused kernel's store geometry: dst as 3840-px
+ * BGRX rows, pitch 15360 B, each unit one 512-B-wide strip of 2*write_kib
+ * rows, two row segments per wave store instruction).  Mixes (KiB): 6:8 (4:2:0 task), 6:4 (4:4:4
  * task), 0:8, 6:0, 4:4, 3:4.  *units_out = units moved (bytes = units *
  * (read_kib + write_kib) KiB).  dst_bytes >= 1 KiB. */
 int hjd_debug_rw_mix(hjd_ctx* ctx, const void* d_src, void* d_dst, int64_t src_bytes, int64_t dst_bytes,

@@ -76,7 +76,7 @@ SIGNATURES = {
                                      ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]),
     "hjd_debug_csc_exhaustive": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
     "hjd_debug_plan_launch_stages": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
-                                                    ctypes.c_void_p]),
+                                                    ctypes.c_void_p, ctypes.c_int]),
     "hjd_debug_rw_mix": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                         ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                         ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)]),

@@ -234,12 +234,13 @@ class Plan:
         op = self._check_tensor(out, "out", 0, self.out_bytes_needed)
         check(self.lib.hjd_plan_launch(self.handle, cp, op, _stream_ptr(stream), grid_blocks), "hjd_plan_launch")
 
-    def launch_stages(self, stages: int, coefs, out, stream=None):
+    def launch_stages(self, stages: int, coefs, out, stream=None, grid_blocks: int = 0):
         """Timing-only launch with kernel stages skipped (hjd_debug_plan_launch_stages;
         80 memory only, 4 no stores, ...): the output is WRONG by design."""
         cp = self._check_tensor(coefs, "coefs", self.coef_elem_bytes, self.coef_elems_needed * self.coef_elem_bytes)
         op = self._check_tensor(out, "out", 0, self.out_bytes_needed)
-        check(self.lib.hjd_debug_plan_launch_stages(self.handle, int(stages), cp, op, _stream_ptr(stream)),
+        check(self.lib.hjd_debug_plan_launch_stages(self.handle, int(stages), cp, op, _stream_ptr(stream),
+                                                    int(grid_blocks)),
               "hjd_debug_plan_launch_stages")
 
     def close(self):

@@ -194,6 +194,13 @@ constexpr int kOutBgr24 = 32;
 // Gather pairs as ds_read_u16 | ds_read_u16_d16_hi (load_round_pk_d16): only
 // valid where d16 loads zero the other half (sramecc+), chosen at launch.
 constexpr int kVarD16 = 128;
+// Task order (hjd_plan_set_variant bit 2, HJD_ORDER=strided): a resident grid
+// (one generation of groups) whose waves stride through the task list --
+// wave L takes tasks L, L + N, L + 2N, ... (N = waves of the grid, L in the
+// XCD-contiguous order of group_order) -- so the resident waves always work
+// on N consecutive tasks, as with one short chunk per wave, while each wave's
+// setup and its prefetch pipeline span many tasks.
+constexpr int kVarStrided = 256;
 template <int kVariant>
 constexpr int kOutBytes = (kVariant & kOutBgr24) != 0 ? 3 : 4;
 
@@ -869,7 +876,12 @@ __global__ __launch_bounds__(kGroupThreads, KLayout<kSampling>::min_waves) void 
 
     // this wave's task sequence: t_begin, t_begin + t_step, ... (< t_end)
     int64_t t_begin, t_end, t_step;
-    if constexpr ((kVariant & kVarWgInterleave) != 0) {
+    if constexpr ((kVariant & kVarStrided) != 0) {
+        const int64_t nwaves = static_cast<int64_t>(gridDim.x) * kWavesPerGroup;
+        t_begin = static_cast<int64_t>(group_order(blockIdx.x, gridDim.x)) * kWavesPerGroup + wave;
+        t_end = total_tasks;
+        t_step = nwaves;
+    } else if constexpr ((kVariant & kVarWgInterleave) != 0) {
         const int64_t nquads = (total_tasks + kWavesPerGroup - 1) / kWavesPerGroup;
         const int64_t chunk = nquads / gridDim.x, rem = nquads % gridDim.x;
         const int64_t qb = static_cast<int64_t>(blockIdx.x) * chunk + min<int64_t>(blockIdx.x, rem);

@@ -42,18 +42,26 @@ __device__ __forceinline__ uint32_t xcd_order(uint32_t bid, uint32_t ngroups)
 // feeds every store, so no load is dead.  flags bit 2 (pipelined): the next
 // unit's loads are issued before this unit's stores, the fused kernel's
 // one-task-ahead prefetch; otherwise each unit loads, then stores.
+// Stores of unit u.  Contiguous: W KiB at dst + u*W KiB.  Image rows (flags
+// bit 3): the fused kernel's store geometry -- dst is a stack of 3840-px BGRX
+// images (pitch 15360 B = 30 strips of 512 B); unit u is strip u % 30 of row
+// band u / 30 (2W rows), and each wave store instruction writes two 512-B row
+// segments (lanes 0-31 one row, lanes 32-63 the next).
 template <int R, int W>
-__device__ __forceinline__ void rw_store(u32x4* __restrict__ dst, int64_t u, int lane, u32x4 acc, bool nt)
+__device__ __forceinline__ void rw_store(u32x4* __restrict__ dst, int64_t u, int lane, u32x4 acc, bool nt, bool rows)
 {
-    u32x4* d = dst + u * W * 64 + lane;
+    constexpr int64_t kPitch = 15360 / 16, kStrips = 30;   // in 16-B words
+    u32x4* d = rows ? dst + (u / kStrips) * (2 * W) * kPitch + (u % kStrips) * 32 + (lane >> 5) * kPitch + (lane & 31)
+                    : dst + u * W * 64 + lane;
 #pragma unroll
     for (int k = 0; k < W; ++k) {
         u32x4 o = acc;
         o.y += static_cast<unsigned>(k);
+        u32x4* q = rows ? d + 2 * k * kPitch : d + 64 * k;
         if (nt)
-            __builtin_nontemporal_store(o, d + 64 * k);
+            __builtin_nontemporal_store(o, q);
         else
-            d[64 * k] = o;
+            *q = o;
     }
 }
 
@@ -77,6 +85,7 @@ __global__ __launch_bounds__(256) void rw_mix_kernel(const u32x4* __restrict__ s
     const int64_t u0 = gw * upw;
     const int64_t u1 = u0 + upw < units ? u0 + upw : units;
     const bool nt = (flags & 1) != 0;
+    const bool rows = (flags & 8) != 0;
     if constexpr (R > 0 && W > 0) {
         if (flags & 4) {   // pipelined
             u32x4 cur[R], nxt[R];
@@ -86,7 +95,7 @@ __global__ __launch_bounds__(256) void rw_mix_kernel(const u32x4* __restrict__ s
                 u32x4 acc = {static_cast<unsigned>(lane), 0u, 0u, static_cast<unsigned>(u)};
 #pragma unroll
                 for (int k = 0; k < R; ++k) acc ^= cur[k];
-                rw_store<R, W>(dst, u, lane, acc, nt);
+                rw_store<R, W>(dst, u, lane, acc, nt, rows);
 #pragma unroll
                 for (int k = 0; k < R; ++k) cur[k] = nxt[k];
             }
@@ -102,7 +111,7 @@ __global__ __launch_bounds__(256) void rw_mix_kernel(const u32x4* __restrict__ s
             for (int k = 0; k < R; ++k) acc ^= v[k];
         }
         if constexpr (W > 0) {
-            rw_store<R, W>(dst, u, lane, acc, nt);
+            rw_store<R, W>(dst, u, lane, acc, nt, rows);
         } else {
             // read-only mix: keep the loads alive without a store per unit (a
             // data-dependent condition the compiler cannot fold; dst >= 1 KiB)
@@ -200,7 +209,7 @@ extern "C" {
 int hjd_debug_rw_mix(hjd_ctx* ctx, const void* d_src, void* d_dst, int64_t src_bytes, int64_t dst_bytes,
                      int read_kib, int write_kib, int units_per_wave, int flags, void* stream, int64_t* units_out)
 {
-    if (!ctx || units_per_wave <= 0 || (flags & ~7)) return hjd_internal::set_error(HJD_E_INVALID, "invalid arguments");
+    if (!ctx || units_per_wave <= 0 || (flags & ~15)) return hjd_internal::set_error(HJD_E_INVALID, "invalid arguments");
     using K = void (*)(const u32x4*, u32x4*, int64_t, int, int);
     K k = nullptr;
     if (read_kib == 6 && write_kib == 8) k = rw_mix_kernel<6, 8>;
@@ -215,6 +224,10 @@ int hjd_debug_rw_mix(hjd_ctx* ctx, const void* d_src, void* d_dst, int64_t src_b
     int64_t units = INT64_MAX;
     if (read_kib > 0) units = std::min<int64_t>(units, src_bytes / (1024 * read_kib));
     if (write_kib > 0) units = std::min<int64_t>(units, dst_bytes / (1024 * write_kib));
+    if (flags & 8) {   // image rows: whole bands of 30 strips
+        if (write_kib == 0) return hjd_internal::set_error(HJD_E_INVALID, "image-row stores need a write mix");
+        units = units / 30 * 30;
+    }
     if (units <= 0 || !d_dst || dst_bytes < 1024 || (read_kib > 0 && !d_src)) return hjd_internal::set_error(HJD_E_INVALID, "buffers too small");
     if ((reinterpret_cast<uintptr_t>(d_src) | reinterpret_cast<uintptr_t>(d_dst)) & 15)
         return hjd_internal::set_error(HJD_E_INVALID, "buffers must be 16-byte aligned");

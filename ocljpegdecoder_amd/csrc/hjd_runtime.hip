@@ -120,6 +120,21 @@ static bool device_d16_gather(int device) { return hjd_internal::d16_gather_sele
 static int geometry(int width, int height, int sampling, int& mcu_w, int& mcu_h, int& bpm, int& tasks_mcus);
 static int decode_grid(int sampling, int fmt, int64_t tasks);
 
+// Plan variant bit 2 (hjd_plan_set_variant; HJD_ORDER=strided sets it on
+// every plan): the strided task order (hjd::kVarStrided).
+constexpr int kPlanVarStrided = 4;
+// launch_decode variant bits 8 and up: a stage-skipping measurement variant
+// (hjd_debug_plan_launch_stages), stages << kStageShift | plan variant bits.
+constexpr int kStageShift = 8;
+// One resident generation of the fused kernel's groups: 4 per CU (LDS: four
+// 40-KiB groups fill the 160 KiB; VGPRs allow 4 waves per SIMD), but no more
+// groups than the tasks fill.
+static int resident_groups(int num_cu, int64_t tasks)
+{
+    const int64_t need = (tasks + hjd::kWavesPerGroup - 1) / hjd::kWavesPerGroup;
+    return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(static_cast<int64_t>(num_cu) * 4, need)));
+}
+
 int hjd_internal::ctx_num_cu(const hjd_ctx* ctx) { return ctx->num_cu; }
 
 int64_t hjd_internal::make_frame_record(int width, int height, int sampling, int64_t coef_base, int64_t out_base,
@@ -153,16 +168,15 @@ int hjd_internal::launch_decode(int device, int num_cu, int sampling, int input_
 {
     HJD_HIP(hipSetDevice(device));
     const int fmt = input_format == HJD_IN_Q16_ZIGZAG ? 0 : 1;
-    (void)num_cu;
     SamplingGeom sg;
     if (!sampling_geom(sampling, &sg)) return set_error(HJD_E_INVALID, "unsupported sampling %d", sampling);
-    const int grid = grid_blocks > 0 ? grid_blocks : decode_grid(sampling, fmt, tasks);
+    int grid = grid_blocks > 0 ? grid_blocks : decode_grid(sampling, fmt, tasks);
     if (out_format != HJD_OUT_BGRX && out_format != HJD_OUT_BGR24)
         return set_error(HJD_E_INVALID, "unknown output format %d", out_format);
     using K = void (*)(const void*, const int*, const FrameDev*, int, int64_t, uint8_t*);
     const bool latency = kernel_mode == HJD_KERNEL_LATENCY ||
                          (kernel_mode == HJD_KERNEL_AUTO && grid_blocks == 0 && tasks <= latency_max_tasks());
-    if (latency && (variant & ~3) == 0) {   // [output format][sampling index][input format]
+    if (latency && (variant >> kStageShift) == 0) {   // [output format][sampling index][input format]
 #define HJD_KL(V) hjd::decode_kernel_lat<0, 0, V>, hjd::decode_kernel_lat<0, 1, V>, \
                   hjd::decode_kernel_lat<1, 0, V>, hjd::decode_kernel_lat<1, 1, V>, \
                   hjd::decode_kernel_lat<2, 0, V>, hjd::decode_kernel_lat<2, 1, V>, \
@@ -187,7 +201,7 @@ int hjd_internal::launch_decode(int device, int num_cu, int sampling, int input_
             hjd::decode_kernel<3, 0, hjd::kOutBgr24>, hjd::decode_kernel<3, 1, hjd::kOutBgr24>,
             hjd::decode_kernel<4, 0, hjd::kOutBgr24>, hjd::decode_kernel<4, 1, hjd::kOutBgr24>,
             hjd::decode_kernel<5, 0, hjd::kOutBgr24>, hjd::decode_kernel<5, 1, hjd::kOutBgr24>};
-        if (variant != 0) return set_error(HJD_E_INVALID, "kernel variants are BGRX-only");
+        if ((variant & 3) != 0) return set_error(HJD_E_INVALID, "kernel variants are BGRX-only");
         K k24 = kTable24[(sg.index << 1) | fmt];
         if (sampling == HJD_YUV444 && fmt == 0 && device_d16_gather(device))
             k24 = hjd::decode_kernel<0, 0, hjd::kOutBgr24 | hjd::kVarD16>;
@@ -197,23 +211,27 @@ int hjd_internal::launch_decode(int device, int num_cu, int sampling, int input_
         HJD_HIP(hipGetLastError());
         return HJD_OK;
     }
-    if (fmt == 0 && variant > 3) {   // stage-skipping measurement variants (hjd_debug_plan_launch_stages)
+    if (fmt == 0 && (variant >> kStageShift) != 0) {   // stage-skipping measurement variants
         if (sg.index > 1) return hjd_internal::set_error(HJD_E_INVALID, "ablation variants are 4:4:4/4:2:0 only");
-        K k = nullptr;
-        const bool s420 = sampling == HJD_YUV420;
-        const bool d16 = !s420 && device_d16_gather(device);   // as the product 4:4:4 kernel gathers
-        switch (variant) {
-        case 4: k = s420 ? hjd::decode_kernel<1, 0, 4> : d16 ? hjd::decode_kernel<0, 0, 4 | hjd::kVarD16>
-                                                             : hjd::decode_kernel<0, 0, 4>; break;
-        case 8: k = s420 ? hjd::decode_kernel<1, 0, 8> : hjd::decode_kernel<0, 0, 8>; break;
-        case 16: k = s420 ? hjd::decode_kernel<1, 0, 16> : hjd::decode_kernel<0, 0, 16>; break;
-        case 20: k = s420 ? hjd::decode_kernel<1, 0, 20> : hjd::decode_kernel<0, 0, 20>; break;
-        case 24: k = s420 ? hjd::decode_kernel<1, 0, 24> : hjd::decode_kernel<0, 0, 24>; break;
-        case 64: k = s420 ? hjd::decode_kernel<1, 0, 64> : d16 ? hjd::decode_kernel<0, 0, 64 | hjd::kVarD16>
-                                                               : hjd::decode_kernel<0, 0, 64>; break;
-        case 80: k = s420 ? hjd::decode_kernel<1, 0, 80> : hjd::decode_kernel<0, 0, 80>; break;
-        default: return hjd_internal::set_error(HJD_E_INVALID, "unknown ablation variant %d", variant);
-        }
+        constexpr int kStages[7] = {4, 8, 16, 20, 24, 64, 80};
+        const int stages = variant >> kStageShift;
+        int si = -1;
+        for (int i = 0; i < 7; ++i)
+            if (kStages[i] == stages) si = i;
+        if (si < 0) return hjd_internal::set_error(HJD_E_INVALID, "unknown ablation variant %d", stages);
+#define HJD_ST(S, B) {hjd::decode_kernel<S, 0, 4 | (B)>, hjd::decode_kernel<S, 0, 8 | (B)>,                  \
+                      hjd::decode_kernel<S, 0, 16 | (B)>, hjd::decode_kernel<S, 0, 20 | (B)>,                \
+                      hjd::decode_kernel<S, 0, 24 | (B)>, hjd::decode_kernel<S, 0, 64 | (B)>,                \
+                      hjd::decode_kernel<S, 0, 80 | (B)>}
+        // [strided][4:2:0, 4:4:4, 4:4:4 d16 gather][stages]
+        static const K kStageK[2][3][7] = {
+            {HJD_ST(1, 0), HJD_ST(0, 0), HJD_ST(0, hjd::kVarD16)},
+            {HJD_ST(1, hjd::kVarStrided), HJD_ST(0, hjd::kVarStrided), HJD_ST(0, hjd::kVarStrided | hjd::kVarD16)}};
+#undef HJD_ST
+        const bool strided = (variant & kPlanVarStrided) != 0;
+        const int col = sampling == HJD_YUV420 ? 0 : device_d16_gather(device) ? 2 : 1;   // as the product gathers
+        const K k = kStageK[strided][col][si];
+        if (strided && grid_blocks <= 0) grid = resident_groups(num_cu, tasks);
         hipLaunchKernelGGL(k, dim3(grid), dim3(hjd::kGroupThreads), 0, static_cast<hipStream_t>(stream), d_coefs,
                            d_qt_nat, reinterpret_cast<const FrameDev*>(d_frames), nframes, tasks,
                            static_cast<uint8_t*>(d_out));
@@ -231,6 +249,13 @@ int hjd_internal::launch_decode(int device, int num_cu, int sampling, int input_
     K k = kTable[key];
     if (sampling == HJD_YUV444 && fmt == 0 && (variant & 3) == 0 && device_d16_gather(device))
         k = hjd::decode_kernel<0, 0, hjd::kVarD16>;
+    if ((variant & kPlanVarStrided) && fmt == 0 && (sampling == HJD_YUV420 || sampling == HJD_YUV444)) {
+        // strided task order over one resident generation of groups
+        k = sampling == HJD_YUV420 ? hjd::decode_kernel<1, 0, hjd::kVarStrided>
+          : device_d16_gather(device) ? hjd::decode_kernel<0, 0, hjd::kVarStrided | hjd::kVarD16>
+                                      : hjd::decode_kernel<0, 0, hjd::kVarStrided>;
+        if (grid_blocks <= 0) grid = resident_groups(num_cu, tasks);
+    }
     hipLaunchKernelGGL(k, dim3(grid), dim3(hjd::kGroupThreads), 0, static_cast<hipStream_t>(stream),
                        d_coefs, d_qt_nat, reinterpret_cast<const FrameDev*>(d_frames), nframes, tasks,
                        static_cast<uint8_t*>(d_out));
@@ -368,6 +393,10 @@ int hjd_plan_create(hjd_ctx* ctx, const hjd_frame* frames, int nframes, int inpu
     p->sampling = sampling;
     p->out_format = out_format;
     p->nframes = nframes;
+    {
+        const char* e = getenv("HJD_ORDER");   // A/B: the strided task order on every plan
+        if (e && !strcmp(e, "strided")) p->variant |= kPlanVarStrided;
+    }
     p->tasks = tasks;
     p->pixels = pixels;
     p->coef_bytes = blocks * (input_format == HJD_IN_Q16_ZIGZAG ? 128 : 256);
@@ -410,7 +439,7 @@ int hjd_plan_set_variant(hjd_plan* plan, int variant)
 #ifdef HJD_ABLATION
     if (variant < 0 || variant > 127) return fail(HJD_E_INVALID, "unknown kernel variant %d", variant);
 #else
-    if (variant < 0 || variant > 3) return fail(HJD_E_INVALID, "unknown kernel variant %d", variant);
+    if (variant < 0 || variant > 7) return fail(HJD_E_INVALID, "unknown kernel variant %d", variant);
 #endif
     plan->variant = variant;
     return HJD_OK;
@@ -485,7 +514,8 @@ int hjd_plan_launch(hjd_plan* plan, const void* d_coefs, void* d_out, void* stre
                                        plan->kernel_mode);
 }
 
-int hjd_debug_plan_launch_stages(hjd_plan* plan, int stages, const void* d_coefs, void* d_out, void* stream)
+int hjd_debug_plan_launch_stages(hjd_plan* plan, int stages, const void* d_coefs, void* d_out, void* stream,
+                                 int grid_blocks)
 {
     if (!plan) return fail(HJD_E_INVALID, "plan is NULL");
     if (stages != 4 && stages != 16 && stages != 20 && stages != 64 && stages != 80 && stages != 8 && stages != 24)
@@ -496,11 +526,11 @@ int hjd_debug_plan_launch_stages(hjd_plan* plan, int stages, const void* d_coefs
     if (plan->tasks == 0) return HJD_OK;
     if (!d_coefs || !d_out || ((reinterpret_cast<uintptr_t>(d_coefs) | reinterpret_cast<uintptr_t>(d_out)) & 15))
         return fail(HJD_E_INVALID, "NULL or unaligned device buffer");
-    return hjd_internal::launch_decode(plan->ctx->device, plan->ctx->num_cu, plan->sampling, plan->input_format, stages,
-                                       d_coefs, plan->d_qt,
+    return hjd_internal::launch_decode(plan->ctx->device, plan->ctx->num_cu, plan->sampling, plan->input_format,
+                                       (stages << kStageShift) | (plan->variant & kPlanVarStrided), d_coefs, plan->d_qt,
                                        reinterpret_cast<const hjd_internal::FrameRecord*>(plan->d_frames),
-                                       plan->nframes, plan->tasks, d_out, stream, 0, plan->out_format,
-                                       HJD_KERNEL_PERSISTENT);
+                                       plan->nframes, plan->tasks, d_out, stream, grid_blocks < 0 ? 0 : grid_blocks,
+                                       plan->out_format, HJD_KERNEL_PERSISTENT);
 }
 
 int hjd_idct_blocks(hjd_ctx* ctx, const int32_t* d_in, int32_t* d_out, int64_t nblocks, void* stream)

@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--grids", default="0")
     ap.add_argument("--kernels", default="1", help="hjd_kernel_mode list: 1 persistent, 2 latency")
     ap.add_argument("--no-check", action="store_true", help="ablation variants: outputs differ by design")
+    ap.add_argument("--stages", default="0", help="stage variants (hjd_debug_plan_launch_stages): 0 = the product, "
+                                                  "80 memory only, 4 no stores, ... (outputs wrong by design)")
     args = ap.parse_args()
 
     import torch
@@ -55,28 +57,35 @@ def main():
     grids = [int(g) for g in args.grids.split(",")]
     kernels = [int(k) for k in args.kernels.split(",")]
     stream = torch.cuda.current_stream()
-    times = {(k, v, g): [] for k in kernels for v in variants for g in grids}
+    stages = [int(x) for x in args.stages.split(",")]
+    times = {(k, v, g, st): [] for k in kernels for v in variants for g in grids for st in stages}
     ref = None
     for rnd in range(args.rounds):
-        for k, v, g in times:
+        for k, v, g, st in times:
             plan.set_kernel(k)
             plan.set_variant(v)
-            plan.launch(coefs, out, stream, grid_blocks=g)   # warm
+
+            def go():
+                if st:
+                    plan.launch_stages(st, coefs, out, stream, grid_blocks=g)
+                else:
+                    plan.launch(coefs, out, stream, grid_blocks=g)
+            go()   # warm
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
             for _ in range(args.reps):
-                plan.launch(coefs, out, stream, grid_blocks=g)
+                go()
             e1.record(stream)
             torch.cuda.synchronize()
-            times[(k, v, g)].append(e0.elapsed_time(e1) / args.reps)
-            if rnd == 0 and not args.no_check:
+            times[(k, v, g, st)].append(e0.elapsed_time(e1) / args.reps)
+            if rnd == 0 and not args.no_check and not st:
                 sig = int(out[:, ::97, ::89].sum().item())
                 ref = sig if ref is None else ref
                 assert sig == ref, f"kernel {k} variant {v} grid {g} output differs"
     res = {"workload": args.workload, "frames": nf, "bytes_per_launch": nbytes, "signature": ref, "results": []}
-    for (k, v, g), ts in times.items():
+    for (k, v, g, st), ts in times.items():
         med = statistics.median(ts)
-        res["results"].append({"kernel": k, "variant": v, "grid": g, "median_ms": round(med, 4),
+        res["results"].append({"kernel": k, "variant": v, "grid": g, "stages": st, "median_ms": round(med, 4),
                                "min_ms": round(min(ts), 4),
                                "GBps_median": round(nbytes / med / 1e6, 1),
                                "GBps_best": round(nbytes / min(ts) / 1e6, 1)})
