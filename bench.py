@@ -954,17 +954,23 @@ def box_ceiling(torch, ctx, src, dst, stream, mix, memory_only=None, reps=5):
 
 def box_identity(torch):
     """Which GPU this line was measured on (the container hostname is not
-    unique): the device's unique id and serial from rocm-smi, when readable."""
-    import subprocess
+    unique): the amdgpu unique id and product serial from sysfs.  No
+    subprocess (rocm-smi is a Python script started through /usr/bin/env; run
+    from a process that has initialised the GPU -- under rocprofv3 every
+    process has -- that exec is refused on the GPU box)."""
     ident = {"hostname": socket.gethostname(), "device": torch.cuda.get_device_name(0)}
-    try:
-        r = subprocess.run(["rocm-smi", "--showserial", "--showuniqueid", "--json"], capture_output=True, text=True,
-                           timeout=20)
-        card = next(iter(json.loads(r.stdout).values()))
-        ident["unique_id"] = card.get("Unique ID")
-        ident["serial"] = card.get("Serial Number")
-    except Exception:
-        pass
+    for card in sorted(glob.glob("/sys/class/drm/card*/device")):
+        try:
+            if open(os.path.join(card, "vendor")).read().strip() != "0x1002":
+                continue
+            for key, f in (("unique_id", "unique_id"), ("serial", "serial_number")):
+                pth = os.path.join(card, f)
+                if os.path.exists(pth):
+                    ident[key] = open(pth).read().strip()
+            if "unique_id" in ident or "serial" in ident:
+                break
+        except OSError:
+            continue
     return ident
 
 
@@ -1071,6 +1077,16 @@ def pixel_batch(args, wl, hjd, torch, dist, world, rank, dev, qt, steps, warmup,
     torch.cuda.synchronize()
 
     stream = torch.cuda.current_stream()
+    # adapt the launch shape to this device (hjd_plan_autotune: tasks per wave x
+    # store policy, timed on these buffers; untimed setup, identical pixels)
+    launch = {"autotuned": False, "tasks_per_wave": None, "variant": 0}
+    if not args.no_autotune and not args.grid:
+        t0 = time.perf_counter()
+        tpw, var = plan.autotune(coefs, out, stream)
+        launch = {"autotuned": tpw > 0, "tasks_per_wave": tpw or None, "variant": var,
+                  "stores": "plain" if var & 1 else "nt", "seconds": round(time.perf_counter() - t0, 2),
+                  "how": "hjd_plan_autotune: 1/2/4/8/16 tasks per wave x nt/plain stores, 2 interleaved rounds of "
+                         "one warm + two timed launches each on this run's buffers; fastest kept"}
     for _ in range(warmup):
         plan.launch(coefs, out, stream, grid_blocks=args.grid)
     torch.cuda.synchronize()
@@ -1126,7 +1142,7 @@ def pixel_batch(args, wl, hjd, torch, dist, world, rank, dev, qt, steps, warmup,
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
     return {"value": round(value, 1), "output_check": checked, "device_copy_GBps": copy_gbps,
-            "stages": stages, "box": box, "clock": clock,
+            "stages": stages, "box": box, "clock": clock, "launch": launch,
             "_pool_host": pool_host, "_wall_max": wall_max, "_kernel_ms": kernel_ms, "_achieved": achieved,
             "_bytes_per_launch": bytes_per_launch, "_tasks": tasks}
 
@@ -1140,6 +1156,8 @@ def main():
     ap.add_argument("--frames", type=int, default=0, help="override batch size")
     ap.add_argument("--grid", type=int, default=0, help="persistent grid (workgroups), 0 = default")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-autotune", action="store_true",
+                    help="pixel batches: keep the shape-default launch instead of hjd_plan_autotune's choice")
     ap.add_argument("--no-stages", action="store_true",
                     help="skip the same-run stage ablation and box-ceiling measurements of the pixel batches")
     ap.add_argument("--no-fhd", action="store_true",
@@ -1223,7 +1241,7 @@ def main():
             "workload": wl4["desc"], "frames_per_gpu": wl4["frames"], "sampling": "4:4:4",
             "output_checked_vs_oracle": r4["output_check"]["ok"], "output_check": r4["output_check"],
             "roofline": roofline_obj(r4["_achieved"], r4["_bytes_per_launch"], r4["_kernel_ms"], traffic4, r4["box"]),
-            "stages": r4["stages"], "box_ceiling": r4["box"], "clock_under_load": r4["clock"],
+            "stages": r4["stages"], "box_ceiling": r4["box"], "clock_under_load": r4["clock"], "launch": r4["launch"],
             "reference_path": "src/idct8x8.cl:168-192 (batch_idct_csc_444), src/decoder.cpp:457-471"}
         checked_all_ok = checked["ok"] and r4["output_check"]["ok"]
     else:
@@ -1275,6 +1293,7 @@ def main():
             "output_check": checked,
             "roofline": roofline_obj(achieved, bytes_per_launch, kernel_ms, traffic, res_px["box"]),
             "stages": res_px["stages"], "box_ceiling": res_px["box"], "clock_under_load": res_px["clock"],
+            "launch": res_px["launch"],
             "box": box_identity(torch),
             "cpu_baseline": cpu,
             "device_copy_GBps": res_px["device_copy_GBps"],

@@ -129,6 +129,10 @@ int hjd_plan_destroy(hjd_plan* plan);
  * Results are identical for every variant. */
 int hjd_plan_set_variant(hjd_plan* plan, int variant);
 int hjd_plan_set_kernel(hjd_plan* plan, int mode);   /* hjd_kernel_mode */
+/* Pin the persistent kernel's task chunk without hjd_plan_autotune: `tasks`
+ * consecutive tasks per wave (1..4096; 0 restores the shape default).
+ * Identical pixels either way. */
+int hjd_plan_set_chunk(hjd_plan* plan, int tasks);
 int64_t hjd_plan_tasks(const hjd_plan* plan);      /* work items (strips) */
 int64_t hjd_plan_pixels(const hjd_plan* plan);     /* visible pixels */
 int64_t hjd_plan_coef_bytes(const hjd_plan* plan); /* algorithmic input bytes */
@@ -144,6 +148,20 @@ int64_t hjd_plan_coef_bytes(const hjd_plan* plan); /* algorithmic input bytes */
  * src/idct8x8.cl:136-155, is not reproduced).
  */
 int hjd_plan_launch(hjd_plan* plan, const void* d_coefs, void* d_out, void* stream, int grid_blocks);
+
+/*
+ * Adapt the plan's launch to this device (synchronous, setup time): times
+ * every candidate launch shape -- chunks of 1, 2, 4, 8 or 16 tasks per wave,
+ * each with nt or plain output stores (BGRX) -- with the plan's own buffers,
+ * `rounds`
+ * interleaved rounds (0 = 2) of one warm and two timed launches each, and
+ * keeps the fastest for the plan's later launches with grid_blocks = 0.
+ * Every candidate writes identical pixels (d_out holds a valid decode on
+ * return).  Plans the latency kernel serves are left unchanged.  Optional
+ * outputs: the chosen tasks per wave (0 = unchanged) and the variant bits.
+ */
+int hjd_plan_autotune(hjd_plan* plan, const void* d_coefs, void* d_out, void* stream, int rounds,
+                      int32_t* tasks_per_wave, int32_t* variant);
 
 /* IDCT only (the reference's batch_idct, src/idct8x8.cl:157-166), out of
  * place: int32 natural-order dequantised blocks -> int32 samples [-256,255]. */
@@ -171,7 +189,8 @@ int hjd_debug_csc_exhaustive(hjd_ctx* ctx, uint32_t* d_out, int mode, void* stre
  * reads and BGRX stores kept; no IDCT, no colour math), 4 = no stores,
  * 16 = no IDCT, 64 = no colour math, 20 = no IDCT and no stores, 8 = no colour
  * stage, 24 = neither IDCT nor colour stage.  4:2:0 / 4:4:4, int16 zigzag
- * input, BGRX output only.  grid_blocks as hjd_plan_launch (0 = default). */
+ * input, BGRX output only.  grid_blocks as hjd_plan_launch (0 = the plan's launch shape,
+ * hjd_plan_autotune's if it ran). */
 int hjd_debug_plan_launch_stages(hjd_plan* plan, int stages, const void* d_coefs, void* d_out, void* stream,
                                  int grid_blocks);
 

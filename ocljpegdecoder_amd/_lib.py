@@ -65,11 +65,14 @@ SIGNATURES = {
     "hjd_plan_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "hjd_plan_set_variant": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "hjd_plan_set_kernel": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "hjd_plan_set_chunk": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "hjd_plan_tasks": (ctypes.c_int64, [ctypes.c_void_p]),
     "hjd_plan_pixels": (ctypes.c_int64, [ctypes.c_void_p]),
     "hjd_plan_coef_bytes": (ctypes.c_int64, [ctypes.c_void_p]),
     "hjd_plan_launch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                        ctypes.c_int]),
+    "hjd_plan_autotune": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_int, c_i32p, c_i32p]),
     "hjd_idct_blocks": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                        ctypes.c_void_p]),
     "hjd_debug_csc": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
@@ -113,7 +116,11 @@ def load():
         pass
     lib = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
-        fn = getattr(lib, name)
+        # a tuning build named by HJD_LIB (e.g. an older tree for an A/B) may
+        # lack newer entry points; the product library must export them all
+        fn = getattr(lib, name, None) if os.environ.get("HJD_LIB") else getattr(lib, name)
+        if fn is None:
+            continue
         fn.restype = res
         fn.argtypes = args
     _bind_host(lib)

@@ -224,6 +224,10 @@ class Plan:
         """KERNEL_AUTO (default), KERNEL_PERSISTENT or KERNEL_LATENCY; identical outputs."""
         check(self.lib.hjd_plan_set_kernel(self.handle, int(mode)), "hjd_plan_set_kernel")
 
+    def set_chunk(self, tasks: int):
+        """Pin the persistent kernel's tasks per wave (hjd_plan_set_chunk); 0 = default."""
+        check(self.lib.hjd_plan_set_chunk(self.handle, int(tasks)), "hjd_plan_set_chunk")
+
     def set_variant(self, variant: int):
         """Kernel variant bits (tuning/A-B only; outputs are identical)."""
         check(self.lib.hjd_plan_set_variant(self.handle, int(variant)), "hjd_plan_set_variant")
@@ -233,6 +237,16 @@ class Plan:
         cp = self._check_tensor(coefs, "coefs", self.coef_elem_bytes, self.coef_elems_needed * self.coef_elem_bytes)
         op = self._check_tensor(out, "out", 0, self.out_bytes_needed)
         check(self.lib.hjd_plan_launch(self.handle, cp, op, _stream_ptr(stream), grid_blocks), "hjd_plan_launch")
+
+    def autotune(self, coefs, out, stream=None, rounds: int = 2):
+        """hjd_plan_autotune: time the launch shapes on these buffers and keep
+        the fastest for later launches; returns (tasks_per_wave, variant)."""
+        cp = self._check_tensor(coefs, "coefs", self.coef_elem_bytes, self.coef_elems_needed * self.coef_elem_bytes)
+        op = self._check_tensor(out, "out", 0, self.out_bytes_needed)
+        tpw, var = ctypes.c_int32(0), ctypes.c_int32(0)
+        check(self.lib.hjd_plan_autotune(self.handle, cp, op, _stream_ptr(stream), int(rounds), ctypes.byref(tpw),
+                                         ctypes.byref(var)), "hjd_plan_autotune")
+        return tpw.value, var.value
 
     def launch_stages(self, stages: int, coefs, out, stream=None, grid_blocks: int = 0):
         """Timing-only launch with kernel stages skipped (hjd_debug_plan_launch_stages;

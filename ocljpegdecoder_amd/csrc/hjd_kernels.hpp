@@ -194,13 +194,6 @@ constexpr int kOutBgr24 = 32;
 // Gather pairs as ds_read_u16 | ds_read_u16_d16_hi (load_round_pk_d16): only
 // valid where d16 loads zero the other half (sramecc+), chosen at launch.
 constexpr int kVarD16 = 128;
-// Task order (hjd_plan_set_variant bit 2, HJD_ORDER=strided): a resident grid
-// (one generation of groups) whose waves stride through the task list --
-// wave L takes tasks L, L + N, L + 2N, ... (N = waves of the grid, L in the
-// XCD-contiguous order of group_order) -- so the resident waves always work
-// on N consecutive tasks, as with one short chunk per wave, while each wave's
-// setup and its prefetch pipeline span many tasks.
-constexpr int kVarStrided = 256;
 template <int kVariant>
 constexpr int kOutBytes = (kVariant & kOutBgr24) != 0 ? 3 : 4;
 
@@ -861,7 +854,8 @@ template <int kSampling, int kFmt, int kVariant>
 __global__ __launch_bounds__(kGroupThreads, KLayout<kSampling>::min_waves) void decode_kernel(const void* __restrict__ coefs,
                                                               const int* __restrict__ qt_pool,
                                                               const FrameDev* __restrict__ frames, int nframes,
-                                                              int64_t total_tasks, uint8_t* __restrict__ out)
+                                                              int64_t total_tasks, uint8_t* __restrict__ out,
+                                                              int64_t chunk, int64_t rem)
 {
     using L = KLayout<kSampling>;
     __shared__ __attribute__((aligned(16))) char lds[kWavesPerGroup * L::wave_lds];
@@ -875,24 +869,19 @@ __global__ __launch_bounds__(kGroupThreads, KLayout<kSampling>::min_waves) void 
     const int r = lane & 7;
 
     // this wave's task sequence: t_begin, t_begin + t_step, ... (< t_end)
+    // chunk / rem: the split of the task list over the grid, computed on the
+    // host (launch_decode) so no wave spends a 64-bit division on it:
+    // default order, total_tasks = chunk * (grid * 4 waves) + rem;
+    // wg-interleave, ceil(total_tasks / 4) quads = chunk * grid + rem.
     int64_t t_begin, t_end, t_step;
-    if constexpr ((kVariant & kVarStrided) != 0) {
-        const int64_t nwaves = static_cast<int64_t>(gridDim.x) * kWavesPerGroup;
-        t_begin = static_cast<int64_t>(group_order(blockIdx.x, gridDim.x)) * kWavesPerGroup + wave;
-        t_end = total_tasks;
-        t_step = nwaves;
-    } else if constexpr ((kVariant & kVarWgInterleave) != 0) {
-        const int64_t nquads = (total_tasks + kWavesPerGroup - 1) / kWavesPerGroup;
-        const int64_t chunk = nquads / gridDim.x, rem = nquads % gridDim.x;
+    if constexpr ((kVariant & kVarWgInterleave) != 0) {
         const int64_t qb = static_cast<int64_t>(blockIdx.x) * chunk + min<int64_t>(blockIdx.x, rem);
         const int64_t qe = qb + chunk + (blockIdx.x < rem ? 1 : 0);
         t_begin = qb * kWavesPerGroup + wave;
         t_end = min<int64_t>(qe * kWavesPerGroup, total_tasks);
         t_step = kWavesPerGroup;
     } else {
-        const int64_t nwaves = static_cast<int64_t>(gridDim.x) * kWavesPerGroup;
         const int64_t gw = static_cast<int64_t>(group_order(blockIdx.x, gridDim.x)) * kWavesPerGroup + wave;
-        const int64_t chunk = total_tasks / nwaves, rem = total_tasks % nwaves;
         t_begin = gw * chunk + min(gw, rem);
         t_end = t_begin + chunk + (gw < rem ? 1 : 0);
         t_step = 1;
@@ -937,10 +926,18 @@ __global__ __launch_bounds__(kGroupThreads, KLayout<kSampling>::min_waves) void 
     };
     if constexpr (kFmt == 0) {
         prefetch(task_geom<kSampling>(pc, t_begin));
+        // the first task's table rows load beside its coefficients, so a wave
+        // start waits for one memory round trip, not two
+        if constexpr (!L::t2) {
+            q_tables[0] = pc.qt0; q_tables[1] = pc.qt1; q_tables[2] = pc.qt2;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) load_qrow_pk(qt_pool, q_tables[c], r, q[c]);
+        }
         __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0): see the edge-strip drain below
     }
 
-    for (int64_t task = t_begin; task < t_end; task += t_step) {
+    for (int64_t task = t_begin, next_task; task >= 0; task = next_task) {
+        next_task = task + t_step < t_end ? task + t_step : -1;   // -1: this is the wave's last task
         const FrameCursor cc = pc;
         const TaskGeom tg = task_geom<kSampling>(cc, task);
         if constexpr (kFmt == 0) {
@@ -966,13 +963,13 @@ __global__ __launch_bounds__(kGroupThreads, KLayout<kSampling>::min_waves) void 
                 *reinterpret_cast<int4*>(slots + (j >> 3) * kSlotBytes + (j & 7) * 16) = pre[k];
             }
             wave_lds_sync();
-            if (HJD_PREFETCH_AT < 0 && task + t_step < t_end) {
-                while (task + t_step >= pc.end) cursor_load(pc, frames, nframes, total_tasks, pc.idx + 1);
-                prefetch(task_geom<kSampling>(pc, task + t_step));
+            if (HJD_PREFETCH_AT < 0 && next_task >= 0) {
+                while (next_task >= pc.end) cursor_load(pc, frames, nframes, total_tasks, pc.idx + 1);
+                prefetch(task_geom<kSampling>(pc, next_task));
             }
         } else {
-            if (task + t_step < t_end)
-                while (task + t_step >= pc.end) cursor_load(pc, frames, nframes, total_tasks, pc.idx + 1);
+            if (next_task >= 0)
+                while (next_task >= pc.end) cursor_load(pc, frames, nframes, total_tasks, pc.idx + 1);
         }
 
         // HJD_PREFETCH_AT >= 0 (tuning): the next task's loads are issued after
@@ -984,9 +981,9 @@ __global__ __launch_bounds__(kGroupThreads, KLayout<kSampling>::min_waves) void 
         constexpr bool kSplit = HJD_SPLIT444 != 0 && kSampling == 0 && (kVariant & (kAblNoColour | kAblNoIdct)) == 0;
         auto late_prefetch = [&](int i) {
             if constexpr (kFmt == 0 && HJD_PREFETCH_AT >= 0) {
-                if (i == HJD_PREFETCH_AT && task + t_step < t_end) {
-                    while (task + t_step >= pc.end) cursor_load(pc, frames, nframes, total_tasks, pc.idx + 1);
-                    prefetch(task_geom<kSampling>(pc, task + t_step));
+                if (i == HJD_PREFETCH_AT && next_task >= 0) {
+                    while (next_task >= pc.end) cursor_load(pc, frames, nframes, total_tasks, pc.idx + 1);
+                    prefetch(task_geom<kSampling>(pc, next_task));
                 }
             }
             if constexpr (kSplit) {

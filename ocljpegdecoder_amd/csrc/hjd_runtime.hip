@@ -85,6 +85,8 @@ struct hjd_plan {
     int variant = 0;            // kernel variant bits (hjd_plan_set_variant)
     int out_format = HJD_OUT_BGRX;   // common output format of all frames
     int kernel_mode = HJD_KERNEL_AUTO;
+    int tuned_grid = 0;         // hjd_plan_autotune's grid (0: the shape default)
+    int tuned_per_wave = 0;     // its tasks per wave
 };
 
 constexpr int64_t kDefaultLatencyMaxTasks = 1024;   // measured: profiles/r01_latency_kernel.json
@@ -119,21 +121,11 @@ static bool device_d16_gather(int device) { return hjd_internal::d16_gather_sele
 
 static int geometry(int width, int height, int sampling, int& mcu_w, int& mcu_h, int& bpm, int& tasks_mcus);
 static int decode_grid(int sampling, int fmt, int64_t tasks);
+static int grid_for_chunk(int64_t tasks, int64_t per_wave);
 
-// Plan variant bit 2 (hjd_plan_set_variant; HJD_ORDER=strided sets it on
-// every plan): the strided task order (hjd::kVarStrided).
-constexpr int kPlanVarStrided = 4;
 // launch_decode variant bits 8 and up: a stage-skipping measurement variant
 // (hjd_debug_plan_launch_stages), stages << kStageShift | plan variant bits.
 constexpr int kStageShift = 8;
-// One resident generation of the fused kernel's groups: 4 per CU (LDS: four
-// 40-KiB groups fill the 160 KiB; VGPRs allow 4 waves per SIMD), but no more
-// groups than the tasks fill.
-static int resident_groups(int num_cu, int64_t tasks)
-{
-    const int64_t need = (tasks + hjd::kWavesPerGroup - 1) / hjd::kWavesPerGroup;
-    return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(static_cast<int64_t>(num_cu) * 4, need)));
-}
 
 int hjd_internal::ctx_num_cu(const hjd_ctx* ctx) { return ctx->num_cu; }
 
@@ -168,14 +160,21 @@ int hjd_internal::launch_decode(int device, int num_cu, int sampling, int input_
 {
     HJD_HIP(hipSetDevice(device));
     const int fmt = input_format == HJD_IN_Q16_ZIGZAG ? 0 : 1;
+    (void)num_cu;
     SamplingGeom sg;
     if (!sampling_geom(sampling, &sg)) return set_error(HJD_E_INVALID, "unsupported sampling %d", sampling);
-    int grid = grid_blocks > 0 ? grid_blocks : decode_grid(sampling, fmt, tasks);
+    const int grid = grid_blocks > 0 ? grid_blocks : decode_grid(sampling, fmt, tasks);
     if (out_format != HJD_OUT_BGRX && out_format != HJD_OUT_BGR24)
         return set_error(HJD_E_INVALID, "unknown output format %d", out_format);
-    using K = void (*)(const void*, const int*, const FrameDev*, int, int64_t, uint8_t*);
+    using K = void (*)(const void*, const int*, const FrameDev*, int, int64_t, uint8_t*);   // latency kernels
+    using KP = void (*)(const void*, const int*, const FrameDev*, int, int64_t, uint8_t*, int64_t, int64_t);
     const bool latency = kernel_mode == HJD_KERNEL_LATENCY ||
                          (kernel_mode == HJD_KERNEL_AUTO && grid_blocks == 0 && tasks <= latency_max_tasks());
+    // the task split of the persistent kernels (see decode_kernel): default
+    // order over grid * 4 waves, wg-interleave over grid groups of 4-task quads
+    const int64_t split_n = (variant & 2) ? static_cast<int64_t>(grid) : static_cast<int64_t>(grid) * hjd::kWavesPerGroup;
+    const int64_t split_t = (variant & 2) ? (tasks + hjd::kWavesPerGroup - 1) / hjd::kWavesPerGroup : tasks;
+    const int64_t chunk = split_t / split_n, rem = split_t % split_n;
     if (latency && (variant >> kStageShift) == 0) {   // [output format][sampling index][input format]
 #define HJD_KL(V) hjd::decode_kernel_lat<0, 0, V>, hjd::decode_kernel_lat<0, 1, V>, \
                   hjd::decode_kernel_lat<1, 0, V>, hjd::decode_kernel_lat<1, 1, V>, \
@@ -194,7 +193,7 @@ int hjd_internal::launch_decode(int device, int num_cu, int sampling, int input_
         return HJD_OK;
     }
     if (out_format == HJD_OUT_BGR24) {   // [sampling index][input format], default variant
-        static const K kTable24[12] = {
+        static const KP kTable24[12] = {
             hjd::decode_kernel<0, 0, hjd::kOutBgr24>, hjd::decode_kernel<0, 1, hjd::kOutBgr24>,
             hjd::decode_kernel<1, 0, hjd::kOutBgr24>, hjd::decode_kernel<1, 1, hjd::kOutBgr24>,
             hjd::decode_kernel<2, 0, hjd::kOutBgr24>, hjd::decode_kernel<2, 1, hjd::kOutBgr24>,
@@ -202,12 +201,13 @@ int hjd_internal::launch_decode(int device, int num_cu, int sampling, int input_
             hjd::decode_kernel<4, 0, hjd::kOutBgr24>, hjd::decode_kernel<4, 1, hjd::kOutBgr24>,
             hjd::decode_kernel<5, 0, hjd::kOutBgr24>, hjd::decode_kernel<5, 1, hjd::kOutBgr24>};
         if ((variant & 3) != 0) return set_error(HJD_E_INVALID, "kernel variants are BGRX-only");
-        K k24 = kTable24[(sg.index << 1) | fmt];
+        KP k24 = kTable24[(sg.index << 1) | fmt];
         if (sampling == HJD_YUV444 && fmt == 0 && device_d16_gather(device))
             k24 = hjd::decode_kernel<0, 0, hjd::kOutBgr24 | hjd::kVarD16>;
         hipLaunchKernelGGL(k24, dim3(grid), dim3(hjd::kGroupThreads), 0,
                            static_cast<hipStream_t>(stream), d_coefs, d_qt_nat,
-                           reinterpret_cast<const FrameDev*>(d_frames), nframes, tasks, static_cast<uint8_t*>(d_out));
+                           reinterpret_cast<const FrameDev*>(d_frames), nframes, tasks, static_cast<uint8_t*>(d_out),
+                           chunk, rem);
         HJD_HIP(hipGetLastError());
         return HJD_OK;
     }
@@ -223,18 +223,14 @@ int hjd_internal::launch_decode(int device, int num_cu, int sampling, int input_
                       hjd::decode_kernel<S, 0, 16 | (B)>, hjd::decode_kernel<S, 0, 20 | (B)>,                \
                       hjd::decode_kernel<S, 0, 24 | (B)>, hjd::decode_kernel<S, 0, 64 | (B)>,                \
                       hjd::decode_kernel<S, 0, 80 | (B)>}
-        // [strided][4:2:0, 4:4:4, 4:4:4 d16 gather][stages]
-        static const K kStageK[2][3][7] = {
-            {HJD_ST(1, 0), HJD_ST(0, 0), HJD_ST(0, hjd::kVarD16)},
-            {HJD_ST(1, hjd::kVarStrided), HJD_ST(0, hjd::kVarStrided), HJD_ST(0, hjd::kVarStrided | hjd::kVarD16)}};
+        // [4:2:0, 4:4:4, 4:4:4 d16 gather][stages]
+        static const KP kStageK[3][7] = {HJD_ST(1, 0), HJD_ST(0, 0), HJD_ST(0, hjd::kVarD16)};
 #undef HJD_ST
-        const bool strided = (variant & kPlanVarStrided) != 0;
         const int col = sampling == HJD_YUV420 ? 0 : device_d16_gather(device) ? 2 : 1;   // as the product gathers
-        const K k = kStageK[strided][col][si];
-        if (strided && grid_blocks <= 0) grid = resident_groups(num_cu, tasks);
+        const KP k = kStageK[col][si];
         hipLaunchKernelGGL(k, dim3(grid), dim3(hjd::kGroupThreads), 0, static_cast<hipStream_t>(stream), d_coefs,
                            d_qt_nat, reinterpret_cast<const FrameDev*>(d_frames), nframes, tasks,
-                           static_cast<uint8_t*>(d_out));
+                           static_cast<uint8_t*>(d_out), chunk, rem);
         HJD_HIP(hipGetLastError());
         return HJD_OK;
     }
@@ -242,23 +238,17 @@ int hjd_internal::launch_decode(int device, int num_cu, int sampling, int input_
     const int key = (sg.index << 3) | (fmt << 2) | (variant & 3);
 #define HJD_K4(S, F) hjd::decode_kernel<S, F, 0>, hjd::decode_kernel<S, F, 1>, hjd::decode_kernel<S, F, 2>, \
                      hjd::decode_kernel<S, F, 3>
-    static const K kTable[48] = {HJD_K4(0, 0), HJD_K4(0, 1), HJD_K4(1, 0), HJD_K4(1, 1),
+    static const KP kTable[48] = {HJD_K4(0, 0), HJD_K4(0, 1), HJD_K4(1, 0), HJD_K4(1, 1),
                                  HJD_K4(2, 0), HJD_K4(2, 1), HJD_K4(3, 0), HJD_K4(3, 1),
                                  HJD_K4(4, 0), HJD_K4(4, 1), HJD_K4(5, 0), HJD_K4(5, 1)};
 #undef HJD_K4
-    K k = kTable[key];
-    if (sampling == HJD_YUV444 && fmt == 0 && (variant & 3) == 0 && device_d16_gather(device))
-        k = hjd::decode_kernel<0, 0, hjd::kVarD16>;
-    if ((variant & kPlanVarStrided) && fmt == 0 && (sampling == HJD_YUV420 || sampling == HJD_YUV444)) {
-        // strided task order over one resident generation of groups
-        k = sampling == HJD_YUV420 ? hjd::decode_kernel<1, 0, hjd::kVarStrided>
-          : device_d16_gather(device) ? hjd::decode_kernel<0, 0, hjd::kVarStrided | hjd::kVarD16>
-                                      : hjd::decode_kernel<0, 0, hjd::kVarStrided>;
-        if (grid_blocks <= 0) grid = resident_groups(num_cu, tasks);
-    }
+    KP k = kTable[key];
+    if (sampling == HJD_YUV444 && fmt == 0 && (variant & 2) == 0 && device_d16_gather(device))
+        k = (variant & 1) ? hjd::decode_kernel<0, 0, hjd::kVarPlainStores | hjd::kVarD16>
+                          : hjd::decode_kernel<0, 0, hjd::kVarD16>;
     hipLaunchKernelGGL(k, dim3(grid), dim3(hjd::kGroupThreads), 0, static_cast<hipStream_t>(stream),
                        d_coefs, d_qt_nat, reinterpret_cast<const FrameDev*>(d_frames), nframes, tasks,
-                       static_cast<uint8_t*>(d_out));
+                       static_cast<uint8_t*>(d_out), chunk, rem);
     HJD_HIP(hipGetLastError());
     return HJD_OK;
 }
@@ -393,10 +383,6 @@ int hjd_plan_create(hjd_ctx* ctx, const hjd_frame* frames, int nframes, int inpu
     p->sampling = sampling;
     p->out_format = out_format;
     p->nframes = nframes;
-    {
-        const char* e = getenv("HJD_ORDER");   // A/B: the strided task order on every plan
-        if (e && !strcmp(e, "strided")) p->variant |= kPlanVarStrided;
-    }
     p->tasks = tasks;
     p->pixels = pixels;
     p->coef_bytes = blocks * (input_format == HJD_IN_Q16_ZIGZAG ? 128 : 256);
@@ -436,12 +422,16 @@ int hjd_plan_destroy(hjd_plan* plan)
 int hjd_plan_set_variant(hjd_plan* plan, int variant)
 {
     if (!plan) return fail(HJD_E_INVALID, "plan is NULL");
-#ifdef HJD_ABLATION
-    if (variant < 0 || variant > 127) return fail(HJD_E_INVALID, "unknown kernel variant %d", variant);
-#else
-    if (variant < 0 || variant > 7) return fail(HJD_E_INVALID, "unknown kernel variant %d", variant);
-#endif
+    if (variant < 0 || variant > 3) return fail(HJD_E_INVALID, "unknown kernel variant %d", variant);
     plan->variant = variant;
+    return HJD_OK;
+}
+
+int hjd_plan_set_chunk(hjd_plan* plan, int tasks)
+{
+    if (!plan || tasks < 0 || tasks > 4096) return fail(HJD_E_INVALID, "invalid chunk arguments");
+    plan->tuned_per_wave = tasks;
+    plan->tuned_grid = tasks ? grid_for_chunk(std::max<int64_t>(plan->tasks, 1), tasks) : 0;   // 0: shape default
     return HJD_OK;
 }
 
@@ -472,24 +462,30 @@ int64_t hjd_plan_coef_bytes(const hjd_plan* plan) { return plan ? plan->coef_byt
 // -> 0.76) and both int32 (idct.h) formats (4:2:0 0.67 -> 0.76-0.78, 4:4:4
 // 0.74-0.75 -> 0.765-0.77), same box (profiles/r03_tune_tasks_per_wave_ext.json).
 // HJD_TASKS_PER_WAVE overrides it (tuning).
+// Groups for `per_wave` tasks per wave, but never fewer than ~4 waves per
+// SIMD (256 CUs x 4 SIMDs): a single 4:4:4 frame at 16 tasks per wave would
+// leave most of the chip idle.
+static int grid_for_chunk(int64_t tasks, int64_t per_wave)
+{
+    per_wave = std::max<int64_t>(1, std::min<int64_t>(per_wave, tasks / (4 * 1024)));
+    const int64_t waves = (tasks + per_wave - 1) / per_wave;
+    const int64_t groups = (waves + hjd::kWavesPerGroup - 1) / hjd::kWavesPerGroup;
+    return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(groups, int64_t(1) << 24)));
+}
+
 static int decode_grid(int sampling, int fmt, int64_t tasks)
 {
     static const int64_t env = [] {
         const char* e = getenv("HJD_TASKS_PER_WAVE");
         return e ? static_cast<int64_t>(atoll(e)) : int64_t(0);
     }();
-    // ... but never fewer than ~4 waves per SIMD (256 CUs x 4 SIMDs): a single
-    // 4:4:4 frame at 16 tasks per wave would leave most of the chip idle.
     int64_t per_wave = 16;
     if (fmt != 0 || sampling == HJD_GRAY || sampling == HJD_YUV411_H4V1)
         per_wave = 1;
     else if (sampling == HJD_YUV420)
         per_wave = 2;
     if (env > 0) per_wave = env;
-    per_wave = std::max<int64_t>(1, std::min<int64_t>(per_wave, tasks / (4 * 1024)));
-    const int64_t waves = (tasks + per_wave - 1) / per_wave;
-    const int64_t groups = (waves + hjd::kWavesPerGroup - 1) / hjd::kWavesPerGroup;
-    return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(groups, int64_t(1) << 24)));
+    return grid_for_chunk(tasks, per_wave);
 }
 
 static int default_grid(const hjd_ctx* ctx, int64_t work_waves)
@@ -507,11 +503,93 @@ int hjd_plan_launch(hjd_plan* plan, const void* d_coefs, void* d_out, void* stre
     if ((reinterpret_cast<uintptr_t>(d_coefs) | reinterpret_cast<uintptr_t>(d_out)) & 15)
         return fail(HJD_E_INVALID, "device buffers must be 16-byte aligned");
     if (grid_blocks < 0) return fail(HJD_E_INVALID, "grid_blocks < 0");
+    if (grid_blocks == 0 && plan->tuned_grid > 0 && plan->kernel_mode != HJD_KERNEL_LATENCY)
+        grid_blocks = plan->tuned_grid;   // hjd_plan_autotune's / hjd_plan_set_chunk's chunk
     return hjd_internal::launch_decode(plan->ctx->device, plan->ctx->num_cu, plan->sampling, plan->input_format,
                                        plan->variant, d_coefs, plan->d_qt,
                                        reinterpret_cast<const hjd_internal::FrameRecord*>(plan->d_frames),
                                        plan->nframes, plan->tasks, d_out, stream, grid_blocks, plan->out_format,
                                        plan->kernel_mode);
+}
+
+// The fused kernel's launch adapted to the device it runs on (VERDICT r3:
+// the same 4:2:0 kernel ran ~10 % slower on some MI355X boxes, its memory
+// side with it, while 4:4:4 did not; which per-wave chunk and store policy
+// keep HBM busiest differs by box and shape: profiles/r04c_tpw_sweep.json).
+// Times every candidate -- 1, 2, 4, 8 and 16 tasks per wave x nt / plain
+// output stores (BGRX) -- on the plan's own buffers, `rounds` interleaved
+// rounds of one warm + two timed launches each, keeps the fastest (minimum
+// over rounds) for the plan's later default launches.  All candidates give
+// identical pixels.  Synchronous; plans small enough for the latency kernel
+// are left as they are.
+int hjd_plan_autotune(hjd_plan* plan, const void* d_coefs, void* d_out, void* stream, int rounds,
+                      int32_t* tasks_per_wave, int32_t* variant)
+{
+    if (!plan || rounds < 0 || rounds > 16) return fail(HJD_E_INVALID, "invalid autotune arguments");
+    if (!d_coefs || !d_out || ((reinterpret_cast<uintptr_t>(d_coefs) | reinterpret_cast<uintptr_t>(d_out)) & 15))
+        return fail(HJD_E_INVALID, "NULL or unaligned device buffer");
+    if (rounds == 0) rounds = 2;
+    auto report = [&]() {
+        if (tasks_per_wave) *tasks_per_wave = plan->tuned_per_wave;
+        if (variant) *variant = plan->variant;
+        return HJD_OK;
+    };
+    if (plan->tasks == 0 || plan->kernel_mode == HJD_KERNEL_LATENCY ||
+        (plan->kernel_mode == HJD_KERNEL_AUTO && plan->tasks <= latency_max_tasks()))
+        return report();
+    struct Cand {
+        int64_t per_wave;   // tasks per wave
+        int store;          // variant bit 0
+        int grid;
+        float best_ms;
+    };
+    std::vector<Cand> cands;
+    for (int64_t pw : {1, 2, 4, 8, 16}) {
+        const int g = grid_for_chunk(plan->tasks, pw);
+        bool dup = false;
+        for (const Cand& c : cands) dup |= c.grid == g;
+        if (dup) continue;
+        for (int st = 0; st < (plan->out_format == HJD_OUT_BGRX ? 2 : 1); ++st) cands.push_back({pw, st, g, 1e30f});
+    }
+    HJD_HIP(hipSetDevice(plan->ctx->device));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    hipEvent_t e0, e1;
+    HJD_HIP(hipEventCreate(&e0));
+    if (hipEventCreate(&e1) != hipSuccess) {
+        (void)hipEventDestroy(e0);
+        return fail(HJD_E_HIP, "hipEventCreate");
+    }
+    const int keep = plan->variant & ~1;
+    int rc = HJD_OK;
+    for (int r = 0; r < rounds && rc == HJD_OK; ++r) {
+        for (Cand& c : cands) {
+            const int v = keep | c.store;
+            auto go = [&]() {
+                return hjd_internal::launch_decode(plan->ctx->device, plan->ctx->num_cu, plan->sampling,
+                                                   plan->input_format, v, d_coefs, plan->d_qt,
+                                                   reinterpret_cast<const hjd_internal::FrameRecord*>(plan->d_frames),
+                                                   plan->nframes, plan->tasks, d_out, s, c.grid, plan->out_format,
+                                                   HJD_KERNEL_PERSISTENT);
+            };
+            float ms = 0;
+            if ((rc = go()) || (rc = hipEventRecord(e0, s) == hipSuccess ? HJD_OK : HJD_E_HIP) || (rc = go()) ||
+                (rc = go()) || (rc = hipEventRecord(e1, s) == hipSuccess ? HJD_OK : HJD_E_HIP) ||
+                (rc = hipEventSynchronize(e1) == hipSuccess ? HJD_OK : HJD_E_HIP) ||
+                (rc = hipEventElapsedTime(&ms, e0, e1) == hipSuccess ? HJD_OK : HJD_E_HIP))
+                break;
+            c.best_ms = std::min(c.best_ms, ms / 2);
+        }
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (rc) return rc == HJD_E_HIP ? fail(HJD_E_HIP, "autotune timing failed") : rc;
+    const Cand* best = &cands[0];
+    for (const Cand& c : cands)
+        if (c.best_ms < best->best_ms) best = &c;
+    plan->tuned_grid = best->grid;
+    plan->tuned_per_wave = static_cast<int>(best->per_wave);
+    plan->variant = keep | best->store;
+    return report();
 }
 
 int hjd_debug_plan_launch_stages(hjd_plan* plan, int stages, const void* d_coefs, void* d_out, void* stream,
@@ -527,9 +605,10 @@ int hjd_debug_plan_launch_stages(hjd_plan* plan, int stages, const void* d_coefs
     if (!d_coefs || !d_out || ((reinterpret_cast<uintptr_t>(d_coefs) | reinterpret_cast<uintptr_t>(d_out)) & 15))
         return fail(HJD_E_INVALID, "NULL or unaligned device buffer");
     return hjd_internal::launch_decode(plan->ctx->device, plan->ctx->num_cu, plan->sampling, plan->input_format,
-                                       (stages << kStageShift) | (plan->variant & kPlanVarStrided), d_coefs, plan->d_qt,
+                                       stages << kStageShift, d_coefs, plan->d_qt,
                                        reinterpret_cast<const hjd_internal::FrameRecord*>(plan->d_frames),
-                                       plan->nframes, plan->tasks, d_out, stream, grid_blocks < 0 ? 0 : grid_blocks,
+                                       plan->nframes, plan->tasks, d_out, stream,
+                                       grid_blocks > 0 ? grid_blocks : plan->tuned_grid,
                                        plan->out_format, HJD_KERNEL_PERSISTENT);
 }
 

@@ -167,3 +167,74 @@ print("fallback ok")
     env["HJD_D16_PROBE"] = "fail"
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "fallback ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+@pytest.mark.parametrize("s", [0, 1])
+def test_autotune_keeps_pixels(hjd, ctx, s):
+    """hjd_plan_autotune times the launch shapes (tasks per wave x store
+    policy) on the plan's own buffers and keeps the fastest: the chosen shape
+    must be a candidate, the output left by the tuning launches and by a later
+    default launch must both be the oracle's, and a plan small enough for the
+    latency kernel is left unchanged."""
+    import torch
+    w, h, nf = 1920, 1080, 6
+    coefs, qt = O.synthetic_coefs(w, h, s, seed=900 + s)
+    exp = O.decode_q16(coefs, qt, w, h, s)
+    nblk = coefs.shape[0]
+    specs = [hjd.FrameSpec(w, h, s, coef_offset=i * nblk, out_offset=i * h * w * 4, qt_index=(0, 1, 2))
+             for i in range(nf)]
+    plan = hjd.Plan(ctx, specs, hjd.IN_Q16_ZIGZAG, qtables=qt)
+    assert plan.tasks > 1024
+    d_coefs = torch.from_numpy(np.ascontiguousarray(np.tile(coefs, (nf, 1)))).cuda()
+    out = torch.zeros((nf, h, w), dtype=torch.int32, device="cuda")
+    tpw, var = plan.autotune(d_coefs, out)
+    print("autotune chose", tpw, "tasks per wave, variant", var)
+    assert tpw in (1, 2, 4, 8, 16) and var in (0, 1)
+    torch.cuda.synchronize()
+    for i in range(nf):
+        np.testing.assert_array_equal(out[i].cpu().numpy().view(np.uint32), exp, err_msg=f"tuning launch, frame {i}")
+    out.zero_()
+    plan.launch(d_coefs, out)
+    torch.cuda.synchronize()
+    for i in range(nf):
+        np.testing.assert_array_equal(out[i].cpu().numpy().view(np.uint32), exp, err_msg=f"tuned launch, frame {i}")
+    small = hjd.Plan(ctx, specs[:1], hjd.IN_Q16_ZIGZAG, qtables=qt)
+    if small.tasks <= 1024:
+        assert small.autotune(d_coefs, out) == (0, 0)
+
+
+@pytest.mark.parametrize("s", [0, 1])
+@pytest.mark.parametrize("chunk", [1, 3, 16])
+def test_chunking_vs_oracle(hjd, ctx, s, chunk):
+    """The persistent kernel's task chunks (hjd_plan_set_chunk, the shapes
+    hjd_plan_autotune picks from) must each decode every frame of a mixed
+    batch exactly once, bit-exact -- frames of different sizes (right and
+    bottom edge strips), qtables and output pitches, output guard bands
+    untouched, over repeated launches."""
+    import torch
+    tasks = chunk
+    sizes = [(1920, 1080), (313, 234), (3840, 64), (1000, 17), (1920, 1080), (257, 600)]
+    guard = 256
+    specs, coefs, qts, exps, off_blk, off_b = [], [], [], [], 0, guard
+    for i, (w, h) in enumerate(sizes):
+        c, q = O.synthetic_coefs(w, h, s, seed=70 + i + 10 * s, quality_scale=0.6 + 0.2 * i)
+        pitch = 4 * w + 16 * (i % 3)
+        specs.append(hjd.FrameSpec(w, h, s, coef_offset=off_blk, out_offset=off_b, out_pitch=pitch,
+                                   qt_index=(3 * i, 3 * i + 1, 3 * i + 2)))
+        coefs.append(c); qts.append(q); exps.append((O.decode_q16(c, q, w, h, s), off_b, pitch))
+        off_blk += c.shape[0]; off_b += pitch * h + guard
+    plan = hjd.Plan(ctx, specs, hjd.IN_Q16_ZIGZAG, qtables=np.concatenate(qts))
+    plan.set_kernel(hjd.KERNEL_PERSISTENT)
+    plan.set_chunk(tasks)
+    d_coefs = torch.from_numpy(np.concatenate(coefs)).cuda()
+    buf = torch.full((off_b,), 0x5A, dtype=torch.uint8, device="cuda")
+    for rep in range(3):
+        plan.launch(d_coefs, buf)
+    torch.cuda.synchronize()
+    full = buf.cpu().numpy()
+    mask = np.ones(full.shape, bool)
+    for (e, off, pitch), (w, h) in zip(exps, sizes):
+        img = full[off:off + pitch * h].reshape(h, pitch)[:, :4 * w]
+        np.testing.assert_array_equal(np.ascontiguousarray(img).view(np.uint32), e, err_msg=f"{w}x{h} {chunk}")
+        mask[off:off + pitch * h].reshape(h, pitch)[:, :4 * w] = False
+    assert (full[mask] == 0x5A).all(), "write outside the frames"

@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--grids", default="0")
     ap.add_argument("--kernels", default="1", help="hjd_kernel_mode list: 1 persistent, 2 latency")
     ap.add_argument("--no-check", action="store_true", help="ablation variants: outputs differ by design")
+    ap.add_argument("--chunks", default="", help="hjd_plan_set_chunk configs (tasks per wave), e.g. s1,s2,s16; "
+                                                 "replaces --grids")
     ap.add_argument("--stages", default="0", help="stage variants (hjd_debug_plan_launch_stages): 0 = the product, "
                                                   "80 memory only, 4 no stores, ... (outputs wrong by design)")
     args = ap.parse_args()
@@ -58,18 +60,24 @@ def main():
     kernels = [int(k) for k in args.kernels.split(",")]
     stream = torch.cuda.current_stream()
     stages = [int(x) for x in args.stages.split(",")]
+    if args.chunks:
+        grids = args.chunks.split(",")
     times = {(k, v, g, st): [] for k in kernels for v in variants for g in grids for st in stages}
     ref = None
     for rnd in range(args.rounds):
         for k, v, g, st in times:
             plan.set_kernel(k)
             plan.set_variant(v)
+            grid = g
+            if isinstance(g, str):   # --chunks
+                plan.set_chunk(int(g[1:]))
+                grid = 0
 
             def go():
                 if st:
-                    plan.launch_stages(st, coefs, out, stream, grid_blocks=g)
+                    plan.launch_stages(st, coefs, out, stream, grid_blocks=grid)
                 else:
-                    plan.launch(coefs, out, stream, grid_blocks=g)
+                    plan.launch(coefs, out, stream, grid_blocks=grid)
             go()   # warm
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
@@ -82,7 +90,8 @@ def main():
                 sig = int(out[:, ::97, ::89].sum().item())
                 ref = sig if ref is None else ref
                 assert sig == ref, f"kernel {k} variant {v} grid {g} output differs"
-    res = {"workload": args.workload, "frames": nf, "bytes_per_launch": nbytes, "signature": ref, "results": []}
+    res = {"workload": args.workload, "frames": nf, "bytes_per_launch": nbytes, "signature": ref,
+           "box": bench.box_identity(torch), "results": []}
     for (k, v, g, st), ts in times.items():
         med = statistics.median(ts)
         res["results"].append({"kernel": k, "variant": v, "grid": g, "stages": st, "median_ms": round(med, 4),
