@@ -522,6 +522,9 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
     pool = encode_pool(w, h, s, npool, seed0=7919)       # identical on every rank: ids map to the same files
     infos = [hjd.parse(d) for d in pool]
     max_blocks = max(i.nblocks for i in infos)
+    # N>1 from a parent bench run: this GPU's previous-generation rank must have
+    # released its HBM before this rank allocates (max over ranks, reported)
+    released = shard.aggregate(device_released(torch, dev), reduce_max=("hbm_wait_s", "hbm_busy_GiB"))
     ctx = hjd.Context(dev.index)
     gpu_entropy = wl.get("entropy") == "gpu"
     d2h = bool(wl.get("d2h"))
@@ -685,6 +688,10 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
                            "returns frames: 2, 4 and the stream's slot count of concurrent streams, one frame's "
                            "output per copy (plus one stream of 256 MiB copies); the best rate is the ceiling"},
                 "output_checked_vs_oracle": bool(ok)},
+            "hbm_at_start": {"wait_s_max_over_ranks": round(released["hbm_wait_s"], 2),
+                             "busy_GiB_max_over_ranks": round(released["hbm_busy_GiB"], 2),
+                             "how": "hipMemGetInfo polled before the first allocation until at most "
+                                    f"{HBM_BUSY_FRAC:.0%} of the device is held by any process (<= 60 s)"},
             "timed_seconds": round(wall_max, 3),
             "stream_check": {"frames_checked": int(agg["frames_checked"]), "checksum": int(agg["checksum"]),
                              "checksum_oracle": int(agg["checksum_oracle"]), "id_sum": int(agg["id_sum"]),
@@ -1316,7 +1323,9 @@ def main():
 def _wait_sibling_ranks_exit(timeout_s=60.0):
     """Best effort, N>1: before rank 0 starts the child ranks, let the other
     ranks of this run (children of the same torchrun agent) exit, so the GPUs
-    never carry both generations of processes."""
+    never carry both generations of processes.  Returns how many were still
+    alive at the deadline (each child rank also waits for its GPU's HBM to be
+    released: device_released)."""
     agent, me = os.getppid(), os.getpid()
     deadline = time.time() + timeout_s
     while time.time() < deadline:
@@ -1332,8 +1341,26 @@ def _wait_sibling_ranks_exit(timeout_s=60.0):
             if int(fields[1]) == agent and fields[0] not in ("Z", "X"):
                 alive += 1
         if alive == 0:
-            return
+            return 0
         time.sleep(0.5)
+    return alive
+
+
+HBM_BUSY_FRAC = 0.10
+
+
+def device_released(torch, dev, timeout_s=60.0):
+    """Poll the device's free HBM (hipMemGetInfo counts every process's
+    allocations) until at most HBM_BUSY_FRAC of it is in use, so a child run
+    started right after the parent's ranks left does not share the GPU with
+    them.  Returns the wait and the HBM still in use when it ended."""
+    t0 = time.time()
+    while True:
+        free, total = torch.cuda.mem_get_info(dev)
+        busy = total - free
+        if busy <= HBM_BUSY_FRAC * total or time.time() - t0 >= timeout_s:
+            return {"hbm_wait_s": time.time() - t0, "hbm_busy_GiB": busy / 2**30}
+        time.sleep(0.25)
 
 
 def config5_stream_leg(world, dist_backend, frame_ids=100000, workload="stream4k420"):
@@ -1358,8 +1385,7 @@ def config5_stream_leg(world, dist_backend, frame_ids=100000, workload="stream4k
         port = sk.getsockname()[1]
         sk.close()
     cmd, env, _ = stream_leg_command(world, dist_backend, frame_ids, per_gpu, port, os.environ, workload)
-    if world > 1:
-        _wait_sibling_ranks_exit()
+    siblings_alive = _wait_sibling_ranks_exit() if world > 1 else 0
     log("running config-5 stream leg:", " ".join(cmd[1:]))
     p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env,
                          start_new_session=True)
@@ -1384,6 +1410,7 @@ def config5_stream_leg(world, dist_backend, frame_ids=100000, workload="stream4k
             "output": d["config"]["output"],
             "output_checked_vs_oracle": d["end_to_end"]["output_checked_vs_oracle"],
             "steps_checked": d["stream_check"]["steps_checked"],
+            "parent_ranks_alive_at_start": siblings_alive, "hbm_at_start": d.get("hbm_at_start"),
             "command": " ".join(["python"] + [os.path.basename(c) if c.endswith("bench.py") else c
                                               for c in cmd[1:]])}
 

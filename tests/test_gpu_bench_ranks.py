@@ -66,6 +66,9 @@ def test_two_ranks_pixel_bench():
     assert s5["n_gpus"] == 2 and s5["value"] > 0 and s5["output_checked_vs_oracle"] is True
     assert s5["frames_per_gpu_per_step"] == 12 and "shard_round_robin over 2 rank(s)" in s5["sharding"]
     assert s5["steps"] == 3 and s5["timed_frame_ids"] == 72 and s5["steps_checked"] == [2, 3]
+    # the child ranks started on GPUs the parent's ranks had left and released
+    assert s5["parent_ranks_alive_at_start"] == 0
+    assert s5["hbm_at_start"]["wait_s_max_over_ranks"] < 60, s5["hbm_at_start"]
 
 
 @pytest.mark.gpu

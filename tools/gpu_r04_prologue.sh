@@ -49,6 +49,12 @@ PY
   cd /tmp && export TMPDIR=/tmp
   timeout -s KILL 180 rocprofv3 -i $R/tools/pmc_tcc_write.txt --output-format csv -d $O/slow_tcc -o tcc -- \
       python3 $R/bench.py --frames 256 --steps 2 --warmup 1 --no-cpu --no-stream --no-stages --no-fhd --no-autotune > $O/slow_tcc.json 2> $O/slow_tcc.err || { echo "TCC pass failed"; tail -5 $O/slow_tcc.err; }
+  for p in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 300 rocprofv3 --pmc $p --output-format csv -d $O/slow_pmc_$p -o pmc -- \
+        python3 $R/bench.py --frames 256 --steps 3 --warmup 1 --no-cpu --no-stream --no-stages --no-fhd --no-autotune > $O/slow_pmc_$p.json 2> $O/slow_pmc_$p.err || { echo "PMC $p failed"; tail -5 $O/slow_pmc_$p.err; }
+  done
+  timeout -k 10 300 rocprofv3 -i $R/tools/pmc_pixel.txt --output-format csv -d $O/slow_sq_4k420 -o px -- \
+      python3 $R/bench.py --workload 4k420 --frames 256 --steps 2 --warmup 1 --no-cpu --no-stream --no-stages --no-444 --no-fhd --no-autotune > $O/slow_sq_4k420.json 2> $O/slow_sq_4k420.err || { echo "SQ pass failed"; tail -5 $O/slow_sq_4k420.err; }
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/slow_kt -o bench -- \
       python3 $R/bench.py --no-stream --no-cpu --no-fhd > $O/slow_kt_bench.json 2> $O/slow_kt_bench.err || { echo KTRACE FAILED; exit 1; }
   cd $R
