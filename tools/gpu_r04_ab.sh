@@ -8,7 +8,7 @@ O=$R/gpurun_out/${1:-r04ab}
 B=${BASE:-base0}
 mkdir -p $O
 cd $R
-for rep in 1 2; do
+for rep in $(seq 1 ${REPS:-2}); do
   for lib in cur $B; do
     if [ $lib = cur ]; then unset HJD_LIB; else export HJD_LIB=$R/build/variants/$lib/libhjd.so; fi
     for wl in 4k420 4k444; do
