@@ -321,24 +321,19 @@ __device__ __forceinline__ void colour_stage(const char* __restrict__ slots, int
             const ChromaTerms c1 = chroma_terms<1>(cu, cv);
             const ChromaPair p0 = pair_of(c0, c0), p1 = pair_of(c1, c1);
             const int ya0 = y_base + y0;
-            // pixels in either branch, stores after the join: every path
-            // through a full strip issues the same stores (the loop head's
-            // counted wait relies on it, see decode_kernel)
-            uint32_t a[4], b[4];
             if (__builtin_amdgcn_ballot_w64((p0.flagged | p1.flagged) != 0)) {   // wave-uniform, rare
-                pixels2<true>(ya.x, p0, &c0, &c0, a[0], a[1]);
-                pixels2<true>(ya.y, p1, &c1, &c1, a[2], a[3]);
-                pixels2<true>(yb.x, p0, &c0, &c0, b[0], b[1]);
-                pixels2<true>(yb.y, p1, &c1, &c1, b[2], b[3]);
+                if (kFull || ya0 < height)
+                    emit_row4<true, kVariant, kFull>(row0, loff, xa, width, ya.x, ya.y, p0, p1, &c0, &c0, &c1, &c1);
+                if (kFull || ya0 + 1 < height)
+                    emit_row4<true, kVariant, kFull>(row0 + pitch, loff, xa, width, yb.x, yb.y, p0, p1, &c0, &c0, &c1,
+                                                     &c1);
             } else {
-                pixels2<false>(ya.x, p0, &c0, &c0, a[0], a[1]);
-                pixels2<false>(ya.y, p1, &c1, &c1, a[2], a[3]);
-                pixels2<false>(yb.x, p0, &c0, &c0, b[0], b[1]);
-                pixels2<false>(yb.y, p1, &c1, &c1, b[2], b[3]);
+                if (kFull || ya0 < height)
+                    emit_row4<false, kVariant, kFull>(row0, loff, xa, width, ya.x, ya.y, p0, p1, &c0, &c0, &c1, &c1);
+                if (kFull || ya0 + 1 < height)
+                    emit_row4<false, kVariant, kFull>(row0 + pitch, loff, xa, width, yb.x, yb.y, p0, p1, &c0, &c0,
+                                                      &c1, &c1);
             }
-            if (kFull || ya0 < height) store4<kFull, kVariant>(row0, loff, xa, width, a[0], a[1], a[2], a[3]);
-            if (kFull || ya0 + 1 < height)
-                store4<kFull, kVariant>(row0 + pitch, loff, xa, width, b[0], b[1], b[2], b[3]);
         }
     } else if constexpr (kSampling == 0) {
         const int m = cg >> 1;        // MCU within strip (16 x 8 px)
@@ -368,15 +363,12 @@ __device__ __forceinline__ void colour_stage(const char* __restrict__ slots, int
                 const int ya = y_base + y;
                 uint8_t* row = strip + static_cast<int64_t>(4 * it + h) * pitch;   // wave-uniform
                 if (kFull || ya < height) {
-                    uint32_t a[4];   // stores after the join, as at 4:2:0
-                    if (__builtin_amdgcn_ballot_w64((p01.flagged | p23.flagged) != 0)) {
-                        pixels2<true>(sy.x, p01, &c0, &c1, a[0], a[1]);
-                        pixels2<true>(sy.y, p23, &c2, &c3, a[2], a[3]);
-                    } else {
-                        pixels2<false>(sy.x, p01, &c0, &c1, a[0], a[1]);
-                        pixels2<false>(sy.y, p23, &c2, &c3, a[2], a[3]);
-                    }
-                    store4<kFull, kVariant>(row, loff, xa, width, a[0], a[1], a[2], a[3]);
+                    if (__builtin_amdgcn_ballot_w64((p01.flagged | p23.flagged) != 0))
+                        emit_row4<true, kVariant, kFull>(row, loff, xa, width, sy.x, sy.y, p01, p23, &c0, &c1, &c2,
+                                                         &c3);
+                    else
+                        emit_row4<false, kVariant, kFull>(row, loff, xa, width, sy.x, sy.y, p01, p23, &c0, &c1, &c2,
+                                                          &c3);
                 }
             }
         }
@@ -826,6 +818,9 @@ __device__ __forceinline__ void idct_stage(char* __restrict__ slots, char* __res
 #ifndef HJD_XCD
 #define HJD_XCD 1
 #endif
+#ifndef HJD_PREFETCH_AT
+#define HJD_PREFETCH_AT -1   // tuning: issue the next task's loads after IDCT round N (-1: before round 0)
+#endif
 #ifndef HJD_XCD_CHUNK
 #define HJD_XCD_CHUNK 0
 #endif
@@ -850,8 +845,6 @@ __device__ __forceinline__ uint32_t group_order(uint32_t bid, uint32_t ngroups)
         return ((k / C) * 8 + x) * C + k % C;
     }
 }
-
-typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 // The fused kernel.  Persistent grid; wave w owns the contiguous task range
 // [w*T/W, (w+1)*T/W) so its frame changes rarely and the frame record stays in
@@ -906,35 +899,19 @@ __global__ __launch_bounds__(kGroupThreads, KLayout<kSampling>::min_waves) void 
 #pragma unroll
         for (int k = 0; k < 4; ++k) q[c][k] = 0;
 
-    constexpr int kRows = KGeom<kSampling>::kMcuH;
-    constexpr int kStripW = KGeom<kSampling>::kStripW;
-    constexpr bool kSplit = HJD_SPLIT444 != 0 && kSampling == 0 && (kVariant & (kAblNoColour | kAblNoIdct)) == 0;
-    // A full strip lies inside its frame and has 16-byte aligned rows: the
-    // colour stage stores it with one unguarded store per row segment.
-    auto is_full = [&](const FrameCursor& c, const TaskGeom& g) {
-        return c.vec_ok && g.x_base + kStripW <= c.width && g.y_base + kRows <= c.height;
-    };
-
     FrameCursor pc;   // frame of the task being prefetched
     cursor_seek(pc, frames, nframes, total_tasks, t_begin);
-    // the first full strip at or after t in this wave's sequence (pc moved to
-    // its frame), or -1
-    auto next_full = [&](int64_t t) -> int64_t {
-        for (; t < t_end; t += t_step) {
-            while (t >= pc.end) cursor_load(pc, frames, nframes, total_tasks, pc.idx + 1);
-            if (is_full(pc, task_geom<kSampling>(pc, t))) return t;
-        }
-        return -1;
-    };
 
-    i32x4 pre[6];     // prefetch registers (kFmt 0): 6 x 16 B per lane = 6 KiB per wave
+    int4 pre[6];      // prefetch registers (kFmt 0): 6 x 16 B per lane = 6 KiB per wave
     auto prefetch = [&](const TaskGeom& g) {
-        const i32x4* src = reinterpret_cast<const i32x4*>(static_cast<const short*>(coefs) + g.blk0 * 64);
+        const int4* src = reinterpret_cast<const int4*>(static_cast<const short*>(coefs) + g.blk0 * 64);
         if (g.nblk == kTaskBlocks) {
 #pragma unroll
             for (int k = 0; k < 6; ++k) {
 #if HJD_NT_LOAD
-                pre[k] = __builtin_nontemporal_load(src + lane + 64 * k);
+                typedef int i32x4 __attribute__((ext_vector_type(4)));
+                const i32x4 t = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(src) + lane + 64 * k);
+                pre[k] = make_int4(t.x, t.y, t.z, t.w);
 #else
                 pre[k] = src[lane + 64 * k];
 #endif
@@ -943,40 +920,72 @@ __global__ __launch_bounds__(kGroupThreads, KLayout<kSampling>::min_waves) void 
 #pragma unroll
             for (int k = 0; k < 6; ++k) {
                 const int j = lane + 64 * k;   // 16-byte chunk index within the task
-                pre[k] = (j < g.nblk * 8) ? src[j] : i32x4{0, 0, 0, 0};
+                pre[k] = (j < g.nblk * 8) ? src[j] : make_int4(0, 0, 0, 0);
             }
         }
     };
-    // the task's quantisation rows (when its frame's tables differ from the
-    // last task's) and its coefficients from the prefetch registers into LDS
-    auto stage = [&](const FrameCursor& cc) {
-        if (cc.qt0 != q_tables[0] || cc.qt1 != q_tables[1] || cc.qt2 != q_tables[2]) {
-            q_tables[0] = cc.qt0; q_tables[1] = cc.qt1; q_tables[2] = cc.qt2;
-            if constexpr (L::t2) {
-                // lane group c < 3 writes component c's row r into the wave's
-                // table copy (read by later DS ops of this wave, in order)
-                const int c = lane >> 3;
-                if (c < 3) {
-                    uint32_t qq[4];
-                    load_qrow_pk(qt_pool, c == 0 ? q_tables[0] : c == 1 ? q_tables[1] : q_tables[2], r, qq);
-                    *reinterpret_cast<uint4*>(qlds + c * 128 + r * 16) = make_uint4(qq[0], qq[1], qq[2], qq[3]);
+    if constexpr (kFmt == 0) {
+        prefetch(task_geom<kSampling>(pc, t_begin));
+        // the first task's table rows load beside its coefficients, so a wave
+        // start waits for one memory round trip, not two
+        if constexpr (!L::t2) {
+            q_tables[0] = pc.qt0; q_tables[1] = pc.qt1; q_tables[2] = pc.qt2;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) load_qrow_pk(qt_pool, q_tables[c], r, q[c]);
+        }
+        __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0): see the edge-strip drain below
+    }
+
+    for (int64_t task = t_begin, next_task; task >= 0; task = next_task) {
+        next_task = task + t_step < t_end ? task + t_step : -1;   // -1: this is the wave's last task
+        const FrameCursor cc = pc;
+        const TaskGeom tg = task_geom<kSampling>(cc, task);
+        if constexpr (kFmt == 0) {
+            if (cc.qt0 != q_tables[0] || cc.qt1 != q_tables[1] || cc.qt2 != q_tables[2]) {
+                q_tables[0] = cc.qt0; q_tables[1] = cc.qt1; q_tables[2] = cc.qt2;
+                if constexpr (L::t2) {
+                    // lane group c < 3 writes component c's row r into the wave's
+                    // table copy (read by later DS ops of this wave, in order)
+                    const int c = lane >> 3;
+                    if (c < 3) {
+                        uint32_t qq[4];
+                        load_qrow_pk(qt_pool, c == 0 ? q_tables[0] : c == 1 ? q_tables[1] : q_tables[2], r, qq);
+                        *reinterpret_cast<uint4*>(qlds + c * 128 + r * 16) = make_uint4(qq[0], qq[1], qq[2], qq[3]);
+                    }
+                } else {
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) load_qrow_pk(qt_pool, q_tables[c], r, q[c]);
                 }
-            } else {
-#pragma unroll
-                for (int c = 0; c < 3; ++c) load_qrow_pk(qt_pool, q_tables[c], r, q[c]);
             }
-        }
 #pragma unroll
-        for (int k = 0; k < 6; ++k) {
-            const int j = lane + 64 * k;
-            *reinterpret_cast<i32x4*>(slots + (j >> 3) * kSlotBytes + (j & 7) * 16) = pre[k];
+            for (int k = 0; k < 6; ++k) {
+                const int j = lane + 64 * k;
+                *reinterpret_cast<int4*>(slots + (j >> 3) * kSlotBytes + (j & 7) * 16) = pre[k];
+            }
+            wave_lds_sync();
+            if (HJD_PREFETCH_AT < 0 && next_task >= 0) {
+                while (next_task >= pc.end) cursor_load(pc, frames, nframes, total_tasks, pc.idx + 1);
+                prefetch(task_geom<kSampling>(pc, next_task));
+            }
+        } else {
+            if (next_task >= 0)
+                while (next_task >= pc.end) cursor_load(pc, frames, nframes, total_tasks, pc.idx + 1);
         }
-        wave_lds_sync();
-    };
-    // IDCT of the staged task; kSplit converts each 64-px half of a full
-    // 4:4:4 strip right after its rounds (hook), edge strips after the IDCT
-    auto transform = [&](const TaskGeom& tg, uint8_t* fout, const FrameCursor& cc, bool full) {
-        auto hook = [&](int i) {
+
+        // HJD_PREFETCH_AT >= 0 (tuning): the next task's loads are issued after
+        // IDCT round HJD_PREFETCH_AT instead of before round 0
+        constexpr int kRows = KGeom<kSampling>::kMcuH;
+        constexpr int kStripW = KGeom<kSampling>::kStripW;
+        uint8_t* fout = out + cc.out_base;
+        const bool full = cc.vec_ok && tg.x_base + kStripW <= cc.width && tg.y_base + kRows <= cc.height;
+        constexpr bool kSplit = HJD_SPLIT444 != 0 && kSampling == 0 && (kVariant & (kAblNoColour | kAblNoIdct)) == 0;
+        auto late_prefetch = [&](int i) {
+            if constexpr (kFmt == 0 && HJD_PREFETCH_AT >= 0) {
+                if (i == HJD_PREFETCH_AT && next_task >= 0) {
+                    while (next_task >= pc.end) cursor_load(pc, frames, nframes, total_tasks, pc.idx + 1);
+                    prefetch(task_geom<kSampling>(pc, next_task));
+                }
+            }
             if constexpr (kSplit) {
                 if (full && (i == 2 || i == 5))
                     colour_half444<kVariant>(slots, lane, fout, cc.pitch, cc.width, tg.y_base, tg.x_base, i == 5 ? 1 : 0);
@@ -984,73 +993,24 @@ __global__ __launch_bounds__(kGroupThreads, KLayout<kSampling>::min_waves) void 
         };
         if constexpr ((kVariant & kAblNoIdct) == 0)
             idct_stage<kSampling, kFmt, kVariant>(slots, rowbuf, lane, zoff, q, qlds,
-                                                  static_cast<const int*>(coefs) + tg.blk0 * 64, tg.nblk, hook,
-                                                  slots_lds);
-    };
+                                        static_cast<const int*>(coefs) + tg.blk0 * 64, tg.nblk, late_prefetch,
+                                        slots_lds);
+        else
+            late_prefetch(HJD_PREFETCH_AT);
 
-    // Full strips, in order, with the next full strip's coefficients loading
-    // during this one.  Edge strips (right column and bottom row of frames
-    // whose size is not a strip multiple, or frames whose rows are not
-    // 16-byte aligned) are left to the second loop below: with the guarded
-    // edge colour path inside this loop, the compiler's waitcnt pass cannot
-    // prove that a full strip's stores were issued after the prefetch on
-    // every path to the loop head, and waits vmcnt(0) there -- for the
-    // previous strip's stores as well.  Without it the wait is vmcnt(stores
-    // per strip) and those stores drain while the next strip computes.
-    int64_t task = next_full(t_begin);
-    if constexpr (kFmt == 0) {
-        if (task >= 0) {
-            prefetch(task_geom<kSampling>(pc, task));
-            // the first task's table rows load beside its coefficients, so a
-            // wave start waits for one memory round trip, not two
-            if constexpr (!L::t2) {
-                q_tables[0] = pc.qt0; q_tables[1] = pc.qt1; q_tables[2] = pc.qt2;
-#pragma unroll
-                for (int c = 0; c < 3; ++c) load_qrow_pk(qt_pool, q_tables[c], r, q[c]);
-            }
-        }
-        // drained here, so that the loop head's wait is counted from the
-        // loop's own stores on every path into it
-        __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0)
-    }
-    for (int64_t next_task; task >= 0; task = next_task) {
-        const FrameCursor cc = pc;
-        const TaskGeom tg = task_geom<kSampling>(cc, task);
-        next_task = next_full(task + t_step);   // -1: this is the wave's last full strip
-        if constexpr (kFmt == 0) {
-            stage(cc);
-            if (next_task >= 0) prefetch(task_geom<kSampling>(pc, next_task));
-        }
-        uint8_t* fout = out + cc.out_base;
-        transform(tg, fout, cc, true);
         if constexpr ((kVariant & kAblNoColour) != 0) {
             (void)fout;
-        } else if constexpr (!kSplit) {
-            colour_stage<kSampling, true, kVariant>(slots, lane, fout, cc.pitch, cc.width, cc.height, tg.y_base,
-                                                    tg.x_base);
+        } else if (kSplit && full) {
+            // converted inside the IDCT stage (late_prefetch hook)
+        } else if (full)
+            colour_stage<kSampling, true, kVariant>(slots, lane, fout, cc.pitch, cc.width, cc.height, tg.y_base, tg.x_base);
+        else {
+            colour_stage<kSampling, false, kVariant>(slots, lane, fout, cc.pitch, cc.width, cc.height, tg.y_base, tg.x_base);
+            // Edge strips issue a data-dependent number of stores; drain them
+            // here so the loop head's wait for the prefetched coefficients can
+            // be a fixed vmcnt (the full path's stores may stay in flight).
+            __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0)
         }
-        wave_lds_sync();
-    }
-
-    // Edge strips of this wave's sequence (none in frames whose size is a
-    // strip multiple): loaded when reached, guarded per-pixel stores.
-    cursor_seek(pc, frames, nframes, total_tasks, t_begin);
-    for (int64_t t = t_begin; t < t_end; t += t_step) {
-        while (t >= pc.end) cursor_load(pc, frames, nframes, total_tasks, pc.idx + 1);
-        const FrameCursor cc = pc;
-        const TaskGeom tg = task_geom<kSampling>(cc, t);
-        if (is_full(cc, tg)) continue;
-        if constexpr (kFmt == 0) {
-            prefetch(tg);
-            stage(cc);
-        }
-        uint8_t* fout = out + cc.out_base;
-        transform(tg, fout, cc, false);
-        if constexpr ((kVariant & kAblNoColour) != 0)
-            (void)fout;
-        else
-            colour_stage<kSampling, false, kVariant>(slots, lane, fout, cc.pitch, cc.width, cc.height, tg.y_base,
-                                                     tg.x_base);
         wave_lds_sync();
     }
 }
