@@ -24,6 +24,7 @@ import os
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNELS = {"4k420": "hjd::decode_kernel<1,", "4k444": "hjd::decode_kernel<0,"}   # matched without spaces
+# (the product's exact instantiation is picked per workload from the bench line's launch variant)
 PEAK = 8000.0
 
 
@@ -51,17 +52,36 @@ def main():
     out = {"name": args.name, "command": args.command, "source_dir": os.path.relpath(args.dir, REPO),
            "warmup": args.warmup, "steps": args.steps, "workloads": {}}
     n = args.warmup + args.steps
+    clocks = [s for s, e, k in rows if "clock_probe_kernel" in k]
     for wl, key in KERNELS.items():
-        d = [(e - s) / 1e6 for s, e, k in rows if key in k.replace(" ", "")][:n]
+        src = (line if wl == "4k420" else (line or {}).get("config4_444")) or {}
+        var = (src.get("launch") or {}).get("variant") or 0
+        # the product's instantiation: launch variant bits, + the d16 gather bit
+        # at 4:4:4 when the trace has it (hjd_runtime.hip launch_decode)
+        names = {k.replace(" ", "") for _s, _e, k in rows}
+        inst = f"{key}0,{var}>"
+        d16 = f"{key}0,{var | 128}>"
+        if any(d16 in nm for nm in names):
+            inst = d16
+        ds = [(s, e) for s, e, k in rows if inst in k.replace(" ", "")]
+        if not ds:
+            continue
+        # the bench's own launches come before its clock probe (bench.py pixel_batch:
+        # autotune, warmup + timed, then clock_under_load, stage variants, ceiling):
+        # the W + K dispatches right before the first clock probe after this
+        # workload's first dispatch (all of them when no probe ran)
+        stop = next((c for c in clocks if c > ds[0][0]), None)
+        before = [(s, e) for s, e in ds if stop is None or s < stop]
+        d = [(e - s) / 1e6 for s, e in before[-n:]]
         if len(d) < n:
             continue
         timed = d[args.warmup:]
-        e = {"kernel": key + "...>", "frames_per_launch": args.frames, "dispatch_ms": [round(x, 6) for x in d],
+        e = {"kernel": inst, "frames_per_launch": args.frames, "dispatch_ms": [round(x, 6) for x in d],
+             "dispatches_of_kernel_before_timed": len(before) - n,
              "warmup_dispatches": args.warmup, "timed_dispatches": len(timed),
              "timed_mean_ms": round(sum(timed) / len(timed), 6), "timed_min_ms": round(min(timed), 6),
              "timed_max_ms": round(max(timed), 6)}
         if line:
-            src = line if wl == "4k420" else (line.get("config4_444") or {})
             rf = src.get("roofline") or {}
             if rf:
                 algo = rf["algorithmic_bytes_per_launch"]
