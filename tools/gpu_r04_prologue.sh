@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 4 session prologue (VERDICT r3 "Next" #1): the pixel bench on whatever
 # box this is (autotuned launch, same-run stages, box ceiling, clock), and --
-# if its 4:2:0 line shows the slow-box drop (frac <= 0.78) -- the slow-box
+# if its 4:2:0 line shows the slow-box drop (frac <= 0.79) -- the slow-box
 # capture in the same session: box probe (rw-mix rates incl. write-only),
 # tasks-per-wave x store-policy sweep of the product and its memory-only
 # variant, TCC write / DRAM-credit counters, smi under load, kernel trace.
@@ -24,7 +24,7 @@ for n, x in (("420", d), ("444", c)):
           (x.get("launch") or {}).get("stores"), "memonly_ms", (x.get("stages") or {}).get("memory_only_ms"),
           "prod_ms", (x.get("stages") or {}).get("product_ms"), file=sys.stderr)
 print("box", d["box"], file=sys.stderr)
-print(1 if d["roofline"]["frac"] <= 0.78 else 0)
+print(1 if d["roofline"]["frac"] <= 0.79 else 0)
 PY
 )
 if [ "$SLOW" = "1" ]; then
