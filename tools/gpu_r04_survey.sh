@@ -9,8 +9,8 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/${1:-r04s}
 mkdir -p $O
 cd $R
-timeout -k 10 300 python -u bench.py --no-stream --no-cpu --no-fhd > $O/bench_quick.json 2> $O/bench_quick.err \
-    || { echo QUICK BENCH FAILED; tail -20 $O/bench_quick.err; exit 1; }
+timeout -k 10 300 python -u bench.py --no-stream --no-cpu --no-fhd > $O/survey_bench.json 2> $O/survey_bench.err \
+    || { echo QUICK BENCH FAILED; tail -20 $O/survey_bench.err; exit 1; }
 cd /tmp && export TMPDIR=/tmp
 for wl in 4k420 4k444; do
   timeout -s KILL 180 rocprofv3 -i $R/tools/pmc_tcc_write.txt --output-format csv -d $O/tcc_$wl -o tcc -- \
@@ -22,7 +22,7 @@ timeout -k 10 300 python -u tools/box_probe.py > $O/box_probe.json 2> $O/box_pro
 python3 - $O <<'PY'
 import json, sys, subprocess
 o = sys.argv[1]
-b = json.load(open(f"{o}/bench_quick.json"))
+b = json.load(open(f"{o}/survey_bench.json"))
 print("box", b["box"].get("serial"))
 for wl, x, k, t in (("4k420", b, "decode_kernel<1,0,0>", 1036800), ("4k444", b["config4_444"], "decode_kernel<0,0,128>", 2073600)):
     s = x["stages"]
