@@ -50,8 +50,20 @@ def main():
             if l.startswith("{"):
                 line = json.loads(l)
     out = {"name": args.name, "command": args.command, "source_dir": os.path.relpath(args.dir, REPO),
-           "warmup": args.warmup, "steps": args.steps, "workloads": {}}
-    n = args.warmup + args.steps
+           "warmup": args.warmup, "steps": args.steps,
+           "workloads": split(rows, line, args.warmup, args.steps, args.frames)}
+    dst = os.path.join(REPO, "profiles", f"{args.name}_dispatch.json")
+    with open(dst, "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps({k: {kk: vv for kk, vv in v.items() if kk != "dispatch_ms"} for k, v in out["workloads"].items()},
+                     indent=1))
+
+
+def split(rows, line, warmup, steps, frames):
+    """{workload: summary} from (start, end, kernel name) dispatch rows sorted by
+    start and the bench line of the traced run (None if absent)."""
+    workloads = {}
+    n = warmup + steps
     clocks = [s for s, e, k in rows if "clock_probe_kernel" in k]
     for wl, key in KERNELS.items():
         src = (line if wl == "4k420" else (line or {}).get("config4_444")) or {}
@@ -75,10 +87,10 @@ def main():
         d = [(e - s) / 1e6 for s, e in before[-n:]]
         if len(d) < n:
             continue
-        timed = d[args.warmup:]
-        e = {"kernel": inst, "frames_per_launch": args.frames, "dispatch_ms": [round(x, 6) for x in d],
+        timed = d[warmup:]
+        e = {"kernel": inst, "frames_per_launch": frames, "dispatch_ms": [round(x, 6) for x in d],
              "dispatches_of_kernel_before_timed": len(before) - n,
-             "warmup_dispatches": args.warmup, "timed_dispatches": len(timed),
+             "warmup_dispatches": warmup, "timed_dispatches": len(timed),
              "timed_mean_ms": round(sum(timed) / len(timed), 6), "timed_min_ms": round(min(timed), 6),
              "timed_max_ms": round(max(timed), 6)}
         if line:
@@ -90,12 +102,8 @@ def main():
                 e["frac_from_timed_dispatches"] = round(algo / (e["timed_mean_ms"] / 1e3) / 1e9 / PEAK, 4)
                 e["bench_ms_per_step_same_run"] = src.get("ms_per_step")
                 e["bench_value_same_run"] = src.get("value")
-        out["workloads"][wl] = e
-    dst = os.path.join(REPO, "profiles", f"{args.name}_dispatch.json")
-    with open(dst, "w") as f:
-        json.dump(out, f, indent=1)
-    print(json.dumps({k: {kk: vv for kk, vv in v.items() if kk != "dispatch_ms"} for k, v in out["workloads"].items()},
-                     indent=1))
+        workloads[wl] = e
+    return workloads
 
 
 if __name__ == "__main__":
