@@ -30,6 +30,12 @@ def row(o):
                    "rd_credit_stall_per_cycle": d.get("TCC_EA0_RDREQ_DRAM_CREDIT_STALL_per_cycle"),
                    "profiled_clock_GHz": d.get("effective_clock_GHz")}
     out["probe_GBps"] = json.load(open(os.path.join(o, "box_probe.json"))).get("best_GBps_nt_xcd")
+    pro = os.path.join(o, "bench_quick.json")   # the prologue's bench, an earlier process of the same call
+    if bpath != pro and os.path.exists(pro):
+        p = json.load(open(pro))
+        out["prologue_process"] = {wl: {"frac": x["roofline"]["frac"], "product_ms": x["stages"]["product_ms"],
+                                        "memory_only_ms": x["stages"]["memory_only_ms"]}
+                                   for wl, x in (("4k420", p), ("4k444", p["config4_444"]))}
     return out
 
 
