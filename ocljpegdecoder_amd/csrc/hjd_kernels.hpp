@@ -821,6 +821,9 @@ __device__ __forceinline__ void idct_stage(char* __restrict__ slots, char* __res
 #ifndef HJD_PREFETCH_AT
 #define HJD_PREFETCH_AT -1   // tuning: issue the next task's loads after IDCT round N (-1: before round 0)
 #endif
+#ifndef HJD_XCD_SPLIT
+#define HJD_XCD_SPLIT 1   // tuning: parts each XCD's eighth is walked in concurrently
+#endif
 #ifndef HJD_XCD_CHUNK
 #define HJD_XCD_CHUNK 0
 #endif
@@ -837,6 +840,14 @@ __device__ __forceinline__ uint32_t group_order(uint32_t bid, uint32_t ngroups)
         return bid;
     } else if constexpr (HJD_XCD_CHUNK == 0) {
         const uint32_t x = bid & 7, k = bid >> 3, q = ngroups >> 3, rem = ngroups & 7;
+        if constexpr (HJD_XCD_SPLIT > 1) {
+            // the XCD's eighth in HJD_XCD_SPLIT contiguous parts, consecutive
+            // dispatches going to different parts (a bijection on the eighth)
+            constexpr uint32_t S = HJD_XCD_SPLIT;
+            const uint32_t n = q + (x < rem ? 1u : 0u);
+            const uint32_t p = k % S, j = k / S, ps = n / S, pr = n % S;
+            return x * q + min(x, rem) + p * ps + min(p, pr) + j;
+        }
         return x * q + min(x, rem) + k;
     } else {
         constexpr uint32_t C = HJD_XCD_CHUNK;
