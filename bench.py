@@ -85,8 +85,9 @@ WORKLOADS = {
                                   desc="BASELINE configs[4] per GPU, D2H-on, BGR24 sink (SURVEY s8(f) rank 4): as "
                                        "stream4k420_d2h with 3-byte pixels copied back"),
     "stream4k420_host": dict(width=3840, height=2160, sampling=1, frames=128, entropy="host",
-                             desc="BASELINE configs[4] per GPU, host-Huffman variant: host Huffman workers || "
-                                  "pinned H2D || fused kernel"),
+                             desc="BASELINE configs[4] per GPU as north_star names it: host Huffman workers "
+                                  "(jpeg_host.cpp) -> pinned int16 coefficient slots -> hipMemcpyAsync on a copy "
+                                  "stream || fused kernel on a compute stream"),
 }
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 POOL = 8
@@ -605,6 +606,20 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
     wall, wall_max = timed_region(dist, world, body, torch.cuda.synchronize)   # max over ranks
     before, after = stats["before"], stats["after"]
     host_ns = after[stat_key] - before[stat_key]
+    busy = None
+    if not gpu_entropy:
+        # the pipeline's overlap, this rank: how much of the wall time the copy
+        # engine and the kernel were busy (HIP timing events around every
+        # upload and launch, hjd_stream_busy), and the bytes moved
+        h2d_b = after["h2d_bytes"] - before["h2d_bytes"]
+        busy = {"h2d_GBps": round(h2d_b / wall / 1e9, 2),
+                "h2d_busy_frac": round((after["h2d_busy_ns"] - before["h2d_busy_ns"]) / 1e9 / wall, 4),
+                "kernel_busy_frac": round((after["kernel_busy_ns"] - before["kernel_busy_ns"]) / 1e9 / wall, 4),
+                "kernel_us_per_frame": round((after["kernel_busy_ns"] - before["kernel_busy_ns"]) / 1e3 /
+                                             max(1, after["kernel_launches"] - before["kernel_launches"]), 2),
+                "host_threads": nthreads,
+                "host_huffman_Mpx_per_core_s": round(nf * args.steps * w * h / (host_ns / 1e9) / 1e6, 1)
+                if host_ns else None}
     host_scan = after.get("host_scan_bytes", 0) - before.get("host_scan_bytes", 0)
     px = nf * w * h * args.steps * world
 
@@ -687,6 +702,7 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
                     "how": "device -> pinned host copies on this GPU after the timed region, as the stream "
                            "returns frames: 2, 4 and the stream's slot count of concurrent streams, one frame's "
                            "output per copy (plus one stream of 256 MiB copies); the best rate is the ceiling"},
+                "pipeline": busy,
                 "output_checked_vs_oracle": bool(ok)},
             "hbm_at_start": {"wait_s_max_over_ranks": round(released["hbm_wait_s"], 2),
                              "busy_GiB_max_over_ranks": round(released["hbm_busy_GiB"], 2),
@@ -1154,6 +1170,91 @@ def pixel_batch(args, wl, hjd, torch, dist, world, rank, dev, qt, steps, warmup,
             "_bytes_per_launch": bytes_per_launch, "_tasks": tasks}
 
 
+def _leg_summary(leg):
+    """One leg of the compact line: its headline number, time, roofline
+    fraction, same-run ceiling fraction and oracle check."""
+    if not leg:
+        return None
+    if "error" in leg:
+        return {"error": str(leg["error"])[:60]}
+    r = {"Mpx_s": leg.get("value"), "ms": leg.get("ms_per_step")}
+    rf = leg.get("roofline")
+    if rf:
+        r["frac"] = rf.get("frac")
+        r["box_frac"] = rf.get("frac_of_box_ceiling")
+    r["ok"] = leg.get("output_checked_vs_oracle")
+    return r
+
+
+def _stream_summary(leg, ceiling_key=None):
+    if not leg or "error" in leg:
+        return _leg_summary(leg)
+    r = {"Mpx_s": leg["value"], "frame_ids": leg["timed_frame_ids"]}
+    c = leg.get(ceiling_key) if ceiling_key else None
+    if c:
+        r[ceiling_key.split("_")[0] + "_frac"] = c["frac"]
+    p = leg.get("pipeline")
+    if p:
+        r.update({"host_Mpx_s_per_core": p["host_huffman_Mpx_per_core_s"], "cores": p["host_threads"],
+                  "h2d_GBps": p["h2d_GBps"], "kernel_busy": p["kernel_busy_frac"], "h2d_busy": p["h2d_busy_frac"]})
+    r["ok"] = leg["output_checked_vs_oracle"]
+    return r
+
+
+def compact_line(res, detail_path):
+    """The stdout line: the driver keeps only the tail of stdout, so the line
+    stays short (~2 KB) and ends with `summary`, one entry per leg; the full
+    result goes to `detail_path` and stderr (emit)."""
+    rf = res["roofline"]
+    cpu = res.get("cpu_baseline") or {}
+    c4, f1, fj = res.get("config4_444"), res.get("fhd420"), res.get("fhd420_jpeg")
+    ref = res.get("cpu_reference") or {}
+    summary = {
+        "4k420": _leg_summary(res),
+        "4k444": _leg_summary(c4),
+        "fhd420_us_per_launch": f1 and {"us": f1["us_per_launch_kernel"], "ok": f1["output_checked_vs_oracle"]},
+        "fhd420_jpeg_ms_per_image": fj and {"ms": fj["ms_per_image"], "ok": fj["output_checked_vs_oracle"]},
+        "c5_gpu_huffman": _stream_summary(res.get("config5_stream"), "h2d_ceiling"),
+        "c5_host_huffman": _stream_summary(res.get("config5_stream_host")),
+        "c5_d2h": _stream_summary(res.get("config5_stream_d2h"), "d2h_ceiling"),
+        "cpu_port": cpu.get("value") and {"Mpx_s": cpu["value"], "cores": cpu["cores"]},
+        "cpu_reference": ref.get("value") and {"Mpx_s": ref["value"], "cores": ref.get("cores")},
+    }
+    oks = [v.get("ok") for v in summary.values() if isinstance(v, dict) and "ok" in v]
+    keep = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype")
+    line = {k: res[k] for k in keep}
+    line["data"] = "synthetic, resident in HBM"
+    cfg = res["config"]
+    line["config"] = {"workload": "configs[2]: %d x %dx%d %s, int16 zigzag in, %s" % (
+        cfg["frames_per_gpu"], cfg["width"], cfg["height"], cfg["sampling"],
+        "BGRX out" if "BGRX" in cfg["output"] else "BGR24 out"), "parallelism": cfg["parallelism"]}
+    line["roofline"] = {k: rf.get(k) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic",
+                                                "algorithmic_bytes_per_launch", "kernel_ms_per_launch",
+                                                "frac_of_box_ceiling")}
+    line["cpu_baseline"] = cpu and {k: cpu.get(k) for k in ("value", "unit", "cores", "kind")}
+    if cpu:
+        line["cpu_baseline"]["sample"] = cpu.get("sample", "")[:60]
+    line["output_checked_vs_oracle"] = all(o is not False for o in oks)
+    line["detail"] = detail_path
+    line["summary"] = summary
+    return line
+
+
+def emit(res, detail_path):
+    """Full result to `detail_path` (and stderr), compact line to stdout."""
+    full = json.dumps(res)
+    try:
+        d = os.path.dirname(os.path.abspath(detail_path))
+        os.makedirs(d, exist_ok=True)
+        with open(detail_path, "w") as f:
+            f.write(full + "\n")
+    except OSError as e:
+        log(f"could not write {detail_path}: {e}")
+    log("BENCH_DETAIL " + full)
+    print(json.dumps(compact_line(res, detail_path)), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -1175,6 +1276,13 @@ def main():
                     help="4k420: skip the configs[3] 4:4:4 batch reported under config4_444")
     ap.add_argument("--stream-frame-ids", type=int, default=100000,
                     help="config-5 stream leg: global frame ids to cover (BASELINE configs[4]: 100k images)")
+    ap.add_argument("--stream-host-frame-ids", type=int, default=10240,
+                    help="config-5 host-Huffman leg (config5_stream_host): global frame ids to cover")
+    ap.add_argument("--no-stream-host", action="store_true",
+                    help="skip the host-Huffman config-5 leg (config5_stream_host)")
+    ap.add_argument("--detail-out", default=os.path.join("gpurun_out", "bench_detail.json"),
+                    help="where the full result (every leg's measurements and how they were taken) is written; "
+                         "stdout carries the compact line")
     ap.add_argument("--no-stream", action="store_true",
                     help="N=1 pixel workloads: skip the config-5 stream leg (a child bench.py run, reported "
                          "under config5_stream)")
@@ -1264,13 +1372,16 @@ def main():
         if world == 1 and not args.no_cpu:
             log("running CPU baseline leg ...")
             cpu = cpu_baseline(pool_host, qt, wl, value)
-        stream5 = stream5_d2h = None
+        stream5 = stream5_d2h = stream5_host = None
         if not args.no_stream and args.workload == "4k420":
             torch.cuda.synchronize()
             torch.cuda.empty_cache()
             if world > 1:
                 dist.destroy_process_group()   # the other ranks are leaving; the child run has its own group
             stream5 = config5_stream_leg(world, args.dist_backend, args.stream_frame_ids)
+            if not args.no_stream_host:
+                stream5_host = config5_stream_leg(world, args.dist_backend, args.stream_host_frame_ids,
+                                                  workload="stream4k420_host")
             if not args.no_d2h:
                 stream5_d2h = config5_stream_leg(world, args.dist_backend, args.stream_frame_ids,
                                                  workload="stream4k420_d2h")
@@ -1306,13 +1417,14 @@ def main():
             "device_copy_GBps": res_px["device_copy_GBps"],
             "config4_444": config4,
             "config5_stream": stream5,
+            "config5_stream_host": stream5_host,
             "config5_stream_d2h": stream5_d2h,
             "fhd420": fhd,
             "fhd420_jpeg": fhd_jpeg,
         }
         if cpu and "reference" in cpu:
             res["cpu_reference"] = cpu.pop("reference")
-        print(json.dumps(res), flush=True)
+        emit(res, args.detail_out)
     if world > 1 and dist.is_initialized():
         dist.destroy_process_group()
     if not checked_all_ok:
@@ -1407,6 +1519,8 @@ def config5_stream_leg(world, dist_backend, frame_ids=100000, workload="stream4k
             "jpeg_GBps_in": d["end_to_end"]["jpeg_GBps_in"], "destuff": d["end_to_end"]["destuff"],
             "h2d_ceiling": d["end_to_end"].get("h2d_ceiling"),
             "d2h_ceiling": d["end_to_end"].get("d2h_ceiling"),
+            "pipeline": d["end_to_end"].get("pipeline"),
+            "host_threads_per_gpu": d["config"]["host_threads_per_gpu"],
             "output": d["config"]["output"],
             "output_checked_vs_oracle": d["end_to_end"]["output_checked_vs_oracle"],
             "steps_checked": d["stream_check"]["steps_checked"],

@@ -129,9 +129,11 @@ int hjd_plan_destroy(hjd_plan* plan);
  * Results are identical for every variant. */
 int hjd_plan_set_variant(hjd_plan* plan, int variant);
 int hjd_plan_set_kernel(hjd_plan* plan, int mode);   /* hjd_kernel_mode */
-/* Pin the persistent kernel's task chunk without hjd_plan_autotune: `tasks`
- * consecutive tasks per wave (1..4096; 0 restores the shape default).
- * Identical pixels either way. */
+/* Pin the persistent kernel's task chunk without hjd_plan_autotune: exactly
+ * `tasks` consecutive tasks per wave (1..4096, no occupancy floor; 0 restores
+ * the shape default, which never drops below ~4 waves per SIMD).  Applies to
+ * launches that take the persistent kernel: an HJD_KERNEL_AUTO plan small
+ * enough for the latency kernel keeps it.  Identical pixels either way. */
 int hjd_plan_set_chunk(hjd_plan* plan, int tasks);
 int64_t hjd_plan_tasks(const hjd_plan* plan);      /* work items (strips) */
 int64_t hjd_plan_pixels(const hjd_plan* plan);     /* visible pixels */
@@ -157,11 +159,29 @@ int hjd_plan_launch(hjd_plan* plan, const void* d_coefs, void* d_out, void* stre
  * interleaved rounds (0 = 2) of one warm and two timed launches each, and
  * keeps the fastest for the plan's later launches with grid_blocks = 0.
  * Every candidate writes identical pixels (d_out holds a valid decode on
- * return).  Plans the latency kernel serves are left unchanged.  Optional
+ * return unless the choice came from the cache, below).  Plans the latency
+ * kernel serves are left unchanged.  Optional
  * outputs: the chosen tasks per wave (0 = unchanged) and the variant bits.
  */
 int hjd_plan_autotune(hjd_plan* plan, const void* d_coefs, void* d_out, void* stream, int rounds,
                       int32_t* tasks_per_wave, int32_t* variant);
+/* hjd_plan_autotune's choice is cached per process (device x sampling x
+ * input format x output format x the other variant bits x floor(log2 tasks)):
+ * a later plan of the same key takes it with no launch (and d_out is then NOT
+ * written).  HJD_AUTOTUNE_CACHE=0 disables the cache; this empties it. */
+int hjd_autotune_cache_clear(void);
+
+/* The launch shape a plan's next hjd_plan_launch(grid_blocks = 0) uses. */
+typedef struct hjd_launch_shape {
+    int32_t kernel;             /* HJD_KERNEL_PERSISTENT or HJD_KERNEL_LATENCY */
+    int32_t tasks_per_wave;     /* persistent: the chunk asked for (pinned, tuned or the shape default) */
+    int32_t max_tasks_per_wave; /* persistent: the most tasks one wave takes with that grid */
+    int32_t grid;               /* workgroups (latency: one per task) */
+    int32_t variant;            /* variant bits */
+    int32_t autotune_launches;  /* kernel launches the last hjd_plan_autotune made (0: none or cached) */
+    int32_t autotune_cached;    /* 1: the last hjd_plan_autotune reused a cached choice */
+} hjd_launch_shape;
+int hjd_plan_launch_shape(const hjd_plan* plan, hjd_launch_shape* out);
 
 /* IDCT only (the reference's batch_idct, src/idct8x8.cl:157-166), out of
  * place: int32 natural-order dequantised blocks -> int32 samples [-256,255]. */
@@ -219,9 +239,10 @@ int hjd_debug_clock_probe(hjd_ctx* ctx, uint64_t* d_out, int nsamples, int inter
 
 /* The 4:4:4 kernels' d16 gather (ds_read_u16_d16_hi) is valid only where that
  * load zeroes the low half of its destination.  *probe_zeroes: the one-wave
- * hardware probe's answer for `device` (run once per device at first use;
- * HJD_D16_PROBE=fail forces 0); *selected: whether the 4:4:4 launches take
- * the d16 kernels (the probe, unless HJD_D16=0/1 overrides it). */
+ * hardware probe's answer for `device` (hjd_ctx_create runs it; a completed
+ * run is cached per device, a failed one reads 0 and is retried; HJD_D16_PROBE=
+ * fail forces 0); *selected: whether the 4:4:4 launches take the d16 kernels
+ * (the cached probe passed, and HJD_D16 is not 0). */
 int hjd_debug_d16_gather(int device, int* probe_zeroes, int* selected);
 
 #ifdef __cplusplus

@@ -82,6 +82,12 @@ int hjd_stream_submit(hjd_stream* s, const uint8_t* data, size_t size, void* d_o
 /* Wait for every submitted image; returns the first error, if any.  stats (may
  * be NULL) receives {images, pixels, host_decode_ns, h2d_bytes, kernel_launches}. */
 int hjd_stream_sync(hjd_stream* s, int64_t stats[5]);
+/* Cumulative GPU-side busy time of the stream's jobs, complete as of the last
+ * hjd_stream_sync: the sum of every upload's duration on the copy stream and
+ * of every fused-kernel launch on the compute stream (HIP timing events).
+ * Divided by a wall-clock interval it is the fraction of the time the host
+ * Huffman workers kept the copy engine / the kernel fed. */
+int hjd_stream_busy(hjd_stream* s, int64_t* h2d_busy_ns, int64_t* kernel_busy_ns);
 /* Pixel format of subsequent submits: HJD_OUT_BGRX (default) or HJD_OUT_BGR24
  * (d_out 4-byte aligned, pitch >= 3*width); jobs already queued keep theirs. */
 int hjd_stream_set_output_format(hjd_stream* s, int out_format);

@@ -32,6 +32,12 @@ class HjdFrame(ctypes.Structure):
 assert ctypes.sizeof(HjdFrame) == 48
 
 
+class HjdLaunchShape(ctypes.Structure):
+    """struct hjd_launch_shape (include/hjd.h)."""
+    _fields_ = [(n, ctypes.c_int32) for n in ("kernel", "tasks_per_wave", "max_tasks_per_wave", "grid", "variant",
+                                              "autotune_launches", "autotune_cached")]
+
+
 class HjdJpegInfo(ctypes.Structure):
     """struct hjd_jpeg_info (include/hjd_host.h)."""
     _fields_ = [
@@ -73,6 +79,8 @@ SIGNATURES = {
                                        ctypes.c_int]),
     "hjd_plan_autotune": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.c_int, c_i32p, c_i32p]),
+    "hjd_autotune_cache_clear": (ctypes.c_int, []),
+    "hjd_plan_launch_shape": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HjdLaunchShape)]),
     "hjd_idct_blocks": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                        ctypes.c_void_p]),
     "hjd_debug_csc": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
@@ -145,6 +153,7 @@ def _bind_host(lib):
         "hjd_stream_destroy": (ctypes.c_int, [vp]),
         "hjd_stream_submit": (ctypes.c_int, [vp, u8p, ctypes.c_size_t, vp, ctypes.c_int32]),
         "hjd_stream_sync": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int64)]),
+        "hjd_stream_busy": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
         "hjd_gdec_create": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
                                            ctypes.POINTER(vp)]),
         "hjd_gdec_destroy": (ctypes.c_int, [vp]),

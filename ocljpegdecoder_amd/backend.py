@@ -248,6 +248,15 @@ class Plan:
                                          ctypes.byref(var)), "hjd_plan_autotune")
         return tpw.value, var.value
 
+    def launch_shape(self) -> dict:
+        """hjd_plan_launch_shape: the shape the next default launch uses, and
+        what the last autotune did (launches made, cache hit)."""
+        r = _lib.HjdLaunchShape()
+        check(self.lib.hjd_plan_launch_shape(self.handle, ctypes.byref(r)), "hjd_plan_launch_shape")
+        d = {n: getattr(r, n) for n, _ in r._fields_}
+        d["kernel"] = {KERNEL_PERSISTENT: "persistent", KERNEL_LATENCY: "latency"}.get(d["kernel"], d["kernel"])
+        return d
+
     def launch_stages(self, stages: int, coefs, out, stream=None, grid_blocks: int = 0):
         """Timing-only launch with kernel stages skipped (hjd_debug_plan_launch_stages;
         80 memory only, 4 no stores, ...): the output is WRONG by design."""
@@ -267,6 +276,11 @@ class Plan:
             self.close()
         except Exception:
             pass
+
+
+def autotune_cache_clear():
+    """Forget every cached hjd_plan_autotune choice of this process."""
+    check(_lib.load().hjd_autotune_cache_clear(), "hjd_autotune_cache_clear")
 
 
 def decode_frame(ctx: Context, coefs, qt: np.ndarray, width: int, height: int, sampling: int,

@@ -94,11 +94,16 @@ int parse_scan_headers(const uint8_t* data, size_t size, std::vector<ScanHeader>
 // hjd_ctx accessors for the other translation units
 int ctx_num_cu(const struct ::hjd_ctx* ctx);
 
-// d16 gather (hjd_probe.hip): 1 if ds_read_u16_d16_hi zeroes the low half of
-// its destination on `device` (one-wave probe, run once per device and
-// cached; HJD_D16_PROBE=fail forces 0).  d16_gather_selected(): whether the
-// 4:4:4 launches take the kVarD16 kernels (the probe, or HJD_D16=0/1).
+// d16 gather (hjd_probe.hip): d16_probe() is 1 if ds_read_u16_d16_hi zeroes
+// the low half of its destination on `device` (one-wave probe; a completed run
+// is cached per device, a failed one returns 0 and is retried next time;
+// HJD_D16_PROBE=fail forces 0).  hjd_ctx_create runs it.  d16_probe_cached()
+// never runs it: the cached answer, or -1.  d16_gather_selected(): whether
+// the 4:4:4 launches take the kVarD16 kernels (the cached probe passed and
+// HJD_D16 is not 0); a launch never runs the probe itself, so it stays legal
+// inside stream capture.
 int d16_probe(int device);
+int d16_probe_cached(int device);
 bool d16_gather_selected(int device);
 
 }  // namespace hjd_internal

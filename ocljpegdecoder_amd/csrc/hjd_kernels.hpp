@@ -27,22 +27,14 @@ constexpr int kRowStride = 48;       // transpose buffer: bytes per row (b128 ro
 constexpr int kRowBufBlock = 416;    // transpose buffer: bytes per block (104 dwords = 8 mod 32 banks)
 constexpr int kWavesPerGroup = 4;
 constexpr int kGroupThreads = 64 * kWavesPerGroup;
-#ifndef HJD_T2
-#define HJD_T2 0
-#endif
 
-// Per-wave LDS layout of the fused kernel.  Default: 48 block slots plus a
-// transpose buffer (10240 B, 4 waves per SIMD).  t2 (HJD_T2, 4:4:4): the
-// row->column transpose goes through the round's own block slot (its
-// coefficients are already gathered) in two halves, and the lane rows of the
-// three dequant tables live in LDS (384 B) instead of 12 VGPRs, so a wave needs
-// 7296 B and <= 96 VGPRs: 5 waves per SIMD.
-template <int kSampling>
+// Per-wave LDS layout of the fused kernel: 48 block slots plus a transpose
+// buffer (10240 B, 4 waves per SIMD).  A 5-wave layout (transpose through the
+// round's own slot, tables in LDS) measured -1.0 % at 4:4:4 and was removed
+// (DESIGN.md s3.4).
 struct KLayout {
-    static constexpr bool t2 = HJD_T2 != 0 && kSampling == 0;
-    static constexpr int q_lds = 3 * 8 * 16;
-    static constexpr int wave_lds = kTaskBlocks * kSlotBytes + (t2 ? q_lds : 8 * kRowBufBlock);
-    static constexpr int min_waves = t2 ? 5 : 4;
+    static constexpr int wave_lds = kTaskBlocks * kSlotBytes + 8 * kRowBufBlock;
+    static constexpr int min_waves = 4;
     static_assert(kWavesPerGroup * wave_lds * min_waves <= 160 * 1024, "the groups per CU must fit the 160 KiB LDS");
 };
 
@@ -182,8 +174,9 @@ constexpr int kVarPlainStores = 1;
 // 4q + w of the group's contiguous quad range) instead of one contiguous range
 // per wave: the group's 4 waves then write adjacent 512-byte row segments.
 constexpr int kVarWgInterleave = 2;
-// Ablation bits: compiled into the tuning-only library (HJD_ABLATION, see
-// tools/build_native.py --ablation); their outputs are deliberately wrong.
+// Ablation bits: the stage-skipping measurement variants behind
+// hjd_debug_plan_launch_stages (bench.py stage_times); their outputs are
+// deliberately wrong.
 constexpr int kAblNoStore = 4, kAblNoColour = 8, kAblNoIdct = 16;
 // kAblNoCsc: the colour stage keeps its LDS reads and stores but skips the
 // chroma terms and pixel math (stores raw sample words).
@@ -507,45 +500,6 @@ __device__ __forceinline__ void colour_stage(const char* __restrict__ slots, int
     }
 }
 
-#ifndef HJD_SPLIT444
-#define HJD_SPLIT444 0   // tuning: 4:4:4 colour of each 64-px half right after its IDCT rounds
-#endif
-
-// 4:4:4 colour of one 64x8 half of a full strip (HJD_SPLIT444): lane = (4-px
-// column group cg = lane & 15, row lane >> 4); unit u covers rows 4u..4u+3, so
-// each wave store instruction writes four 256-byte row segments.
-template <int kVariant>
-__device__ __forceinline__ void colour_half444(const char* __restrict__ slots, int lane, uint8_t* __restrict__ out,
-                                               int pitch, int width, int y_base, int x_base, int half)
-{
-    constexpr int kPx = kOutBytes<kVariant>;
-    const int cg = lane & 15;
-    const int x0 = cg * 4;
-    const int m = half * 8 + (cg >> 1);
-    const int xm = x0 & 7;
-    const int rsub = lane >> 4;
-    const uint32_t loff = static_cast<uint32_t>(x0 * kPx) + static_cast<uint32_t>(rsub) * static_cast<uint32_t>(pitch);
-    uint8_t* const strip = out + static_cast<int64_t>(y_base) * pitch + static_cast<int64_t>(x_base + 64 * half) * kPx;
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-        const int y = 4 * u + rsub;
-        const char* base = slots + m * 3 * kSlotBytes + y * 16 + xm * 2;
-        const int2 sy = *reinterpret_cast<const int2*>(base);
-        const uint2 su = *reinterpret_cast<const uint2*>(base + kSlotBytes);
-        const uint2 sv = *reinterpret_cast<const uint2*>(base + 2 * kSlotBytes);
-        const ChromaTerms c0 = chroma_terms<0>(su.x, sv.x);
-        const ChromaTerms c1 = chroma_terms<1>(su.x, sv.x);
-        const ChromaTerms c2 = chroma_terms<0>(su.y, sv.y);
-        const ChromaTerms c3 = chroma_terms<1>(su.y, sv.y);
-        const ChromaPair p01 = pair_of(c0, c1), p23 = pair_of(c2, c3);
-        uint8_t* row = strip + static_cast<int64_t>(4 * u) * pitch;   // wave-uniform
-        if (__builtin_amdgcn_ballot_w64((p01.flagged | p23.flagged) != 0))
-            emit_row4<true, kVariant, true>(row, loff, x_base, width, sy.x, sy.y, p01, p23, &c0, &c1, &c2, &c3);
-        else
-            emit_row4<false, kVariant, true>(row, loff, x_base, width, sy.x, sy.y, p01, p23, &c0, &c1, &c2, &c3);
-    }
-}
-
 // Task-local block (= LDS slot) transformed by lane group g in round i.  The
 // mapping keeps each round's component uniform across the wave (dequant table
 // and luma level shift): 4:4:4 / 4:2:0 / gray blocks are MCU-interleaved with
@@ -566,10 +520,6 @@ __device__ __forceinline__ int round_block(int i, int g)
         }
         const int idx = (i - 3) * 8 + g;        // 0-11 Cb, 12-23 Cr
         return idx < 12 ? 4 * idx + 2 : 4 * (idx - 12) + 3;
-    } else if constexpr (kSampling == 0 && HJD_SPLIT444 != 0) {
-        // MCUs 0-7 (the strip's left 64 px) in rounds 0-2, MCUs 8-15 in rounds
-        // 3-5, so the left half's colour can run before rounds 3-5
-        return i < 3 ? 3 * g + i : 24 + 3 * g + (i - 3);
     } else {
         return 6 * g + i;
     }
@@ -618,21 +568,17 @@ __device__ __forceinline__ bool round_is_luma(int i)
 // the pairs (q0,q4), (q1,q7), (q3,q5), (q2,q6) (load_qrow_pk).
 template <int kSampling>
 __device__ __forceinline__ RowPk load_round_pk(const char* __restrict__ slots, int lane, int i, const int (&zoff)[8],
-                                               const uint32_t (&q)[3][4], const char* __restrict__ qlds)
+                                               const uint32_t (&q)[3][4])
 {
     const int g = lane >> 3;
     const int b = round_block<kSampling>(i, g);
     const int comp = round_component<kSampling>(i);
     const char* blk = slots + b * kSlotBytes;
-    uint4 ql = make_uint4(0, 0, 0, 0);
-    if constexpr (KLayout<kSampling>::t2)   // this lane's table row pairs from the wave's LDS copy
-        ql = *reinterpret_cast<const uint4*>(qlds + (comp >= 0 ? comp : (g < 4 ? 1 : 2)) * 128 + (lane & 7) * 16);
     auto pair = [&](int ca, int cb, int k) {
         const s16x2 c = {*reinterpret_cast<const short*>(blk + zoff[ca]),
                          *reinterpret_cast<const short*>(blk + zoff[cb])};
         // a mixed round (4:2:2 round 4) selects the table per lane
-        const uint32_t qq = KLayout<kSampling>::t2 ? (k == 0 ? ql.x : k == 1 ? ql.y : k == 2 ? ql.z : ql.w)
-                          : comp >= 0 ? q[comp < 0 ? 0 : comp][k] : (g < 4 ? q[1][k] : q[2][k]);
+        const uint32_t qq = comp >= 0 ? q[comp < 0 ? 0 : comp][k] : (g < 4 ? q[1][k] : q[2][k]);
         return c * __builtin_bit_cast(s16x2, qq);   // dequant (src/decoder.cpp:340)
     };
     RowPk p;
@@ -646,11 +592,10 @@ __device__ __forceinline__ RowPk load_round_pk(const char* __restrict__ slots, i
 // kVarD16 kernels (the runtime launches them on sramecc+ devices only, where
 // d16 LDS loads zero the other half): shapes whose round blocks are 6g + i
 // with a wave-uniform component (4:4:4, 4:2:0, 4:1:1, grayscale), staged
-// int16 (kFmt 0), default layout.  Instantiated for 4:4:4 (hjd_runtime.hip).
+// int16 (kFmt 0).  Instantiated for 4:4:4 (hjd_runtime.hip).
 template <int kSampling, int kFmt, int kVariant>
-constexpr bool kD16Gather = (kVariant & kVarD16) != 0 && kFmt == 0 && !KLayout<kSampling>::t2 &&
-                            (round_class(kSampling) == 0 || round_class(kSampling) == 1 || round_class(kSampling) == 3) &&
-                            !(kSampling == 0 && HJD_SPLIT444 != 0);
+constexpr bool kD16Gather = (kVariant & kVarD16) != 0 && kFmt == 0 &&
+                            (round_class(kSampling) == 0 || round_class(kSampling) == 1 || round_class(kSampling) == 3);
 
 // load_round_pk for kD16Gather shapes, round kI: each pair's second
 // coefficient is loaded straight into the high half of its word with
@@ -734,13 +679,10 @@ __device__ __forceinline__ void load_qrow_pk(const int* __restrict__ qt_pool, in
 // Samples end up as int16 row-major in the block slots (luma as Y + 128).  The next round's
 // coefficient gathers are issued before this round's column math, so their
 // LDS latency overlaps it.
-struct NoHook {
-    __device__ __forceinline__ void operator()(int) const {}
-};
-template <int kSampling, int kFmt, int kVariant = 0, typename AfterRound = NoHook>
+template <int kSampling, int kFmt, int kVariant = 0>
 __device__ __forceinline__ void idct_stage(char* __restrict__ slots, char* __restrict__ rowbuf, int lane,
-                                           const int (&zoff)[8], const uint32_t (&q)[3][4], const char* __restrict__ qlds,
-                                           const int* __restrict__ src32, int nblk, AfterRound after_round = {},
+                                           const int (&zoff)[8], const uint32_t (&q)[3][4],
+                                           const int* __restrict__ src32, int nblk,
                                            uint32_t slots_lds = 0)
 {
     const int g = lane >> 3, r = lane & 7;
@@ -749,7 +691,7 @@ __device__ __forceinline__ void idct_stage(char* __restrict__ slots, char* __res
     if constexpr (kD16Gather<kSampling, kFmt, kVariant>)
         pk = load_round_pk_d16_at<kSampling>(0, slots, slots_lds, lane, zoff, q);
     else if constexpr (kFmt == 0)
-        pk = load_round_pk<kSampling>(slots, lane, 0, zoff, q, qlds);
+        pk = load_round_pk<kSampling>(slots, lane, 0, zoff, q);
     else
         load_round_i32<kSampling>(lane, 0, src32, nblk, v);
 #pragma unroll
@@ -760,27 +702,7 @@ __device__ __forceinline__ void idct_stage(char* __restrict__ slots, char* __res
         else
             idct8<false>(v);
         int c8[8];
-        if constexpr (KLayout<kSampling>::t2) {
-            // Transpose through block b's own slot, whose coefficients the
-            // previous gather already read (DS ops of a wave run in order):
-            // row halves 0-3 (128 B) serve columns 0-3, then halves 4-7 serve
-            // columns 4-7.
-            char* tb = slots + b * kSlotBytes;
-            const char* col = tb + (r & 3) * 4;
-            *reinterpret_cast<int4*>(tb + r * 16) = make_int4(v[0], v[1], v[2], v[3]);
-            wave_lds_sync();
-            if (r < 4) {
-#pragma unroll
-                for (int k = 0; k < 8; ++k) c8[k] = *reinterpret_cast<const int*>(col + k * 16);
-            }
-            wave_lds_sync();
-            *reinterpret_cast<int4*>(tb + r * 16) = make_int4(v[4], v[5], v[6], v[7]);
-            wave_lds_sync();
-            if (r >= 4) {
-#pragma unroll
-                for (int k = 0; k < 8; ++k) c8[k] = *reinterpret_cast<const int*>(col + k * 16);
-            }
-        } else {
+        {
             int4* dst = reinterpret_cast<int4*>(rowbuf + g * kRowBufBlock + r * kRowStride);
             dst[0] = make_int4(v[0], v[1], v[2], v[3]);
             dst[1] = make_int4(v[4], v[5], v[6], v[7]);
@@ -793,7 +715,7 @@ __device__ __forceinline__ void idct_stage(char* __restrict__ slots, char* __res
             if constexpr (kD16Gather<kSampling, kFmt, kVariant>)
                 pk = load_round_pk_d16_at<kSampling>(i + 1, slots, slots_lds, lane, zoff, q);
             else if constexpr (kFmt == 0)
-                pk = load_round_pk<kSampling>(slots, lane, i + 1, zoff, q, qlds);
+                pk = load_round_pk<kSampling>(slots, lane, i + 1, zoff, q);
             else
                 load_round_i32<kSampling>(lane, i + 1, src32, nblk, v);
         }
@@ -808,53 +730,20 @@ __device__ __forceinline__ void idct_stage(char* __restrict__ slots, char* __res
                 *reinterpret_cast<short*>(blk + k * 16) = static_cast<short>(static_cast<uint32_t>(c8[k]) >> 16);
         }
         wave_lds_sync();
-        after_round(i);
     }
 }
 
-#ifndef HJD_NT_LOAD
-#define HJD_NT_LOAD 1   // non-temporal coefficient loads (read once; +2.5 % 4:2:0, +1.2 % 4:4:4 same-box)
-#endif
-#ifndef HJD_XCD
-#define HJD_XCD 1
-#endif
-#ifndef HJD_PREFETCH_AT
-#define HJD_PREFETCH_AT -1   // tuning: issue the next task's loads after IDCT round N (-1: before round 0)
-#endif
-#ifndef HJD_XCD_SPLIT
-#define HJD_XCD_SPLIT 1   // tuning: parts each XCD's eighth is walked in concurrently
-#endif
-#ifndef HJD_XCD_CHUNK
-#define HJD_XCD_CHUNK 0
-#endif
 // Logical position of workgroup `bid` in the task order.  The hardware deals
 // consecutive workgroups to the 8 XCDs in turn, so in launch order adjacent
-// strips land in 8 different L2s.  With HJD_XCD (default on) each XCD's
-// groups cover contiguous task ranges instead: XCD x = bid % 8 takes runs of
-// HJD_XCD_CHUNK consecutive positions (0: one contiguous eighth of the grid,
-// x*q + min(x, rem) + bid/8), the tail that does not fill 8 runs keeps launch
-// order.
+// strips land in 8 different L2s.  Instead each XCD's groups cover one
+// contiguous eighth of the grid: XCD x = bid % 8 takes positions
+// x*q + min(x, rem) + bid/8 (+1.8 % at 4:2:0, +2.9 % at 4:4:4 same-box,
+// profiles/r02_xcd_order_ab.json; runs of 4..1024 groups per XCD and several
+// concurrent regions per XCD measured no better).
 __device__ __forceinline__ uint32_t group_order(uint32_t bid, uint32_t ngroups)
 {
-    if constexpr (HJD_XCD == 0) {
-        return bid;
-    } else if constexpr (HJD_XCD_CHUNK == 0) {
-        const uint32_t x = bid & 7, k = bid >> 3, q = ngroups >> 3, rem = ngroups & 7;
-        if constexpr (HJD_XCD_SPLIT > 1) {
-            // the XCD's eighth in HJD_XCD_SPLIT contiguous parts, consecutive
-            // dispatches going to different parts (a bijection on the eighth)
-            constexpr uint32_t S = HJD_XCD_SPLIT;
-            const uint32_t n = q + (x < rem ? 1u : 0u);
-            const uint32_t p = k % S, j = k / S, ps = n / S, pr = n % S;
-            return x * q + min(x, rem) + p * ps + min(p, pr) + j;
-        }
-        return x * q + min(x, rem) + k;
-    } else {
-        constexpr uint32_t C = HJD_XCD_CHUNK;
-        if (bid >= ngroups / (8 * C) * (8 * C)) return bid;
-        const uint32_t x = bid & 7, k = bid >> 3;
-        return ((k / C) * 8 + x) * C + k % C;
-    }
+    const uint32_t x = bid & 7, k = bid >> 3, q = ngroups >> 3, rem = ngroups & 7;
+    return x * q + min(x, rem) + k;
 }
 
 // The fused kernel.  Persistent grid; wave w owns the contiguous task range
@@ -862,21 +751,20 @@ __device__ __forceinline__ uint32_t group_order(uint32_t bid, uint32_t ngroups)
 // SGPRs; the next task's coefficients are prefetched into VGPRs while the
 // current one is transformed.
 template <int kSampling, int kFmt, int kVariant>
-__global__ __launch_bounds__(kGroupThreads, KLayout<kSampling>::min_waves) void decode_kernel(const void* __restrict__ coefs,
+__global__ __launch_bounds__(kGroupThreads, KLayout::min_waves) void decode_kernel(const void* __restrict__ coefs,
                                                               const int* __restrict__ qt_pool,
                                                               const FrameDev* __restrict__ frames, int nframes,
                                                               int64_t total_tasks, uint8_t* __restrict__ out,
                                                               int64_t chunk, int64_t rem)
 {
-    using L = KLayout<kSampling>;
+    using L = KLayout;
     __shared__ __attribute__((aligned(16))) char lds[kWavesPerGroup * L::wave_lds];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     char* slots = lds + wave * L::wave_lds;
     // LDS byte address of this wave's slots (inline-asm DS loads, kVarD16)
     const uint32_t slots_lds = static_cast<uint32_t>(reinterpret_cast<size_t>(lds)) + wave * L::wave_lds;
-    char* rowbuf = slots + kTaskBlocks * kSlotBytes;   // transpose buffer (default) or table rows (t2)
-    char* qlds = rowbuf;
+    char* rowbuf = slots + kTaskBlocks * kSlotBytes;   // transpose buffer
     const int r = lane & 7;
 
     // this wave's task sequence: t_begin, t_begin + t_step, ... (< t_end)
@@ -919,13 +807,10 @@ __global__ __launch_bounds__(kGroupThreads, KLayout<kSampling>::min_waves) void 
         if (g.nblk == kTaskBlocks) {
 #pragma unroll
             for (int k = 0; k < 6; ++k) {
-#if HJD_NT_LOAD
+                // non-temporal: read once (+2.5 % 4:2:0, +1.2 % 4:4:4 same-box, profiles/r02_ntload_ab.json)
                 typedef int i32x4 __attribute__((ext_vector_type(4)));
                 const i32x4 t = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(src) + lane + 64 * k);
                 pre[k] = make_int4(t.x, t.y, t.z, t.w);
-#else
-                pre[k] = src[lane + 64 * k];
-#endif
             }
         } else {
 #pragma unroll
@@ -939,11 +824,9 @@ __global__ __launch_bounds__(kGroupThreads, KLayout<kSampling>::min_waves) void 
         prefetch(task_geom<kSampling>(pc, t_begin));
         // the first task's table rows load beside its coefficients, so a wave
         // start waits for one memory round trip, not two
-        if constexpr (!L::t2) {
-            q_tables[0] = pc.qt0; q_tables[1] = pc.qt1; q_tables[2] = pc.qt2;
+        q_tables[0] = pc.qt0; q_tables[1] = pc.qt1; q_tables[2] = pc.qt2;
 #pragma unroll
-            for (int c = 0; c < 3; ++c) load_qrow_pk(qt_pool, q_tables[c], r, q[c]);
-        }
+        for (int c = 0; c < 3; ++c) load_qrow_pk(qt_pool, q_tables[c], r, q[c]);
         __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0): see the edge-strip drain below
     }
 
@@ -954,19 +837,8 @@ __global__ __launch_bounds__(kGroupThreads, KLayout<kSampling>::min_waves) void 
         if constexpr (kFmt == 0) {
             if (cc.qt0 != q_tables[0] || cc.qt1 != q_tables[1] || cc.qt2 != q_tables[2]) {
                 q_tables[0] = cc.qt0; q_tables[1] = cc.qt1; q_tables[2] = cc.qt2;
-                if constexpr (L::t2) {
-                    // lane group c < 3 writes component c's row r into the wave's
-                    // table copy (read by later DS ops of this wave, in order)
-                    const int c = lane >> 3;
-                    if (c < 3) {
-                        uint32_t qq[4];
-                        load_qrow_pk(qt_pool, c == 0 ? q_tables[0] : c == 1 ? q_tables[1] : q_tables[2], r, qq);
-                        *reinterpret_cast<uint4*>(qlds + c * 128 + r * 16) = make_uint4(qq[0], qq[1], qq[2], qq[3]);
-                    }
-                } else {
 #pragma unroll
-                    for (int c = 0; c < 3; ++c) load_qrow_pk(qt_pool, q_tables[c], r, q[c]);
-                }
+                for (int c = 0; c < 3; ++c) load_qrow_pk(qt_pool, q_tables[c], r, q[c]);
             }
 #pragma unroll
             for (int k = 0; k < 6; ++k) {
@@ -974,7 +846,7 @@ __global__ __launch_bounds__(kGroupThreads, KLayout<kSampling>::min_waves) void 
                 *reinterpret_cast<int4*>(slots + (j >> 3) * kSlotBytes + (j & 7) * 16) = pre[k];
             }
             wave_lds_sync();
-            if (HJD_PREFETCH_AT < 0 && next_task >= 0) {
+            if (next_task >= 0) {   // the next task's loads fly during this task
                 while (next_task >= pc.end) cursor_load(pc, frames, nframes, total_tasks, pc.idx + 1);
                 prefetch(task_geom<kSampling>(pc, next_task));
             }
@@ -983,36 +855,16 @@ __global__ __launch_bounds__(kGroupThreads, KLayout<kSampling>::min_waves) void 
                 while (next_task >= pc.end) cursor_load(pc, frames, nframes, total_tasks, pc.idx + 1);
         }
 
-        // HJD_PREFETCH_AT >= 0 (tuning): the next task's loads are issued after
-        // IDCT round HJD_PREFETCH_AT instead of before round 0
         constexpr int kRows = KGeom<kSampling>::kMcuH;
         constexpr int kStripW = KGeom<kSampling>::kStripW;
         uint8_t* fout = out + cc.out_base;
         const bool full = cc.vec_ok && tg.x_base + kStripW <= cc.width && tg.y_base + kRows <= cc.height;
-        constexpr bool kSplit = HJD_SPLIT444 != 0 && kSampling == 0 && (kVariant & (kAblNoColour | kAblNoIdct)) == 0;
-        auto late_prefetch = [&](int i) {
-            if constexpr (kFmt == 0 && HJD_PREFETCH_AT >= 0) {
-                if (i == HJD_PREFETCH_AT && next_task >= 0) {
-                    while (next_task >= pc.end) cursor_load(pc, frames, nframes, total_tasks, pc.idx + 1);
-                    prefetch(task_geom<kSampling>(pc, next_task));
-                }
-            }
-            if constexpr (kSplit) {
-                if (full && (i == 2 || i == 5))
-                    colour_half444<kVariant>(slots, lane, fout, cc.pitch, cc.width, tg.y_base, tg.x_base, i == 5 ? 1 : 0);
-            }
-        };
         if constexpr ((kVariant & kAblNoIdct) == 0)
-            idct_stage<kSampling, kFmt, kVariant>(slots, rowbuf, lane, zoff, q, qlds,
-                                        static_cast<const int*>(coefs) + tg.blk0 * 64, tg.nblk, late_prefetch,
-                                        slots_lds);
-        else
-            late_prefetch(HJD_PREFETCH_AT);
+            idct_stage<kSampling, kFmt, kVariant>(slots, rowbuf, lane, zoff, q,
+                                                  static_cast<const int*>(coefs) + tg.blk0 * 64, tg.nblk, slots_lds);
 
         if constexpr ((kVariant & kAblNoColour) != 0) {
             (void)fout;
-        } else if (kSplit && full) {
-            // converted inside the IDCT stage (late_prefetch hook)
         } else if (full)
             colour_stage<kSampling, true, kVariant>(slots, lane, fout, cc.pitch, cc.width, cc.height, tg.y_base, tg.x_base);
         else {

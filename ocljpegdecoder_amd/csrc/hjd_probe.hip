@@ -9,9 +9,10 @@
 //    THIS box's achievable rate next to the fraction of the 8 TB/s spec.
 // 2. The d16 gather probe: the 4:4:4 kernels gather coefficient pairs with
 //    ds_read_u16_d16_hi, which is only a valid gather where that load zeroes
-//    the low half of its destination (sramecc+ parts).  The runtime runs a
-//    one-wave probe per device at first use and takes the kVarD16 kernels only
-//    if every lane saw the low half zeroed (hjd_runtime.hip device_d16_gather).
+//    the low half of its destination (sramecc+ parts).  hjd_ctx_create runs a
+//    one-wave probe per device (eagerly, outside any launch or stream capture)
+//    and the launches take the kVarD16 kernels only if it completed and every
+//    lane saw the low half zeroed (hjd_runtime.hip d16_gather_selected).
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
@@ -161,47 +162,78 @@ __global__ __launch_bounds__(64) void clock_probe_kernel(unsigned long long* __r
 }
 
 std::mutex g_probe_mu;
-std::vector<int> g_probe;   // per device: -1 not run, 0 preserves / failed, 1 zeroes
+std::vector<int> g_probe;   // per device: -1 not run (or the run failed), 0 preserves, 1 zeroes
+
+// A failed HIP call inside the probe must not leave its error behind for the
+// caller's next hipGetLastError() (a launch would then report a failure of
+// the probe as its own).
+int probe_failed(int prev)
+{
+    (void)hipGetLastError();
+    (void)hipSetDevice(prev);
+    (void)hipGetLastError();
+    return -1;
+}
+
+// One run of the probe on `device`: 1 zeroes, 0 preserves, -1 could not run
+// (HIP error, cleared).  HJD_D16_PROBE=hipfail makes the first HIP call fail
+// for real (an allocation no device can satisfy): the test of the failure path.
+int run_probe(int device)
+{
+    int prev = 0;
+    if (hipGetDevice(&prev) != hipSuccess) return probe_failed(0);
+    if (hipSetDevice(device) != hipSuccess) return probe_failed(prev);
+    const char* force = getenv("HJD_D16_PROBE");
+    const size_t bytes = (force && strcmp(force, "hipfail") == 0) ? (size_t(1) << 60) : 64 * sizeof(uint32_t);
+    uint32_t* d = nullptr;
+    if (hipMalloc(&d, bytes) != hipSuccess) return probe_failed(prev);
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+        (void)hipFree(d);
+        return probe_failed(prev);
+    }
+    hipLaunchKernelGGL(d16_probe_kernel, dim3(1), dim3(64), 0, s, d);
+    uint32_t h[64];
+    int result = -1;
+    if (hipGetLastError() == hipSuccess && hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, s) == hipSuccess &&
+        hipStreamSynchronize(s) == hipSuccess) {
+        result = 1;
+        for (int lane = 0; lane < 64; ++lane)
+            if (h[lane] != static_cast<uint32_t>(0x1234 + 3 * (63 - lane)) << 16) result = 0;
+    }
+    const bool ok = hipStreamDestroy(s) == hipSuccess && hipFree(d) == hipSuccess && result >= 0;
+    if (!ok) return probe_failed(prev);
+    (void)hipSetDevice(prev);
+    return result;
+}
 
 }  // namespace
 
 // 1 if ds_read_u16_d16_hi zeroes the low half on `device` (every lane), 0 if it
-// does not or the probe could not run.  Runs once per device (cached);
-// HJD_D16_PROBE=fail forces 0 (tests of the fallback).
+// does not or the probe could not run.  A completed probe is cached per device;
+// a failed one is not (the next call -- the next hjd_ctx_create -- tries
+// again).  HJD_D16_PROBE=fail forces 0 (tests of the fallback).
 int hjd_internal::d16_probe(int device)
 {
     std::lock_guard<std::mutex> lock(g_probe_mu);
     if (device < 0) return 0;
     if (static_cast<size_t>(device) >= g_probe.size()) g_probe.resize(device + 1, -1);
     if (g_probe[device] >= 0) return g_probe[device];
-    int result = 0;
     const char* force = getenv("HJD_D16_PROBE");
     if (force && strcmp(force, "fail") == 0) {
         g_probe[device] = 0;
         return 0;
     }
-    int prev = 0;
-    uint32_t* d = nullptr;
-    if (hipGetDevice(&prev) == hipSuccess && hipSetDevice(device) == hipSuccess &&
-        hipMalloc(&d, 64 * sizeof(uint32_t)) == hipSuccess) {
-        hipStream_t s = nullptr;
-        if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess) {
-            hipLaunchKernelGGL(d16_probe_kernel, dim3(1), dim3(64), 0, s, d);
-            uint32_t h[64];
-            if (hipGetLastError() == hipSuccess &&
-                hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, s) == hipSuccess &&
-                hipStreamSynchronize(s) == hipSuccess) {
-                result = 1;
-                for (int lane = 0; lane < 64; ++lane)
-                    if (h[lane] != static_cast<uint32_t>(0x1234 + 3 * (63 - lane)) << 16) result = 0;
-            }
-            (void)hipStreamDestroy(s);
-        }
-        (void)hipFree(d);
-    }
-    (void)hipSetDevice(prev);
-    g_probe[device] = result;
-    return result;
+    const int r = run_probe(device);
+    if (r >= 0) g_probe[device] = r;
+    return r > 0 ? 1 : 0;
+}
+
+int hjd_internal::d16_probe_cached(int device)
+{
+    std::lock_guard<std::mutex> lock(g_probe_mu);
+    if (device < 0 || static_cast<size_t>(device) >= g_probe.size()) return -1;
+    return g_probe[device];
 }
 
 extern "C" {

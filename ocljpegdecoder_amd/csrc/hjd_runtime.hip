@@ -11,7 +11,9 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <mutex>
+#include <tuple>
 #include <new>
 #include <string>
 #include <vector>
@@ -85,8 +87,10 @@ struct hjd_plan {
     int variant = 0;            // kernel variant bits (hjd_plan_set_variant)
     int out_format = HJD_OUT_BGRX;   // common output format of all frames
     int kernel_mode = HJD_KERNEL_AUTO;
-    int tuned_grid = 0;         // hjd_plan_autotune's grid (0: the shape default)
+    int tuned_grid = 0;         // hjd_plan_autotune's / hjd_plan_set_chunk's grid (0: the shape default)
     int tuned_per_wave = 0;     // its tasks per wave
+    int autotune_launches = 0;  // kernel launches of the last hjd_plan_autotune
+    int autotune_cached = 0;    // 1: that call reused a cached choice
 };
 
 constexpr int64_t kDefaultLatencyMaxTasks = 1024;   // measured: profiles/r01_latency_kernel.json
@@ -107,21 +111,21 @@ static int64_t latency_max_tasks()
 // the register.  MI355X as deployed (sramecc+) does that
 // (profiles/r03_d16_probe.txt); a half-preserving part would corrupt the
 // pairs.  So the variant is taken only where the one-wave hardware probe
-// (hjd_probe.hip, once per device) saw every lane's low half zeroed; the
-// v_perm kernels are the fallback.  HJD_D16=0 / 1 overrides the probe (A/B).
-constexpr bool kD16Default = true;   // same-box A/B: profiles/r03_444_d16_gather_ab.json
+// (hjd_probe.hip, run by hjd_ctx_create) completed and saw every lane's low
+// half zeroed; the v_perm kernels are the fallback.  HJD_D16=0 forces the
+// fallback (A/B); nothing forces the d16 kernels onto a part the probe did not
+// pass.  Launches only read the cached answer.
 bool hjd_internal::d16_gather_selected(int device)
 {
     const char* e = getenv("HJD_D16");
-    if (e) return e[0] != '0';
-    if (!kD16Default || device < 0) return false;
-    return hjd_internal::d16_probe(device) == 1;
+    if (e && e[0] == '0') return false;
+    return device >= 0 && hjd_internal::d16_probe_cached(device) == 1;
 }
 static bool device_d16_gather(int device) { return hjd_internal::d16_gather_selected(device); }
 
 static int geometry(int width, int height, int sampling, int& mcu_w, int& mcu_h, int& bpm, int& tasks_mcus);
-static int decode_grid(int sampling, int fmt, int64_t tasks);
-static int grid_for_chunk(int64_t tasks, int64_t per_wave);
+static int64_t default_per_wave(int sampling, int fmt);
+static int grid_for_chunk(int64_t tasks, int64_t per_wave, bool occupancy_floor = true);
 
 // launch_decode variant bits 8 and up: a stage-skipping measurement variant
 // (hjd_debug_plan_launch_stages), stages << kStageShift | plan variant bits.
@@ -163,7 +167,7 @@ int hjd_internal::launch_decode(int device, int num_cu, int sampling, int input_
     (void)num_cu;
     SamplingGeom sg;
     if (!sampling_geom(sampling, &sg)) return set_error(HJD_E_INVALID, "unsupported sampling %d", sampling);
-    const int grid = grid_blocks > 0 ? grid_blocks : decode_grid(sampling, fmt, tasks);
+    const int grid = grid_blocks > 0 ? grid_blocks : grid_for_chunk(tasks, default_per_wave(sampling, fmt));
     if (out_format != HJD_OUT_BGRX && out_format != HJD_OUT_BGR24)
         return set_error(HJD_E_INVALID, "unknown output format %d", out_format);
     using K = void (*)(const void*, const int*, const FrameDev*, int, int64_t, uint8_t*);   // latency kernels
@@ -288,6 +292,10 @@ int hjd_ctx_create(int device, hjd_ctx** out)
     int cu = 0;
     if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cu > 0)
         c->num_cu = cu;
+    // the d16 gather probe runs here, once per device, so that no launch (which
+    // may be inside a stream capture) ever has to run it; a failed probe leaves
+    // no HIP error behind and the launches use the v_perm kernels
+    (void)hjd_internal::d16_probe(device);
     *out = c;
     return HJD_OK;
 }
@@ -431,7 +439,8 @@ int hjd_plan_set_chunk(hjd_plan* plan, int tasks)
 {
     if (!plan || tasks < 0 || tasks > 4096) return fail(HJD_E_INVALID, "invalid chunk arguments");
     plan->tuned_per_wave = tasks;
-    plan->tuned_grid = tasks ? grid_for_chunk(std::max<int64_t>(plan->tasks, 1), tasks) : 0;   // 0: shape default
+    // exactly `tasks` per wave: no occupancy floor (unlike the shape default)
+    plan->tuned_grid = tasks ? grid_for_chunk(std::max<int64_t>(plan->tasks, 1), tasks, false) : 0;   // 0: default
     return HJD_OK;
 }
 
@@ -462,30 +471,41 @@ int64_t hjd_plan_coef_bytes(const hjd_plan* plan) { return plan ? plan->coef_byt
 // -> 0.76) and both int32 (idct.h) formats (4:2:0 0.67 -> 0.76-0.78, 4:4:4
 // 0.74-0.75 -> 0.765-0.77), same box (profiles/r03_tune_tasks_per_wave_ext.json).
 // HJD_TASKS_PER_WAVE overrides it (tuning).
-// Groups for `per_wave` tasks per wave, but never fewer than ~4 waves per
-// SIMD (256 CUs x 4 SIMDs): a single 4:4:4 frame at 16 tasks per wave would
-// leave most of the chip idle.
-static int grid_for_chunk(int64_t tasks, int64_t per_wave)
-{
-    per_wave = std::max<int64_t>(1, std::min<int64_t>(per_wave, tasks / (4 * 1024)));
-    const int64_t waves = (tasks + per_wave - 1) / per_wave;
-    const int64_t groups = (waves + hjd::kWavesPerGroup - 1) / hjd::kWavesPerGroup;
-    return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(groups, int64_t(1) << 24)));
-}
-
-static int decode_grid(int sampling, int fmt, int64_t tasks)
+static int64_t default_per_wave(int sampling, int fmt)
 {
     static const int64_t env = [] {
         const char* e = getenv("HJD_TASKS_PER_WAVE");
         return e ? static_cast<int64_t>(atoll(e)) : int64_t(0);
     }();
-    int64_t per_wave = 16;
-    if (fmt != 0 || sampling == HJD_GRAY || sampling == HJD_YUV411_H4V1)
-        per_wave = 1;
-    else if (sampling == HJD_YUV420)
-        per_wave = 2;
-    if (env > 0) per_wave = env;
-    return grid_for_chunk(tasks, per_wave);
+    if (env > 0) return env;
+    if (fmt != 0 || sampling == HJD_GRAY || sampling == HJD_YUV411_H4V1) return 1;
+    return sampling == HJD_YUV420 ? 2 : 16;
+}
+
+// Tasks per wave a chunk request turns into: with the occupancy floor (the
+// shape default and the autotune candidates) never fewer than ~4 waves per
+// SIMD (256 CUs x 4 SIMDs), since a single 4:4:4 frame at 16 tasks per wave
+// would leave most of the chip idle; hjd_plan_set_chunk pins it exactly.
+static int64_t effective_per_wave(int64_t tasks, int64_t per_wave, bool occupancy_floor)
+{
+    if (occupancy_floor) per_wave = std::min<int64_t>(per_wave, tasks / (4 * 1024));
+    return std::max<int64_t>(1, per_wave);
+}
+
+// Groups for `per_wave` tasks per wave.
+static int grid_for_chunk(int64_t tasks, int64_t per_wave, bool occupancy_floor)
+{
+    per_wave = effective_per_wave(tasks, per_wave, occupancy_floor);
+    const int64_t waves = (tasks + per_wave - 1) / per_wave;
+    const int64_t groups = (waves + hjd::kWavesPerGroup - 1) / hjd::kWavesPerGroup;
+    return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(groups, int64_t(1) << 24)));
+}
+
+// A default launch of this plan takes the persistent kernel (not the latency one).
+static bool plan_is_persistent(const hjd_plan* p)
+{
+    return p->kernel_mode == HJD_KERNEL_PERSISTENT ||
+           (p->kernel_mode == HJD_KERNEL_AUTO && p->tasks > latency_max_tasks());
 }
 
 static int default_grid(const hjd_ctx* ctx, int64_t work_waves)
@@ -503,8 +523,9 @@ int hjd_plan_launch(hjd_plan* plan, const void* d_coefs, void* d_out, void* stre
     if ((reinterpret_cast<uintptr_t>(d_coefs) | reinterpret_cast<uintptr_t>(d_out)) & 15)
         return fail(HJD_E_INVALID, "device buffers must be 16-byte aligned");
     if (grid_blocks < 0) return fail(HJD_E_INVALID, "grid_blocks < 0");
-    if (grid_blocks == 0 && plan->tuned_grid > 0 && plan->kernel_mode != HJD_KERNEL_LATENCY)
-        grid_blocks = plan->tuned_grid;   // hjd_plan_autotune's / hjd_plan_set_chunk's chunk
+    // hjd_plan_autotune's / hjd_plan_set_chunk's chunk, for plans that take the
+    // persistent kernel anyway (a small AUTO plan keeps the latency kernel)
+    if (grid_blocks == 0 && plan->tuned_grid > 0 && plan_is_persistent(plan)) grid_blocks = plan->tuned_grid;
     return hjd_internal::launch_decode(plan->ctx->device, plan->ctx->num_cu, plan->sampling, plan->input_format,
                                        plan->variant, d_coefs, plan->d_qt,
                                        reinterpret_cast<const hjd_internal::FrameRecord*>(plan->d_frames),
@@ -522,6 +543,48 @@ int hjd_plan_launch(hjd_plan* plan, const void* d_coefs, void* d_out, void* stre
 // over rounds) for the plan's later default launches.  All candidates give
 // identical pixels.  Synchronous; plans small enough for the latency kernel
 // are left as they are.
+//
+// The choice is cached per process: device x sampling x input format x output
+// format x the plan's other variant bits x task-count octave (floor(log2
+// tasks)).  A later plan of the same key takes the cached shape with no
+// launch (the search cost ~1 s per plan).  HJD_AUTOTUNE_CACHE=0
+// disables the cache; hjd_autotune_cache_clear() empties it.
+namespace {
+struct TuneKey {
+    int device, sampling, input_format, out_format, keep_variant, octave;
+    bool operator<(const TuneKey& o) const
+    {
+        return std::tie(device, sampling, input_format, out_format, keep_variant, octave) <
+               std::tie(o.device, o.sampling, o.input_format, o.out_format, o.keep_variant, o.octave);
+    }
+};
+std::mutex g_tune_mu;
+std::map<TuneKey, std::pair<int, int>> g_tune;   // -> (tasks per wave, store bit)
+
+int octave_of(int64_t n)
+{
+    int k = 0;
+    while (n > 1) {
+        n >>= 1;
+        ++k;
+    }
+    return k;
+}
+
+bool tune_cache_enabled()
+{
+    const char* e = getenv("HJD_AUTOTUNE_CACHE");
+    return !(e && e[0] == '0');
+}
+}  // namespace
+
+int hjd_autotune_cache_clear(void)
+{
+    std::lock_guard<std::mutex> lock(g_tune_mu);
+    g_tune.clear();
+    return HJD_OK;
+}
+
 int hjd_plan_autotune(hjd_plan* plan, const void* d_coefs, void* d_out, void* stream, int rounds,
                       int32_t* tasks_per_wave, int32_t* variant)
 {
@@ -534,9 +597,23 @@ int hjd_plan_autotune(hjd_plan* plan, const void* d_coefs, void* d_out, void* st
         if (variant) *variant = plan->variant;
         return HJD_OK;
     };
-    if (plan->tasks == 0 || plan->kernel_mode == HJD_KERNEL_LATENCY ||
-        (plan->kernel_mode == HJD_KERNEL_AUTO && plan->tasks <= latency_max_tasks()))
-        return report();
+    plan->autotune_launches = 0;
+    plan->autotune_cached = 0;
+    if (plan->tasks == 0 || !plan_is_persistent(plan)) return report();
+    const int keep = plan->variant & ~1;
+    const TuneKey key{plan->ctx->device, plan->sampling, plan->input_format, plan->out_format, keep,
+                      octave_of(plan->tasks)};
+    if (tune_cache_enabled()) {
+        std::lock_guard<std::mutex> lock(g_tune_mu);
+        auto it = g_tune.find(key);
+        if (it != g_tune.end()) {
+            plan->tuned_per_wave = it->second.first;
+            plan->tuned_grid = grid_for_chunk(plan->tasks, it->second.first);
+            plan->variant = keep | it->second.second;
+            plan->autotune_cached = 1;
+            return report();
+        }
+    }
     struct Cand {
         int64_t per_wave;   // tasks per wave
         int store;          // variant bit 0
@@ -559,12 +636,12 @@ int hjd_plan_autotune(hjd_plan* plan, const void* d_coefs, void* d_out, void* st
         (void)hipEventDestroy(e0);
         return fail(HJD_E_HIP, "hipEventCreate");
     }
-    const int keep = plan->variant & ~1;
     int rc = HJD_OK;
     for (int r = 0; r < rounds && rc == HJD_OK; ++r) {
         for (Cand& c : cands) {
             const int v = keep | c.store;
             auto go = [&]() {
+                plan->autotune_launches++;
                 return hjd_internal::launch_decode(plan->ctx->device, plan->ctx->num_cu, plan->sampling,
                                                    plan->input_format, v, d_coefs, plan->d_qt,
                                                    reinterpret_cast<const hjd_internal::FrameRecord*>(plan->d_frames),
@@ -589,7 +666,45 @@ int hjd_plan_autotune(hjd_plan* plan, const void* d_coefs, void* d_out, void* st
     plan->tuned_grid = best->grid;
     plan->tuned_per_wave = static_cast<int>(best->per_wave);
     plan->variant = keep | best->store;
+    if (tune_cache_enabled()) {
+        std::lock_guard<std::mutex> lock(g_tune_mu);
+        g_tune[key] = {static_cast<int>(best->per_wave), best->store};
+    }
     return report();
+}
+
+int hjd_plan_launch_shape(const hjd_plan* plan, hjd_launch_shape* out)
+{
+    if (!plan || !out) return fail(HJD_E_INVALID, "invalid arguments");
+    hjd_launch_shape r;
+    memset(&r, 0, sizeof(r));
+    r.variant = plan->variant;
+    r.autotune_launches = plan->autotune_launches;
+    r.autotune_cached = plan->autotune_cached;
+    if (plan->tasks > 0 && !plan_is_persistent(plan)) {
+        r.kernel = HJD_KERNEL_LATENCY;
+        r.grid = static_cast<int32_t>(std::min<int64_t>(plan->tasks, INT32_MAX));
+        r.tasks_per_wave = 1;
+        r.max_tasks_per_wave = 1;
+    } else {
+        r.kernel = HJD_KERNEL_PERSISTENT;
+        const int fmt = plan->input_format == HJD_IN_Q16_ZIGZAG ? 0 : 1;
+        const int64_t t = std::max<int64_t>(plan->tasks, 1);
+        const bool pinned = plan->tuned_grid > 0;
+        r.tasks_per_wave = static_cast<int32_t>(
+            pinned ? effective_per_wave(t, plan->tuned_per_wave, false)
+                   : effective_per_wave(t, default_per_wave(plan->sampling, fmt), true));
+        r.grid = pinned ? plan->tuned_grid : grid_for_chunk(t, default_per_wave(plan->sampling, fmt));
+        if ((plan->variant & hjd::kVarWgInterleave) != 0) {   // groups take quads of tasks
+            const int64_t quads = (t + hjd::kWavesPerGroup - 1) / hjd::kWavesPerGroup;
+            r.max_tasks_per_wave = static_cast<int32_t>((quads + r.grid - 1) / r.grid);
+        } else {
+            const int64_t waves = static_cast<int64_t>(r.grid) * hjd::kWavesPerGroup;
+            r.max_tasks_per_wave = static_cast<int32_t>((t + waves - 1) / waves);
+        }
+    }
+    *out = r;
+    return HJD_OK;
 }
 
 int hjd_debug_plan_launch_stages(hjd_plan* plan, int stages, const void* d_coefs, void* d_out, void* stream,

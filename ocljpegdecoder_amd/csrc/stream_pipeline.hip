@@ -11,6 +11,10 @@
 // Slot reuse is ordered by events: the host waits for job j-nslots' upload
 // before refilling pinned slot s, and the upload of job j waits (on the GPU)
 // for job j-nslots' kernel before overwriting device slot s.
+// Every upload and kernel is bracketed by timing events, harvested when the
+// slot is reused (or at sync): hjd_stream_busy reports how long the copy
+// engine and the kernels were busy, i.e. how much of the wall time the
+// pipeline kept the GPU side fed (bench.py config5_stream_host).
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -60,6 +64,8 @@ struct hjd_stream {
     std::vector<uint8_t*> host;      // pinned staging
     std::vector<uint8_t*> dev;       // device slots
     std::vector<hipEvent_t> h2d_done, kernel_done;
+    std::vector<hipEvent_t> h2d_start, kernel_start;   // timing brackets of the slot's last job
+    std::vector<char> timed_pending;    // the slot's last job has unharvested timing events
     std::vector<int64_t> slot_issued;   // last job index whose GPU work was issued on the slot
     hipStream_t copy = nullptr, compute = nullptr;
 
@@ -71,6 +77,7 @@ struct hjd_stream {
     std::vector<std::thread> workers;
 
     std::atomic<int64_t> images{0}, pixels{0}, decode_ns{0}, h2d_bytes{0}, launches{0};
+    std::atomic<int64_t> h2d_busy_ns{0}, kernel_busy_ns{0};
     std::atomic<int> out_format{HJD_OUT_BGRX};   // for subsequent submits
     int first_error = HJD_OK;
     std::string first_error_msg;
@@ -86,7 +93,25 @@ struct hjd_stream {
 
     int run_job(const Job& job);
     void worker();
+    void harvest(int s);
 };
+
+// Add slot s's last job's copy and kernel durations to the busy totals.  The
+// caller owns the slot (its next job, or sync with every job finished).
+void hjd_stream::harvest(int s)
+{
+    if (!timed_pending[s]) return;
+    timed_pending[s] = 0;
+    float copy_ms = 0, kernel_ms = 0;
+    if (hipEventSynchronize(kernel_done[s]) != hipSuccess ||
+        hipEventElapsedTime(&copy_ms, h2d_start[s], h2d_done[s]) != hipSuccess ||
+        hipEventElapsedTime(&kernel_ms, kernel_start[s], kernel_done[s]) != hipSuccess) {
+        (void)hipGetLastError();
+        return;
+    }
+    h2d_busy_ns += static_cast<int64_t>(copy_ms * 1e6);
+    kernel_busy_ns += static_cast<int64_t>(kernel_ms * 1e6);
+}
 
 int hjd_stream::run_job(const Job& job)
 {
@@ -121,15 +146,19 @@ int hjd_stream::run_job(const Job& job)
             for (int k = 0; k < 64; ++k) qn[c * 64 + kZigzag[k]] = info.qt[c][k];
     }
 
+    harvest(s);   // the slot's previous job (issued nslots jobs ago)
     // Issue the GPU work (also on failure, with nothing to do, so the slot's
     // event chain stays intact for the next job).
+    const bool work = rc == HJD_OK && tasks > 0;
     hipError_t e = hipStreamWaitEvent(copy, kernel_done[s], 0);
+    if (e == hipSuccess && work) e = hipEventRecord(h2d_start[s], copy);
     if (e == hipSuccess && rc == HJD_OK)
         e = hipMemcpyAsync(dev[s], h, kHeader + coef_bytes, hipMemcpyHostToDevice, copy);
     if (e == hipSuccess) e = hipEventRecord(h2d_done[s], copy);
     if (e == hipSuccess) e = hipStreamWaitEvent(compute, h2d_done[s], 0);
+    if (e == hipSuccess && work) e = hipEventRecord(kernel_start[s], compute);
     int lrc = HJD_OK;
-    if (e == hipSuccess && rc == HJD_OK && tasks > 0) {
+    if (e == hipSuccess && work) {
         lrc = hjd_internal::launch_decode(device, num_cu, info.sampling, HJD_IN_Q16_ZIGZAG, 0, dev[s] + kHeader,
                                           reinterpret_cast<const int32_t*>(dev[s] + kQtOffset),
                                           reinterpret_cast<const FrameRecord*>(dev[s]), 1, tasks, job.d_out,
@@ -137,6 +166,7 @@ int hjd_stream::run_job(const Job& job)
         launches++;
     }
     if (e == hipSuccess) e = hipEventRecord(kernel_done[s], compute);
+    timed_pending[s] = e == hipSuccess && work && lrc == HJD_OK;
     {
         std::lock_guard<std::mutex> g(mu);
         slot_issued[s] = job.index;
@@ -199,6 +229,9 @@ int hjd_stream_create(hjd_ctx* ctx, int64_t max_blocks, int nslots, int nthreads
     st->dev.assign(nslots, nullptr);
     st->h2d_done.assign(nslots, nullptr);
     st->kernel_done.assign(nslots, nullptr);
+    st->h2d_start.assign(nslots, nullptr);
+    st->kernel_start.assign(nslots, nullptr);
+    st->timed_pending.assign(nslots, 0);
     st->slot_issued.assign(nslots, 0);
     for (int s = 0; s < nslots; ++s) {
         st->slot_issued[s] = s - nslots;
@@ -207,10 +240,10 @@ int hjd_stream_create(hjd_ctx* ctx, int64_t max_blocks, int nslots, int nthreads
             return bail("hipHostMalloc", e);
         if ((e = hipMalloc(reinterpret_cast<void**>(&st->dev[s]), st->slot_bytes)) != hipSuccess)
             return bail("hipMalloc", e);
-        if ((e = hipEventCreateWithFlags(&st->h2d_done[s], hipEventDisableTiming)) != hipSuccess)
-            return bail("event", e);
-        if ((e = hipEventCreateWithFlags(&st->kernel_done[s], hipEventDisableTiming)) != hipSuccess)
-            return bail("event", e);
+        if ((e = hipEventCreate(&st->h2d_done[s])) != hipSuccess) return bail("event", e);
+        if ((e = hipEventCreate(&st->kernel_done[s])) != hipSuccess) return bail("event", e);
+        if ((e = hipEventCreate(&st->h2d_start[s])) != hipSuccess) return bail("event", e);
+        if ((e = hipEventCreate(&st->kernel_start[s])) != hipSuccess) return bail("event", e);
     }
     // NUMA-local workers; HJD_NUMA=0 disables
     const char* numa_env = getenv("HJD_NUMA");
@@ -243,6 +276,8 @@ int hjd_stream_destroy(hjd_stream* st)
         if (st->dev[s]) (void)hipFree(st->dev[s]);
         if (st->h2d_done[s]) (void)hipEventDestroy(st->h2d_done[s]);
         if (st->kernel_done[s]) (void)hipEventDestroy(st->kernel_done[s]);
+        if (st->h2d_start[s]) (void)hipEventDestroy(st->h2d_start[s]);
+        if (st->kernel_start[s]) (void)hipEventDestroy(st->kernel_start[s]);
     }
     if (st->copy) (void)hipStreamDestroy(st->copy);
     if (st->compute) (void)hipStreamDestroy(st->compute);
@@ -282,6 +317,8 @@ int hjd_stream_sync(hjd_stream* st, int64_t stats[5])
     hipError_t e = hipSetDevice(st->device);
     if (e == hipSuccess) e = hipStreamSynchronize(st->compute);
     if (e == hipSuccess) e = hipStreamSynchronize(st->copy);
+    if (e == hipSuccess)
+        for (int s = 0; s < st->nslots; ++s) st->harvest(s);   // every job is finished
     if (stats) {
         stats[0] = st->images;
         stats[1] = st->pixels;
@@ -296,6 +333,14 @@ int hjd_stream_sync(hjd_stream* st, int64_t stats[5])
         st->first_error = HJD_OK;
         return set_error(rc, "%s", st->first_error_msg.c_str());
     }
+    return HJD_OK;
+}
+
+int hjd_stream_busy(hjd_stream* st, int64_t* h2d_busy_ns, int64_t* kernel_busy_ns)
+{
+    if (!st) return set_error(HJD_E_INVALID, "stream is NULL");
+    if (h2d_busy_ns) *h2d_busy_ns = st->h2d_busy_ns;
+    if (kernel_busy_ns) *kernel_busy_ns = st->kernel_busy_ns;
     return HJD_OK;
 }
 

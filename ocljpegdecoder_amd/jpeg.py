@@ -160,8 +160,10 @@ class JpegStream:
         rc = self.lib.hjd_stream_sync(self.handle, stats)
         self._keep.clear()
         check(rc, "hjd_stream_sync")
+        h2d_ns, kernel_ns = ctypes.c_int64(0), ctypes.c_int64(0)
+        check(self.lib.hjd_stream_busy(self.handle, ctypes.byref(h2d_ns), ctypes.byref(kernel_ns)), "hjd_stream_busy")
         return {"images": stats[0], "pixels": stats[1], "host_decode_ns": stats[2], "h2d_bytes": stats[3],
-                "kernel_launches": stats[4]}
+                "kernel_launches": stats[4], "h2d_busy_ns": h2d_ns.value, "kernel_busy_ns": kernel_ns.value}
 
     def close(self):
         if self.handle:

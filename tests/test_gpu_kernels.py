@@ -112,15 +112,20 @@ def test_16bit_quantisation_tables(hjd, ctx, mode, s):
     np.testing.assert_array_equal(got, _expect(O.decode_q16(coefs, qt, w, h, s), 0))
 
 
-@pytest.mark.parametrize("d16", ["0", "1"])
+@pytest.mark.parametrize("d16", ["0", "probe"])
 def test_444_gather_forms_vs_oracle(hjd, ctx, monkeypatch, d16):
     """4:4:4 persistent kernel with both coefficient-pair gathers: the
-    ds_read_u16_d16_hi | ds_read_u16 form (hjd::kVarD16, taken on sramecc+
-    devices) and the v_perm form (HJD_D16=0, and sramecc- devices)."""
+    ds_read_u16_d16_hi | ds_read_u16 form (hjd::kVarD16, taken where the
+    hardware probe passed: MI355X as deployed) and the v_perm form (HJD_D16=0,
+    and parts the probe did not pass)."""
     import torch
-    monkeypatch.setenv("HJD_D16", d16)
+    if d16 == "0":
+        monkeypatch.setenv("HJD_D16", "0")
+    else:
+        monkeypatch.delenv("HJD_D16", raising=False)
     arch = torch.cuda.get_device_properties(0).gcnArchName
-    print("device", arch, "d16 gather", d16 == "1" and "sramecc+" in arch)
+    print("device", arch, "d16 gather selected", ctx.d16_gather()[1])
+    assert ctx.d16_gather()[1] == (d16 != "0" and ctx.d16_gather()[0])
     for (w, h) in SIZES + [(3840, 64)]:
         coefs, qt = O.synthetic_coefs(w, h, 0, seed=7 * w + h)
         exp = O.decode_q16(coefs, qt, w, h, 0)
@@ -169,6 +174,38 @@ print("fallback ok")
     assert r.returncode == 0 and "fallback ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
 
 
+def test_d16_probe_hip_failure_is_not_sticky():
+    """a probe whose HIP calls fail (HJD_D16_PROBE=hipfail: its
+    allocation is one no device can satisfy -- a real hipErrorOutOfMemory)
+    must clear that error, must not cache the failure, and the next 4:4:4
+    launch must return HJD_OK with the oracle's pixels (v_perm kernels).  A
+    child process: the probe result is per process."""
+    import os
+    import subprocess
+    import sys
+    code = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, REPO); sys.path.insert(0, REPO + "/tests")
+import ocljpegdecoder_amd as hjd, oracle_py as O
+ctx = hjd.Context(0)                      # runs the probe: it fails inside HIP
+assert ctx.d16_gather() == (False, False), ctx.d16_gather()
+w, h = 1920, 1080
+for s in (0, 1):
+    coefs, qt = O.synthetic_coefs(w, h, s, seed=15 + s)
+    plan = hjd.Plan(ctx, [hjd.FrameSpec(w, h, s, qt_index=(0, 1, 2))], hjd.IN_Q16_ZIGZAG, qtables=qt)
+    plan.set_kernel(hjd.KERNEL_PERSISTENT)
+    out = torch.zeros((h, w), dtype=torch.int32, device="cuda")
+    plan.launch(torch.from_numpy(coefs).cuda(), out)   # raises if a stale HIP error surfaced
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), O.decode_q16(coefs, qt, w, h, s)), s
+print("hipfail ok")
+""".replace("REPO", repr(O.REPO))
+    env = {k: v for k, v in os.environ.items() if k != "HJD_D16"}
+    env["HJD_D16_PROBE"] = "hipfail"
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "hipfail ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
 @pytest.mark.parametrize("s", [0, 1])
 def test_autotune_keeps_pixels(hjd, ctx, s):
     """hjd_plan_autotune times the launch shapes (tasks per wave x store
@@ -187,8 +224,10 @@ def test_autotune_keeps_pixels(hjd, ctx, s):
     assert plan.tasks > 1024
     d_coefs = torch.from_numpy(np.ascontiguousarray(np.tile(coefs, (nf, 1)))).cuda()
     out = torch.zeros((nf, h, w), dtype=torch.int32, device="cuda")
+    hjd.autotune_cache_clear()
     tpw, var = plan.autotune(d_coefs, out)
-    print("autotune chose", tpw, "tasks per wave, variant", var)
+    print("autotune chose", tpw, "tasks per wave, variant", var, plan.launch_shape())
+    assert plan.launch_shape()["autotune_launches"] > 0 and not plan.launch_shape()["autotune_cached"]
     assert tpw in (1, 2, 4, 8, 16) and var in (0, 1)
     torch.cuda.synchronize()
     for i in range(nf):
@@ -201,40 +240,113 @@ def test_autotune_keeps_pixels(hjd, ctx, s):
     small = hjd.Plan(ctx, specs[:1], hjd.IN_Q16_ZIGZAG, qtables=qt)
     if small.tasks <= 1024:
         assert small.autotune(d_coefs, out) == (0, 0)
+        assert small.launch_shape()["kernel"] == "latency"
+    # a second plan of the same key takes the cached choice with no launch
+    again = hjd.Plan(ctx, specs, hjd.IN_Q16_ZIGZAG, qtables=qt)
+    assert again.autotune(d_coefs, out) == (tpw, var)
+    shape = again.launch_shape()
+    assert shape["autotune_launches"] == 0 and shape["autotune_cached"] == 1, shape
+    assert shape["tasks_per_wave"] == plan.launch_shape()["tasks_per_wave"]
+    assert shape["grid"] == plan.launch_shape()["grid"]
+    out.zero_()
+    again.launch(d_coefs, out)
+    torch.cuda.synchronize()
+    for i in range(nf):
+        np.testing.assert_array_equal(out[i].cpu().numpy().view(np.uint32), exp, err_msg=f"cached shape, frame {i}")
 
 
-@pytest.mark.parametrize("s", [0, 1])
-@pytest.mark.parametrize("chunk", [1, 3, 16])
-def test_chunking_vs_oracle(hjd, ctx, s, chunk):
-    """The persistent kernel's task chunks (hjd_plan_set_chunk, the shapes
-    hjd_plan_autotune picks from) must each decode every frame of a mixed
-    batch exactly once, bit-exact -- frames of different sizes (right and
-    bottom edge strips), qtables and output pitches, output guard bands
-    untouched, over repeated launches."""
-    import torch
-    tasks = chunk
+def _mixed_batch(hjd, s, guard=256):
+    """Frames of different sizes (right and bottom edge strips), qtables and
+    output pitches in one plan; returns (specs, coefs, qts, expected, bytes)."""
     sizes = [(1920, 1080), (313, 234), (3840, 64), (1000, 17), (1920, 1080), (257, 600)]
-    guard = 256
     specs, coefs, qts, exps, off_blk, off_b = [], [], [], [], 0, guard
     for i, (w, h) in enumerate(sizes):
         c, q = O.synthetic_coefs(w, h, s, seed=70 + i + 10 * s, quality_scale=0.6 + 0.2 * i)
         pitch = 4 * w + 16 * (i % 3)
         specs.append(hjd.FrameSpec(w, h, s, coef_offset=off_blk, out_offset=off_b, out_pitch=pitch,
                                    qt_index=(3 * i, 3 * i + 1, 3 * i + 2)))
-        coefs.append(c); qts.append(q); exps.append((O.decode_q16(c, q, w, h, s), off_b, pitch))
+        coefs.append(c); qts.append(q); exps.append((O.decode_q16(c, q, w, h, s), off_b, pitch, w, h))
         off_blk += c.shape[0]; off_b += pitch * h + guard
-    plan = hjd.Plan(ctx, specs, hjd.IN_Q16_ZIGZAG, qtables=np.concatenate(qts))
+    return specs, np.concatenate(coefs), np.concatenate(qts), exps, off_b
+
+
+def _check_mixed(buf, exps, what):
+    full = buf.cpu().numpy()
+    mask = np.ones(full.shape, bool)
+    for e, off, pitch, w, h in exps:
+        img = full[off:off + pitch * h].reshape(h, pitch)[:, :4 * w]
+        np.testing.assert_array_equal(np.ascontiguousarray(img).view(np.uint32), e, err_msg=f"{w}x{h} {what}")
+        mask[off:off + pitch * h].reshape(h, pitch)[:, :4 * w] = False
+    assert (full[mask] == 0x5A).all(), f"write outside the frames ({what})"
+
+
+@pytest.mark.parametrize("s", [0, 1])
+def test_every_autotune_candidate_vs_oracle(hjd, ctx, s):
+    """every launch shape hjd_plan_autotune can pick --
+    1/2/4/8/16 tasks per wave x nt/plain stores, and the workgroup-interleaved
+    order with each -- decodes a mixed batch bit-exactly, applied through
+    hjd_plan_set_chunk x hjd_plan_set_variant; the shape the plan reports is
+    the one asked for (set_chunk pins the chunk exactly, so chunks > 1 really
+    run, across frame boundaries and edge strips)."""
+    import torch
+    specs, coefs, qts, exps, nbytes = _mixed_batch(hjd, s)
+    plan = hjd.Plan(ctx, specs, hjd.IN_Q16_ZIGZAG, qtables=qts)
     plan.set_kernel(hjd.KERNEL_PERSISTENT)
-    plan.set_chunk(tasks)
-    d_coefs = torch.from_numpy(np.concatenate(coefs)).cuda()
-    buf = torch.full((off_b,), 0x5A, dtype=torch.uint8, device="cuda")
+    d_coefs = torch.from_numpy(coefs).cuda()
+    buf = torch.empty((nbytes,), dtype=torch.uint8, device="cuda")
+    for chunk in (1, 2, 4, 8, 16):
+        for variant in (0, 1, 2, 3):
+            plan.set_chunk(chunk)
+            plan.set_variant(variant)
+            shape = plan.launch_shape()
+            waves = -(-plan.tasks // chunk)
+            assert shape["tasks_per_wave"] == chunk and shape["grid"] == -(-waves // 4), shape
+            if variant & 2 == 0:
+                assert shape["max_tasks_per_wave"] == -(-plan.tasks // (4 * shape["grid"])), shape
+                assert chunk == 1 or shape["max_tasks_per_wave"] > 1, shape
+            buf.fill_(0x5A)
+            plan.launch(d_coefs, buf)
+            torch.cuda.synchronize()
+            _check_mixed(buf, exps, f"chunk {chunk} variant {variant}")
+
+
+@pytest.mark.parametrize("s", [0, 1])
+@pytest.mark.parametrize("chunk", [1, 3, 16])
+def test_chunking_vs_oracle(hjd, ctx, s, chunk):
+    """The persistent kernel's task chunks (hjd_plan_set_chunk) must each
+    decode every frame of a mixed batch exactly once, bit-exact -- frames of
+    different sizes (right and bottom edge strips), qtables and output pitches,
+    output guard bands untouched, over repeated launches.  The chunk applied is
+    the one asked for (no occupancy floor on a pinned chunk)."""
+    import torch
+    specs, coefs, qts, exps, nbytes = _mixed_batch(hjd, s)
+    plan = hjd.Plan(ctx, specs, hjd.IN_Q16_ZIGZAG, qtables=qts)
+    plan.set_kernel(hjd.KERNEL_PERSISTENT)
+    plan.set_chunk(chunk)
+    assert plan.launch_shape()["tasks_per_wave"] == chunk
+    assert plan.launch_shape()["max_tasks_per_wave"] >= min(chunk, 2) or chunk == 1
+    d_coefs = torch.from_numpy(coefs).cuda()
+    buf = torch.full((nbytes,), 0x5A, dtype=torch.uint8, device="cuda")
     for rep in range(3):
         plan.launch(d_coefs, buf)
     torch.cuda.synchronize()
-    full = buf.cpu().numpy()
-    mask = np.ones(full.shape, bool)
-    for (e, off, pitch), (w, h) in zip(exps, sizes):
-        img = full[off:off + pitch * h].reshape(h, pitch)[:, :4 * w]
-        np.testing.assert_array_equal(np.ascontiguousarray(img).view(np.uint32), e, err_msg=f"{w}x{h} {chunk}")
-        mask[off:off + pitch * h].reshape(h, pitch)[:, :4 * w] = False
-    assert (full[mask] == 0x5A).all(), "write outside the frames"
+    _check_mixed(buf, exps, f"chunk {chunk}")
+
+
+def test_set_chunk_keeps_latency_kernel_for_small_auto_plans(hjd, ctx):
+    """hjd_plan_set_chunk applies to persistent launches; a small
+    HJD_KERNEL_AUTO plan keeps the latency kernel (as hjd_plan_autotune
+    leaves it), with the oracle's pixels."""
+    import torch
+    w, h = 1920, 1080
+    coefs, qt = O.synthetic_coefs(w, h, 1, seed=33)
+    plan = hjd.Plan(ctx, [hjd.FrameSpec(w, h, 1, qt_index=(0, 1, 2))], hjd.IN_Q16_ZIGZAG, qtables=qt)
+    assert plan.tasks <= 1024
+    plan.set_chunk(4)
+    assert plan.launch_shape()["kernel"] == "latency"
+    out = torch.zeros((h, w), dtype=torch.int32, device="cuda")
+    plan.launch(torch.from_numpy(coefs).cuda(), out)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), O.decode_q16(coefs, qt, w, h, 1))
+    plan.set_kernel(hjd.KERNEL_PERSISTENT)
+    assert plan.launch_shape()["kernel"] == "persistent" and plan.launch_shape()["tasks_per_wave"] == 4

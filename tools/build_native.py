@@ -53,20 +53,13 @@ def _headers():
     return hs
 
 
-def build(verbose: bool = False, force: bool = False, ablation: bool = False, variant: str = "",
+def build(verbose: bool = False, force: bool = False, variant: str = "",
           defines=(), record: bool = False) -> str:
-    """ablation=True builds the TUNING-ONLY library build/ablation/libhjd.so with
-    -DHJD_ABLATION (stage-skipping kernel variants for tools/tune.py; wrong
-    outputs by design).  Load it with HJD_LIB=build/ablation/libhjd.so.
-    variant="name", defines=("FLAG", ...) builds an A/B library
-    build/variants/<name>/libhjd.so with -DFLAG (tuning only)."""
+    """variant="name", defines=("FLAG", ...) builds an A/B library
+    build/variants/<name>/libhjd.so with -DFLAG (tuning only; load it with
+    HJD_LIB=build/variants/<name>/libhjd.so)."""
     global LIBDIR, LIB, OBJDIR
-    if ablation:
-        LIBDIR = os.path.join(REPO, "build", "ablation")
-        LIB = os.path.join(LIBDIR, "libhjd.so")
-        OBJDIR = os.path.join(REPO, "build", "obj_ablation")
-        COMMON.append("-DHJD_ABLATION")
-    elif variant:
+    if variant:
         LIBDIR = os.path.join(REPO, "build", "variants", variant)
         LIB = os.path.join(LIBDIR, "libhjd.so")
         OBJDIR = os.path.join(REPO, "build", "obj_variants", variant)
@@ -122,5 +115,4 @@ if __name__ == "__main__":
     if "--variant" in sys.argv:
         var = sys.argv[sys.argv.index("--variant") + 1]
         defs = [a[2:] for a in sys.argv if a.startswith("-D")]
-    print(build(verbose=True, force="--force" in sys.argv, ablation="--ablation" in sys.argv, variant=var,
-                defines=defs))
+    print(build(verbose=True, force="--force" in sys.argv, variant=var, defines=defs))

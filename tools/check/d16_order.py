@@ -13,7 +13,8 @@ it is done when k <= the number of DS instructions issued after it (every
 younger DS op is still counted while the d16 op is pending).  SMEM ops share
 the counter but may complete out of order, so they are not counted as cover.
 
-This script extracts the gfx950 code objects from the library (llvm-objdump
+This script extracts the code objects of the build's architecture (HJD_ARCH,
+default gfx950, as tools/build_native.py) from the library (llvm-objdump
 --offloading, in a temporary directory), disassembles them and checks every
 ds_read_u16_d16_hi in program order: the destination register must not
 appear in any operand (read, copy or overwrite) before a covering wait, and
@@ -33,22 +34,24 @@ import tempfile
 LLVM_OBJDUMP = os.environ.get("LLVM_OBJDUMP", "/opt/rocm/lib/llvm/bin/llvm-objdump")
 REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 DEFAULT_LIB = os.path.join(REPO, "ocljpegdecoder_amd", "lib", "libhjd.so")
+# the architecture the library was built for (tools/build_native.py ARCH)
+ARCH = os.environ.get("HJD_ARCH", "gfx950")
 
 _FUNC = re.compile(r"^[0-9a-f]+ <([^>]+)>:")
 _VREG = re.compile(r"\bv(\d+)\b|\bv\[(\d+):(\d+)\]")
 _BRANCH = ("s_branch", "s_cbranch", "s_setpc", "s_swappc", "s_endpgm")
 
 
-def disassemble(lib_path: str) -> str:
-    """Disassembly text of every gfx950 code object bundled in lib_path."""
+def disassemble(lib_path: str, arch: str = ARCH) -> str:
+    """Disassembly text of every `arch` code object bundled in lib_path."""
     tmp = tempfile.mkdtemp(prefix="hjd_d16chk_")
     try:
         dst = os.path.join(tmp, os.path.basename(lib_path))
         shutil.copy(lib_path, dst)
         subprocess.run([LLVM_OBJDUMP, "--offloading", dst], cwd=tmp, check=True, capture_output=True)
         texts = []
-        for co in sorted(glob.glob(os.path.join(tmp, "*gfx950*"))):
-            r = subprocess.run([LLVM_OBJDUMP, "-d", "--mcpu=gfx950", co], check=True, capture_output=True, text=True)
+        for co in sorted(glob.glob(os.path.join(tmp, f"*{arch}*"))):
+            r = subprocess.run([LLVM_OBJDUMP, "-d", f"--mcpu={arch}", co], check=True, capture_output=True, text=True)
             texts.append(r.stdout)
         return "\n".join(texts)
     finally:
