@@ -88,6 +88,17 @@ int hjd_stream_sync(hjd_stream* s, int64_t stats[5]);
  * Divided by a wall-clock interval it is the fraction of the time the host
  * Huffman workers kept the copy engine / the kernel fed. */
 int hjd_stream_busy(hjd_stream* s, int64_t* h2d_busy_ns, int64_t* kernel_busy_ns);
+
+/* Host CPUs of one GPU's worker pool (both stream kinds bind their workers to
+ * them; HJD_NUMA=0 disables the binding): the GPUs on the same NUMA node, in
+ * PCI bus-id order, split that node's CPUs into equal contiguous slices; with
+ * fewer CPUs than GPUs they share the node.  This hook computes the split for
+ * GPU `bus` among `gpus` from a sysfs tree at `sysfs_root` ("" or NULL: the
+ * real one; a test passes a fake topology), optionally intersected with this
+ * process's affinity.  Writes up to `capacity` CPU ids; *ncpus = how many
+ * (0: unknown topology, no binding). */
+int hjd_debug_worker_cpus(const char* sysfs_root, const char* bus, const char* const* gpus, int ngpus,
+                          int only_allowed, int32_t* cpus, int capacity, int32_t* ncpus);
 /* Pixel format of subsequent submits: HJD_OUT_BGRX (default) or HJD_OUT_BGR24
  * (d_out 4-byte aligned, pitch >= 3*width); jobs already queued keep theirs. */
 int hjd_stream_set_output_format(hjd_stream* s, int out_format);

@@ -36,6 +36,7 @@ from .backend import (  # noqa: E402
     device_count,
     frame_blocks,
     mcu_geometry,
+    worker_cpus,
 )
 
 from .jpeg import (GpuDecoder, GpuJpegStream, JpegInfo, JpegStream, bmp_bytes, bmp_header,  # noqa: E402
@@ -46,6 +47,6 @@ __all__ = [
     "GpuDecoder", "GpuJpegStream", "JpegInfo", "JpegStream", "bmp_bytes", "bmp_header", "decode_coefs",
     "decode_coefs_batch", "decode_coefs_into", "decode_jpeg", "emulate_entropy",
     "parse", "pinned_bytes",
-    "Context", "FrameSpec", "Plan", "autotune_cache_clear", "decode_frame", "device_count", "frame_blocks", "mcu_geometry",
+    "Context", "FrameSpec", "Plan", "autotune_cache_clear", "decode_frame", "device_count", "frame_blocks", "mcu_geometry", "worker_cpus",
     "YUV444", "YUV420", "YUV422", "GRAY", "YUV411_H4V1", "YUV440", "OTHER", "block_components", "KERNEL_AUTO", "KERNEL_PERSISTENT", "KERNEL_LATENCY", "OUT_BGRX", "OUT_BGR24", "OUT_BYTES", "default_pitch", "IN_Q16_ZIGZAG", "IN_I32_NATURAL",
 ]

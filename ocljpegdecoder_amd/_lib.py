@@ -154,6 +154,8 @@ def _bind_host(lib):
         "hjd_stream_submit": (ctypes.c_int, [vp, u8p, ctypes.c_size_t, vp, ctypes.c_int32]),
         "hjd_stream_sync": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int64)]),
         "hjd_stream_busy": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
+        "hjd_debug_worker_cpus": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p),
+                                                 ctypes.c_int, ctypes.c_int, c_i32p, ctypes.c_int, c_i32p]),
         "hjd_gdec_create": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
                                            ctypes.POINTER(vp)]),
         "hjd_gdec_destroy": (ctypes.c_int, [vp]),

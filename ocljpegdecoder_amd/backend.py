@@ -278,6 +278,20 @@ class Plan:
             pass
 
 
+def worker_cpus(bus: str, gpus: Sequence[str], sysfs_root: Optional[str] = None, only_allowed: bool = False):
+    """hjd_debug_worker_cpus: the host CPUs the worker pool of the GPU at PCI
+    address `bus` binds to, among the GPUs `gpus` (its NUMA node's CPUs split
+    per GPU of that node), from the sysfs tree at `sysfs_root` (None: the real one)."""
+    lib = _lib.load()
+    arr = (ctypes.c_char_p * max(1, len(gpus)))(*[g.encode() for g in gpus])
+    cap = 4096
+    out = (ctypes.c_int32 * cap)()
+    n = ctypes.c_int32(0)
+    check(lib.hjd_debug_worker_cpus(sysfs_root.encode() if sysfs_root else None, bus.encode(), arr, len(gpus),
+                                    int(only_allowed), out, cap, ctypes.byref(n)), "hjd_debug_worker_cpus")
+    return list(out[:min(n.value, cap)])
+
+
 def autotune_cache_clear():
     """Forget every cached hjd_plan_autotune choice of this process."""
     check(_lib.load().hjd_autotune_cache_clear(), "hjd_autotune_cache_clear")

@@ -137,3 +137,45 @@ def test_stream_leg_command(world):
     assert env["PATH"] == "/usr/bin"
     # small runs (tests) still time >= 3 steps
     assert bench.stream_leg_command(world, "gloo", 10, 12, 1, environ)[2] == 3
+
+
+def test_eight_rank_torchrun_rehearsal(tmp_path):
+    """bench.py's N = 8 bookkeeping, launched the way the
+    driver launches the 8-GPU bench (python -m torch.distributed.run
+    --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1), over gloo on CPU:
+    timed_region's max over 8 ranks, each global frame id of a stream step
+    decoded by exactly one of the 8 ranks, checksums summed over all 8 (one bad
+    rank fails the whole check), the config-5 child commands (both stream legs)
+    for N = 8 with this rank's torchrun identity scrubbed, and rank 0 seeing
+    its 7 siblings gone before it would start the child run."""
+    import json
+    import subprocess
+    world = 8
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "1"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "tests", "bench_rank_worker.py"), str(tmp_path)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    res = [json.load(open(tmp_path / f"rank{k}.json")) for k in range(world)]
+    walls = [x["wall"] for x in res]
+    assert sorted(x["rank"] for x in res) == list(range(world))
+    assert sorted(x["local_rank"] for x in res) == list(range(world))
+    assert len({x["ppid"] for x in res}) == 1                      # one torchrun agent
+    for x in res:
+        assert x["world"] == world and x["nsync"] == 2
+        assert x["wall_max"] == max(walls) and x["wall_max"] >= 0.16
+        assert x["ok"] and not x["ok_bad"]                         # a single bad rank fails everyone's check
+        assert x["agg"]["frames_checked"] == 6 * world
+        G = 6 * world
+        assert x["agg"]["id_sum"] == sum(range(2 * G, 3 * G))
+        assert x["steps"] == 13 and x["steps_host"] == 10          # 100,000 / (1024 x 8); 10,240 / (128 x 8)
+        assert x["env_torchrun_keys"] == [] and x["env_master_addr"] == "127.0.0.1"
+        for c, wl in ((x["cmd"], "stream4k420"), (x["cmd_host"], "stream4k420_host")):
+            assert c[1:3] == ["-m", "torch.distributed.run"] and c[c.index("--nproc-per-node") + 1] == "8"
+            assert c[c.index("--workload") + 1] == wl and c[c.index("--gpus") + 1] == "8"
+    for k in range(3):
+        allids = sorted(i for x in res for i in x["ids"][k])
+        assert allids == list(range(6 * world * k, 6 * world * (k + 1)))
+    assert res[0]["siblings_alive"] == 0
