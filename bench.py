@@ -1108,8 +1108,10 @@ def pixel_batch(args, wl, hjd, torch, dist, world, rank, dev, qt, steps, warmup,
         tpw, var = plan.autotune(coefs, out, stream)
         launch = {"autotuned": tpw > 0, "tasks_per_wave": tpw or None, "variant": var,
                   "stores": "plain" if var & 1 else "nt", "seconds": round(time.perf_counter() - t0, 2),
+                  "shape": plan.launch_shape(),
                   "how": "hjd_plan_autotune: 1/2/4/8/16 tasks per wave x nt/plain stores, 2 interleaved rounds of "
-                         "one warm + two timed launches each on this run's buffers; fastest kept"}
+                         "one warm + two timed launches each on this run's buffers; fastest kept (cached per "
+                         "process by shape)"}
     for _ in range(warmup):
         plan.launch(coefs, out, stream, grid_blocks=args.grid)
     torch.cuda.synchronize()

@@ -24,9 +24,14 @@ def _free_port():
 
 
 def _run(workload, frames, extra=(), ranks=2, steps=3, timeout=110):
+    """Rank 0's one stdout line; for the pixel workloads, whose line is the
+    compact one, the full result from the --detail-out file (with the line
+    itself under "_line")."""
+    import tempfile
     env = dict(os.environ, HJD_BENCH_SAME_DEVICE="1", MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="4")
+    detail = os.path.join(tempfile.mkdtemp(prefix="hjd_bench_"), "detail.json")
     args = [os.path.join(ROOT, "bench.py"), "--gpus", str(ranks), "--steps", str(steps), "--warmup", "1",
-            "--workload", workload, "--frames", str(frames), "--no-cpu", *extra]
+            "--workload", workload, "--frames", str(frames), "--no-cpu", "--detail-out", detail, *extra]
     if ranks == 1:
         cmd = [sys.executable, *args]
     else:
@@ -36,7 +41,13 @@ def _run(workload, frames, extra=(), ranks=2, steps=3, timeout=110):
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, p.stdout[-3000:]           # rank 0 only, one line
-    return json.loads(lines[0])
+    line = json.loads(lines[0])
+    if not os.path.exists(detail):
+        return line
+    full = json.load(open(detail))
+    assert full["value"] == line["value"] and line["detail"] == detail
+    full["_line"] = line
+    return full
 
 
 @pytest.mark.gpu
@@ -47,7 +58,7 @@ def test_two_ranks_pixel_bench():
     extra_env = {"HJD_BENCH_STREAM_FRAMES": "12", "HJD_STREAM_POOL": "8"}
     os.environ.update(extra_env)
     try:
-        r = _run("4k420", 8, extra=("--stream-frame-ids", "72"), timeout=240)
+        r = _run("4k420", 8, extra=("--stream-frame-ids", "72", "--stream-host-frame-ids", "48"), timeout=300)
     finally:
         for k in extra_env:
             os.environ.pop(k, None)
@@ -69,6 +80,16 @@ def test_two_ranks_pixel_bench():
     # the child ranks started on GPUs the parent's ranks had left and released
     assert s5["parent_ranks_alive_at_start"] == 0
     assert s5["hbm_at_start"]["wait_s_max_over_ranks"] < 60, s5["hbm_at_start"]
+    # the north star's host-Huffman pipeline over the same 2 ranks
+    sh = r["config5_stream_host"]
+    assert "error" not in sh, sh
+    assert sh["n_gpus"] == 2 and sh["output_checked_vs_oracle"] is True and sh["timed_frame_ids"] == 48
+    p = sh["pipeline"]
+    assert 0 < p["kernel_busy_frac"] <= 1 and 0 < p["h2d_busy_frac"] <= 1 and p["h2d_GBps"] > 0, p
+    # the compact stdout line carries every leg's headline
+    sm = r["_line"]["summary"]
+    assert sm["4k444"]["Mpx_s"] == c4["value"] and sm["c5_host_huffman"]["Mpx_s"] == sh["value"]
+    assert r["_line"]["output_checked_vs_oracle"] is True
 
 
 @pytest.mark.gpu
