@@ -752,9 +752,6 @@ __device__ __forceinline__ SubStats wave_reduce_ordered(SubStats v, int lane)
     return v;
 }
 
-#ifndef HJD_STEPS
-#define HJD_STEPS 1   // sync runs take the AC step tables (A/B hook: 0 = one unit per step)
-#endif
 
 // LDS layout of the sync kernel after the group's tables (dynamic shared memory).
 struct SyncLds {
@@ -786,7 +783,7 @@ __global__ __launch_bounds__(kGroupSubs) void ent_sync_kernel(EntBatchDev b)
     // groups laid out for a device-destuffed frame's upper bound (raw bytes) past its real end
     if (gl >= frame_groups(F.nsub)) return;
     __shared__ BlockInfo blocks[kMaxBpm];
-    const RunCtx c = make_ctx(b, F, tabs, blocks, HJD_STEPS ? steps : nullptr);
+    const RunCtx c = make_ctx(b, F, tabs, blocks, steps);
     load_tables(tabs, blocks, b.tabs + F.tab_base, F, b.frames + f, tid, kGroupSubs);
     copy_steps(steps, b, F, tid, kGroupSubs);
     if (tid < 2) L.nlist[tid] = 0;
@@ -1058,14 +1055,6 @@ __device__ __forceinline__ SlotRow row_compose(const SlotRow& f, const SlotRow& 
 __global__ __launch_bounds__(kChainThreads) void ent_chain_kernel(EntBatchDev b)
 {
     __shared__ ChainLds L;
-#ifdef HJD_CHAIN_PROFILE   // tuning build: phase timestamps (100 MHz) printed by block 0
-    uint64_t tp[48];
-    int np = 0;
-#define CHAIN_T() do { if (threadIdx.x == 0 && blockIdx.x == 0 && np < 48) tp[np++] = __builtin_amdgcn_s_memrealtime(); } while (0)
-#else
-#define CHAIN_T() do {} while (0)
-#endif
-    CHAIN_T();
     const int tid = threadIdx.x;
     const uint32_t f = blockIdx.x;
     const EntFrame F = b.frames[f];
@@ -1103,14 +1092,12 @@ __global__ __launch_bounds__(kChainThreads) void ent_chain_kernel(EntBatchDev b)
             }
             if (tid == 0) L.brk = ~0ull;
             __syncthreads();
-            CHAIN_T();
             SlotRow v = ident;
 #pragma unroll 1
             for (uint32_t r = r0; r < r0 + kChainRows && r < cn; ++r) v = row_compose(v, row_load(L.rows[r]));
 #pragma unroll
             for (int i = 0; i < kRowWords; ++i) L.fn[0][tid][i] = v.w[i];
             __syncthreads();
-            CHAIN_T();
             int cur = 0;
 #pragma unroll 1
             for (int d = 1; d < kChainThreads; d <<= 1) {   // inclusive: fn[t] = thread 0's rows then ... then t's
@@ -1121,7 +1108,6 @@ __global__ __launch_bounds__(kChainThreads) void ent_chain_kernel(EntBatchDev b)
                 cur ^= 1;
                 __syncthreads();
             }
-            CHAIN_T();
             const uint32_t carry = L.carry;
             slot = tid == 0 ? carry : (carry == kNoCand ? kNoCand : row_get(row_load(L.fn[cur][tid - 1]), carry));
             // the first subsequence without a slot: the row whose map sends the
@@ -1136,7 +1122,6 @@ __global__ __launch_bounds__(kChainThreads) void ent_chain_kernel(EntBatchDev b)
                 s = nx;
             }
             __syncthreads();
-            CHAIN_T();
             const unsigned long long brk = L.brk;
             if (brk == ~0ull) break;
             if (!L.tables_loaded) {   // the frame's tables, for the repair runs (rare)
@@ -1166,7 +1151,6 @@ __global__ __launch_bounds__(kChainThreads) void ent_chain_kernel(EntBatchDev b)
             for (uint32_t i = 0; i < kChainRows && r0 + i < cn; ++i) out[i] = static_cast<uint8_t>(packed[i >> 2] >> ((i & 3) * 8));
         }
         __syncthreads();
-        CHAIN_T();
         if (r0 < cn && (r0 + kChainRows >= cn)) L.carry = s;   // the thread holding the chunk's last row
     }
     __syncthreads();
@@ -1190,17 +1174,7 @@ __global__ __launch_bounds__(kChainThreads) void ent_chain_kernel(EntBatchDev b)
             b.linked[w] = 1u;
         }
     }
-#ifdef HJD_CHAIN_PROFILE
-    __syncthreads();
-    CHAIN_T();
-    if (threadIdx.x == 0 && blockIdx.x == 0) {
-        printf("chain n=%u:", n);
-        for (int i = 1; i < np; ++i) printf(" %d", static_cast<int>(tp[i] - tp[i - 1]));
-        printf("\n");
-    }
-#endif
 }
-#undef CHAIN_T
 
 __global__ __launch_bounds__(256) void ent_link_kernel(EntBatchDev b)
 {

@@ -39,10 +39,9 @@ namespace hjd {
 namespace ent {
 
 constexpr int kLutBits = 10;                    // first-level lookup width
-#ifndef HJD_STEP_BITS
-#define HJD_STEP_BITS 11   // same-box: 11 bits best on the stream, 12 on a lone batch (profiles/r02_entropy_step_bits_ab.json)
-#endif
-constexpr int kStepBits = HJD_STEP_BITS;        // sync-mode AC step table width (>= kLutBits, <= 15)
+// sync-mode AC step table width (>= kLutBits, <= 15); same-box: 11 bits best on the
+// stream, 12 on a lone batch (profiles/r02_entropy_step_bits_ab.json)
+constexpr int kStepBits = 11;
 constexpr int kMaxTables = 6;                   // DC+AC per component at most
 constexpr int kGroupSubs = 256;                 // subsequences per workgroup (one per thread)
 constexpr int kWarm = 8;                        // leading subsequences a group shares with its predecessor

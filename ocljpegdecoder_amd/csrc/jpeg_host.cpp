@@ -3,7 +3,7 @@
 // Produces the fused kernel's input (int16 quantised zigzag coefficients,
 // MCU-major) from a baseline JPEG.  Covers the reference's L2/L3
 // (src/parser.cpp:7-419, src/decoder.cpp:72-365) with a fresh table-driven
-// design: a 64-bit bit accumulator with byte de-stuffing, a 9-bit first-level
+// design: a 64-bit bit accumulator with byte de-stuffing, a kFastBits first-level
 // lookup per Huffman table (canonical MAXCODE/VALPTR search for longer codes,
 // JPEG Annex F.2.2.3), restart-marker resynchronisation, and a thread pool
 // that decodes independent files in parallel.
@@ -20,12 +20,19 @@ using hjd_internal::set_error;
 
 namespace {
 
+#ifndef HJD_HOST_FAST_BITS
+#define HJD_HOST_FAST_BITS 9
+#endif
+constexpr int kFastBits = HJD_HOST_FAST_BITS;   // first-level lookup width (9..12)
+constexpr int kFast = 1 << kFastBits;
+
 struct HuffTable {
     bool defined = false;
     uint8_t counts[16];      // the DHT spec, kept for the GPU tables (hjd_entropy.hip)
     int nsym = 0;
-    uint16_t fast[512];      // (length << 8) | symbol for codes of <= 9 bits; 0 = slow path
-    int32_t fast_ac[512];    // AC: (value << 16) | (run << 5) | (code + extra bits) when those fit 9 bits, else 0
+    uint16_t fast[kFast];    // (length << 8) | symbol for codes of <= kFastBits bits; 0 = slow path
+    // AC: (value << 16) | (run << 5) | (code + extra bits) when those fit kFastBits, else 0
+    int32_t fast_ac[kFast];
     int32_t maxcode[18];     // largest code of each length (-1: none)
     int32_t valptr[17];
     int32_t mincode[17];
@@ -76,8 +83,8 @@ int build_table(HuffTable& t, const uint8_t counts[16], const uint8_t* symbols, 
             if (k >= nsym) return -1;
             if (code >= (1 << len)) return -1;   // over-subscribed table
             t.vals[k] = symbols[k];
-            if (len <= 9) {
-                const int shift = 9 - len;
+            if (len <= kFastBits) {
+                const int shift = kFastBits - len;
                 for (int j = 0; j < (1 << shift); ++j)
                     t.fast[(code << shift) | j] = static_cast<uint16_t>((len << 8) | symbols[k]);
             }
@@ -87,14 +94,14 @@ int build_table(HuffTable& t, const uint8_t counts[16], const uint8_t* symbols, 
     }
     t.maxcode[17] = 0x7fffffff;
     // combined AC entries: symbol and its extra bits in one lookup (nonzero
-    // coefficients whose code + magnitude bits fit the 9-bit index)
+    // coefficients whose code + magnitude bits fit the kFastBits index)
     memset(t.fast_ac, 0, sizeof(t.fast_ac));
-    for (int idx = 0; idx < 512; ++idx) {
+    for (int idx = 0; idx < kFast; ++idx) {
         const uint16_t e = t.fast[idx];
         if (!e) continue;
         const int len = e >> 8, rs = e & 0xFF, run = rs >> 4, size = rs & 15;
-        if (size == 0 || len + size > 9) continue;
-        const int bits = (idx >> (9 - len - size)) & ((1 << size) - 1);
+        if (size == 0 || len + size > kFastBits) continue;
+        const int bits = (idx >> (kFastBits - len - size)) & ((1 << size) - 1);
         const int value = bits < (1 << (size - 1)) ? bits - (1 << size) + 1 : bits;
         t.fast_ac[idx] = static_cast<int32_t>((static_cast<uint32_t>(value) << 16) | (run << 5) | (len + size));
     }
@@ -382,13 +389,13 @@ struct BitReader {
 inline int decode_symbol(BitReader& br, const HuffTable& t)
 {
     if (br.nbits < 16) br.refill();
-    const uint16_t e = t.fast[br.peek(9)];
+    const uint16_t e = t.fast[br.peek(kFastBits)];
     if (e) {
         br.skip(e >> 8);
         return e & 0xFF;
     }
     const uint32_t code16 = br.peek(16);
-    for (int len = 10; len <= 16; ++len) {
+    for (int len = kFastBits + 1; len <= 16; ++len) {
         const int32_t c = static_cast<int32_t>(code16 >> (16 - len));
         if (c <= t.maxcode[len]) {
             br.skip(len);
@@ -412,7 +419,7 @@ inline int receive_extend(BitReader& br, int s)
 inline bool decode_block(BitReader& br, const HuffTable& dc, const HuffTable& ac, int& pred, int16_t* out)
 {
     if (br.nbits < 16) br.refill();
-    const int32_t fd = dc.fast_ac[br.peek(9)];   // a DC table's symbols are sizes: run 0
+    const int32_t fd = dc.fast_ac[br.peek(kFastBits)];   // a DC table's symbols are sizes: run 0
     if (fd) {
         br.skip(fd & 31);
         pred += fd >> 16;
@@ -426,7 +433,7 @@ inline bool decode_block(BitReader& br, const HuffTable& dc, const HuffTable& ac
     out[0] = static_cast<int16_t>(pred);
     for (int k = 1; k < 64;) {
         if (br.nbits < 16) br.refill();
-        const int32_t fe = ac.fast_ac[br.peek(9)];
+        const int32_t fe = ac.fast_ac[br.peek(kFastBits)];
         if (fe) {   // run + nonzero coefficient in one lookup
             br.skip(fe & 31);
             k += (fe >> 5) & 15;
@@ -570,7 +577,7 @@ inline bool ac_first(BitReader& br, const HuffTable& ac, const ScanSpec& sc, int
     }
     for (int k = sc.ss; k <= sc.se;) {
         if (br.nbits < 16) br.refill();
-        const int32_t fe = ac.fast_ac[br.peek(9)];
+        const int32_t fe = ac.fast_ac[br.peek(kFastBits)];
         if (fe) {   // run + nonzero coefficient in one lookup
             br.skip(fe & 31);
             k += (fe >> 5) & 15;
