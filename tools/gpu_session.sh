@@ -10,7 +10,8 @@
 #   bench[:<bench args>]         python bench.py <args> (default: the driver's
 #                                command), bench.json + bench.err + bench_detail.json
 #   ktrace:<workload>[:<args>]   rocprofv3 --kernel-trace --stats of bench.py
-#                                --workload <workload> --no-cpu --no-stream <args>
+#                                --workload <workload> --no-cpu --no-stream <args>;
+#                                ktrace:default traces the driver's own command (python bench.py)
 #   pmc:<workload>               HBM bytes: FETCH_SIZE / WRITE_SIZE passes (tools/pmc/traffic.txt)
 #   sq:<workload>[:<args>]       SQ counters of the fused kernel (tools/pmc/pixel.txt),
 #                                256 frames at the default launch shape
@@ -48,8 +49,10 @@ for step in "$@"; do
           > "$O/bench.json" 2> "$O/bench.err") || fail bench "$O/bench.err"
       cat "$O/bench.json" ;;
     ktrace)
-      (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/ktrace_$a1" -o bench -- \
-          python3 "$R/bench.py" --workload "$a1" --no-cpu --no-stream ${a2//,/ } --detail-out "$O/ktrace_$a1.detail.json" \
+      # ktrace:default = the driver's own command (python bench.py), every leg
+      if [ "$a1" = default ]; then BA=(); else BA=(--workload "$a1" --no-cpu --no-stream); fi
+      (cd /tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/ktrace_$a1" -o bench -- \
+          python3 "$R/bench.py" "${BA[@]}" ${a2//,/ } --detail-out "$O/ktrace_$a1.detail.json" \
           > "$O/ktrace_$a1.json" 2> "$O/ktrace_$a1.err") || fail ktrace "$O/ktrace_$a1.err"
       tail -c 400 "$O/ktrace_$a1.json" ;;
     pmc)

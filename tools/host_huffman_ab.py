@@ -2,7 +2,9 @@
 builds: each round runs every library in its own process on the same pool of
 synthetic 4K q90 JPEGs (bench.encode_pool), 1 thread and N threads.
 
-    python tools/host_huffman_ab.py lib1.so,lib2.so [--rounds 3] [--threads 16] [--sampling 1]
+    python tools/host_huffman_ab.py product+build/variants/x/libhjd.so [--rounds 3] [--threads 16] [--sampling 1]
+
+("product" = the in-tree library; libraries separated by '+').
 """
 import argparse
 import json
@@ -42,7 +44,7 @@ def main():
     a = ap.parse_args()
     rows = []
     for r in range(a.rounds):
-        for lib in a.libs.split(","):
+        for lib in a.libs.split("+"):
             env = dict(os.environ)
             if lib != "product":
                 env["HJD_LIB"] = os.path.join(REPO, lib)
@@ -54,7 +56,7 @@ def main():
             rows.append({"round": r, "lib": lib, **d})
             print(json.dumps(rows[-1]), file=sys.stderr, flush=True)
     summary = {}
-    for lib in a.libs.split(","):
+    for lib in a.libs.split("+"):
         mine = [x for x in rows if x["lib"] == lib]
         summary[lib] = {k: [x[k] for x in mine] for k in ("one_thread", "threads")}
     print(json.dumps({"what": "host Huffman Mpx/s (4K q90 synthetic, bench.encode_pool)", "threads": a.threads,
