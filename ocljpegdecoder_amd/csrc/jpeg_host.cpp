@@ -21,9 +21,11 @@ using hjd_internal::set_error;
 namespace {
 
 #ifndef HJD_HOST_FAST_BITS
-#define HJD_HOST_FAST_BITS 9
+#define HJD_HOST_FAST_BITS 11
 #endif
-constexpr int kFastBits = HJD_HOST_FAST_BITS;   // first-level lookup width (9..12)
+// first-level lookup width: 11 bits, +10 % per thread over 9 (EPYC 9575F, 4K q90;
+// profiles/r05d_host_huffman_lookup_bits_ab.json: 10 and 12 gain less)
+constexpr int kFastBits = HJD_HOST_FAST_BITS;
 constexpr int kFast = 1 << kFastBits;
 
 struct HuffTable {
@@ -65,13 +67,16 @@ struct Frame {
     size_t scan_offset = 0;
     int sampling = -1;
     ScanSpec scan;                   // the scan parse_segments stopped at
+    bool decode_tables = true;       // build the host decoder's lookup tables (false: header parse only)
 };
 
 inline int be16(const uint8_t* p) { return (p[0] << 8) | p[1]; }
 
-int build_table(HuffTable& t, const uint8_t counts[16], const uint8_t* symbols, int nsym)
+// fast = false: the canonical tables only (header parses for the GPU entropy
+// path, which builds its own device tables from counts / symbols).
+int build_table(HuffTable& t, const uint8_t counts[16], const uint8_t* symbols, int nsym, bool fast)
 {
-    memset(t.fast, 0, sizeof(t.fast));
+    if (fast) memset(t.fast, 0, sizeof(t.fast));
     memcpy(t.counts, counts, 16);
     t.nsym = nsym;
     int code = 0, k = 0;
@@ -83,7 +88,7 @@ int build_table(HuffTable& t, const uint8_t counts[16], const uint8_t* symbols, 
             if (k >= nsym) return -1;
             if (code >= (1 << len)) return -1;   // over-subscribed table
             t.vals[k] = symbols[k];
-            if (len <= kFastBits) {
+            if (fast && len <= kFastBits) {
                 const int shift = kFastBits - len;
                 for (int j = 0; j < (1 << shift); ++j)
                     t.fast[(code << shift) | j] = static_cast<uint16_t>((len << 8) | symbols[k]);
@@ -93,6 +98,8 @@ int build_table(HuffTable& t, const uint8_t counts[16], const uint8_t* symbols, 
         code <<= 1;
     }
     t.maxcode[17] = 0x7fffffff;
+    t.defined = true;
+    if (!fast) return 0;
     // combined AC entries: symbol and its extra bits in one lookup (nonzero
     // coefficients whose code + magnitude bits fit the kFastBits index)
     memset(t.fast_ac, 0, sizeof(t.fast_ac));
@@ -105,7 +112,6 @@ int build_table(HuffTable& t, const uint8_t counts[16], const uint8_t* symbols, 
         const int value = bits < (1 << (size - 1)) ? bits - (1 << size) + 1 : bits;
         t.fast_ac[idx] = static_cast<int32_t>((static_cast<uint32_t>(value) << 16) | (run << 5) | (len + size));
     }
-    t.defined = true;
     return 0;
 }
 
@@ -260,7 +266,8 @@ int parse_segments(const uint8_t* d, size_t n, size_t* pp, Frame& f, bool after_
                 for (int i = 0; i < 16; ++i) nsym += s[q + 1 + i];
                 if (nsym > 256 || q + 17 + nsym > sl) return set_error(HJD_E_INVALID, "bad DHT size");
                 HuffTable& t = tc ? f.ac[th] : f.dc[th];
-                if (build_table(t, s + q + 1, s + q + 17, nsym)) return set_error(HJD_E_INVALID, "invalid Huffman table");
+                if (build_table(t, s + q + 1, s + q + 17, nsym, f.decode_tables))
+                    return set_error(HJD_E_INVALID, "invalid Huffman table");
                 q += 17 + nsym;
             }
             break;
@@ -834,6 +841,7 @@ int hjd_internal::parse_scan_header(const uint8_t* data, size_t size, ScanHeader
 {
     if (!data || !h) return set_error(HJD_E_INVALID, "NULL argument");
     Frame f;
+    f.decode_tables = false;
     int rc = parse(data, size, f);
     if (rc) return rc;
     if (f.process == 2)
@@ -848,6 +856,7 @@ int hjd_internal::parse_scan_headers(const uint8_t* data, size_t size, std::vect
     if (!data || !hs) return set_error(HJD_E_INVALID, "NULL argument");
     hs->clear();
     Frame f;
+    f.decode_tables = false;
     int rc = parse(data, size, f);
     if (rc) return rc;
     if (f.process == 2)
@@ -879,6 +888,7 @@ int hjd_jpeg_parse(const uint8_t* data, size_t size, hjd_jpeg_info* info)
 {
     if (!data || !info) return set_error(HJD_E_INVALID, "NULL argument");
     Frame f;
+    f.decode_tables = false;
     int rc = parse(data, size, f);
     if (rc) return rc;
     fill_info(f, info);
