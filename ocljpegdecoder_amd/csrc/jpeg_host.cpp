@@ -27,6 +27,10 @@ namespace {
 // profiles/r05d_host_huffman_lookup_bits_ab.json: 10 and 12 gain less)
 constexpr int kFastBits = HJD_HOST_FAST_BITS;
 constexpr int kFast = 1 << kFastBits;
+#ifndef HJD_HOST_EOB_FAST
+#define HJD_HOST_EOB_FAST 0
+#endif
+constexpr int32_t kFastEob = 0x8000;   // fast_ac flag: symbol 0x00 (AC end of block)
 
 struct HuffTable {
     bool defined = false;
@@ -107,6 +111,12 @@ int build_table(HuffTable& t, const uint8_t counts[16], const uint8_t* symbols, 
         const uint16_t e = t.fast[idx];
         if (!e) continue;
         const int len = e >> 8, rs = e & 0xFF, run = rs >> 4, size = rs & 15;
+#if HJD_HOST_EOB_FAST
+        if (rs == 0) {   // EOB (AC) / a zero difference (DC): bit 15 marks it, value 0
+            t.fast_ac[idx] = kFastEob | len;
+            continue;
+        }
+#endif
         if (size == 0 || len + size > kFastBits) continue;
         const int bits = (idx >> (kFastBits - len - size)) & ((1 << size) - 1);
         const int value = bits < (1 << (size - 1)) ? bits - (1 << size) + 1 : bits;
@@ -443,6 +453,7 @@ inline bool decode_block(BitReader& br, const HuffTable& dc, const HuffTable& ac
         const int32_t fe = ac.fast_ac[br.peek(kFastBits)];
         if (fe) {   // run + nonzero coefficient in one lookup
             br.skip(fe & 31);
+            if (HJD_HOST_EOB_FAST && (fe & kFastEob)) break;
             k += (fe >> 5) & 15;
             if (k > 63) return false;
             out[k++] = static_cast<int16_t>(fe >> 16);
@@ -585,7 +596,7 @@ inline bool ac_first(BitReader& br, const HuffTable& ac, const ScanSpec& sc, int
     for (int k = sc.ss; k <= sc.se;) {
         if (br.nbits < 16) br.refill();
         const int32_t fe = ac.fast_ac[br.peek(kFastBits)];
-        if (fe) {   // run + nonzero coefficient in one lookup
+        if (fe && !(fe & kFastEob)) {   // run + nonzero coefficient in one lookup (EOB0 takes the EOBRUN path)
             br.skip(fe & 31);
             k += (fe >> 5) & 15;
             if (k > sc.se) return false;

@@ -85,7 +85,8 @@ def build(verbose: bool = False, force: bool = False, variant: str = "",
         objs.append(o)
         if force or _needs(o, [s] + headers):
             # host-only C++ (no device code): compiled by hipcc's clang as plain C++
-            jobs.append([HIPCC, *COMMON, "-x", "c++", "-pthread", "-c", s, "-o", o])
+            extra = os.environ.get("HJD_HOST_CXXFLAGS", "").split()   # tuning A/Bs of the host decoder
+            jobs.append([HIPCC, *COMMON, *extra, "-x", "c++", "-pthread", "-c", s, "-o", o])
     t0 = time.time()
     if force:   # a forced build starts from an empty object directory
         for f in os.listdir(OBJDIR):
