@@ -27,10 +27,9 @@ namespace {
 // profiles/r05d_host_huffman_lookup_bits_ab.json: 10 and 12 gain less)
 constexpr int kFastBits = HJD_HOST_FAST_BITS;
 constexpr int kFast = 1 << kFastBits;
-#ifndef HJD_HOST_EOB_FAST
-#define HJD_HOST_EOB_FAST 0
-#endif
-constexpr int32_t kFastEob = 0x8000;   // fast_ac flag: symbol 0x00 (AC end of block)
+// fast_ac flag of symbol 0x00 (AC end of block; a zero DC difference), value 0:
+// the block's EOB costs one lookup (+1.5 % per thread, profiles/r05e_host_huffman_eob_ab.json)
+constexpr int32_t kFastEob = 0x8000;
 
 struct HuffTable {
     bool defined = false;
@@ -111,12 +110,10 @@ int build_table(HuffTable& t, const uint8_t counts[16], const uint8_t* symbols, 
         const uint16_t e = t.fast[idx];
         if (!e) continue;
         const int len = e >> 8, rs = e & 0xFF, run = rs >> 4, size = rs & 15;
-#if HJD_HOST_EOB_FAST
         if (rs == 0) {   // EOB (AC) / a zero difference (DC): bit 15 marks it, value 0
             t.fast_ac[idx] = kFastEob | len;
             continue;
         }
-#endif
         if (size == 0 || len + size > kFastBits) continue;
         const int bits = (idx >> (kFastBits - len - size)) & ((1 << size) - 1);
         const int value = bits < (1 << (size - 1)) ? bits - (1 << size) + 1 : bits;
@@ -453,7 +450,7 @@ inline bool decode_block(BitReader& br, const HuffTable& dc, const HuffTable& ac
         const int32_t fe = ac.fast_ac[br.peek(kFastBits)];
         if (fe) {   // run + nonzero coefficient in one lookup
             br.skip(fe & 31);
-            if (HJD_HOST_EOB_FAST && (fe & kFastEob)) break;
+            if (fe & kFastEob) break;
             k += (fe >> 5) & 15;
             if (k > 63) return false;
             out[k++] = static_cast<int16_t>(fe >> 16);
