@@ -620,6 +620,14 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
                 "host_threads": nthreads,
                 "host_huffman_Mpx_per_core_s": round(nf * args.steps * w * h / (host_ns / 1e9) / 1e6, 1)
                 if host_ns else None}
+        kbusy_s = (after["kernel_busy_ns"] - before["kernel_busy_ns"]) / 1e9
+        # the ceilings of this pipeline: the kernel alone on these
+        # single-frame launches, the host Huffman threads decoding all the time, and
+        # the pinned upload of the int16 coefficients (measured after the check)
+        busy["kernel_only_Mpx_s"] = round(nf * args.steps * w * h / kbusy_s / 1e6, 1) if kbusy_s else None
+        if busy["host_huffman_Mpx_per_core_s"]:
+            busy["host_huffman_ceiling_Mpx_s"] = round(busy["host_huffman_Mpx_per_core_s"] * nthreads, 1)
+        busy["coef_bytes_per_frame"] = int(h2d_b / max(1, after["images"] - before["images"]))
     host_scan = after.get("host_scan_bytes", 0) - before.get("host_scan_bytes", 0)
     px = nf * w * h * args.steps * world
 
@@ -659,6 +667,10 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
     # PCIe ceilings measured the way the stream moves bytes (concurrent slot streams, batch-sized pieces)
     jpeg_mean = float(np.mean([len(d) for d in pool]))
     h2d = pcie_ceiling(torch, dev, "h2d", per_batch * jpeg_mean, sorted({2, 4, nslots})) if gpu_entropy else None
+    if busy:   # hjd_stream uploads one frame's coefficients per copy on one copy stream
+        c = pcie_ceiling(torch, dev, "h2d", busy["coef_bytes_per_frame"], [1, 2])
+        busy["pcie_ceiling_GBps"] = c["GBps"]
+        busy["pcie_ceiling_Mpx_s"] = round(c["GBps"] * 1e9 / (busy["coef_bytes_per_frame"] / (w * h)) / 1e6, 1)
     d2h_c = pcie_ceiling(torch, dev, "d2h", h * pitch, sorted({2, 4, nslots})) if d2h else None
     if rank == 0:
         jpeg_bytes = int(np.mean([len(d) for d in pool]))
@@ -1198,7 +1210,8 @@ def _stream_summary(leg, ceiling_key=None):
     p = leg.get("pipeline")
     if p:
         r.update({"host_Mpx_s_per_core": p["host_huffman_Mpx_per_core_s"], "cores": p["host_threads"],
-                  "h2d_GBps": p["h2d_GBps"], "kernel_busy": p["kernel_busy_frac"], "h2d_busy": p["h2d_busy_frac"]})
+                  "h2d_GBps": p["h2d_GBps"], "kernel_busy": p["kernel_busy_frac"], "h2d_busy": p["h2d_busy_frac"],
+                  "kernel_only_Mpx_s": p.get("kernel_only_Mpx_s"), "pcie_ceiling_Mpx_s": p.get("pcie_ceiling_Mpx_s")})
     r["ok"] = leg["output_checked_vs_oracle"]
     return r
 

@@ -24,7 +24,8 @@ def _full():
     res["config5_stream_host"] = {
         "value": 5900.0, "timed_frame_ids": 10240, "output_checked_vs_oracle": True,
         "pipeline": {"host_huffman_Mpx_per_core_s": 380.1, "host_threads": 16, "h2d_GBps": 2.1,
-                     "kernel_busy_frac": 0.0213, "h2d_busy_frac": 0.05}}
+                     "kernel_busy_frac": 0.0213, "h2d_busy_frac": 0.05, "kernel_only_Mpx_s": 318000.5,
+                     "pcie_ceiling_Mpx_s": 18500.2}}
     return res
 
 
