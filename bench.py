@@ -554,7 +554,8 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
                                per_batch * max_blocks, nslots=nslots, nthreads=nthreads, out_format=ofmt)
         stat_key = "host_prep_ns"
     else:
-        st = hjd.JpegStream(ctx, max_blocks, nslots=nthreads + 4, nthreads=nthreads)
+        # two jobs per worker in flight (hjd_stream pairs its Huffman decodes) + a few for the GPU side
+        st = hjd.JpegStream(ctx, max_blocks, nslots=2 * nthreads + 4, nthreads=nthreads)
         stat_key = "host_decode_ns"
 
     # the pool is held the way a loader would read files: into pinned host memory

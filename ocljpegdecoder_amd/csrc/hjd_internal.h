@@ -5,6 +5,7 @@
 #include <vector>
 
 struct hjd_ctx;
+struct hjd_jpeg_info;
 
 namespace hjd_internal {
 
@@ -90,6 +91,12 @@ int parse_scan_header(const uint8_t* data, size_t size, ScanHeader* h);
 // Every scan of a sequential file (hs[0] == what parse_scan_header gives).
 // Progressive files fail.
 int parse_scan_headers(const uint8_t* data, size_t size, std::vector<ScanHeader>* hs);
+
+// Host Huffman decode of two files on the calling thread (jpeg_host.cpp): as
+// two hjd_jpeg_decode_coefs calls, with the symbol steps of the two files
+// interleaved when both are single-scan sequential files.  rc[i] per file.
+int jpeg_decode_coefs_two(const uint8_t* const data[2], const size_t size[2], ::hjd_jpeg_info* const info[2],
+                          int16_t* const coefs[2], const int64_t capacity[2], int rc[2]);
 
 // hjd_ctx accessors for the other translation units
 int ctx_num_cu(const struct ::hjd_ctx* ctx);

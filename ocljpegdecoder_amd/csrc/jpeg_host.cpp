@@ -27,6 +27,7 @@ namespace {
 // profiles/r05d_host_huffman_lookup_bits_ab.json: 10 and 12 gain less)
 constexpr int kFastBits = HJD_HOST_FAST_BITS;
 constexpr int kFast = 1 << kFastBits;
+constexpr int kMaxBlocksPerMcu = 6;   // 4:2:0 and 4:1:1 (4 luma + 2 chroma)
 // fast_ac flag of symbol 0x00 (AC end of block; a zero DC difference), value 0:
 // the block's EOB costs one lookup (+1.5 % per thread, profiles/r05e_host_huffman_eob_ab.json)
 constexpr int32_t kFastEob = 0x8000;
@@ -506,6 +507,149 @@ int decode_scan(const uint8_t* d, size_t n, const Frame& f, const hjd_jpeg_info&
     return HJD_OK;
 }
 
+// ---- two files on one thread: interleaved symbol steps ---------------------
+// A Huffman decode is one long dependent chain per file (peek -> table load ->
+// shift -> next peek), so one thread decoding two independent files with their
+// symbol steps interleaved keeps two chains in flight: +10 % per thread on the
+// GPU box's EPYC 9575F (profiles/r05i_host_huffman_two_stream_probe.txt;
+// three files gain no more).  SeqDec is decode_scan + decode_block restated as
+// a one-symbol step with the same checks, errors and output, so the pair
+// decode is byte-identical to two decode_scan calls (tests/test_jpeg_host.py).
+struct SeqDec {
+    BitReader br;
+    const HuffTable* dc[kMaxBlocksPerMcu];
+    const HuffTable* ac[kMaxBlocksPerMcu];
+    int comp[kMaxBlocksPerMcu], slot[kMaxBlocksPerMcu];
+    int bpm = 0, bi = 0, k = 0;
+    int64_t nmcu = 0, m = 0;
+    int16_t* out = nullptr;
+    int16_t* coefs = nullptr;
+    int pred[3] = {0, 0, 0};
+    int ri = 0, since = 0, restarts = 0;
+    bool done = false;
+    int rc = HJD_OK;
+
+    void init(const uint8_t* d, size_t n, const Frame& f, const hjd_jpeg_info& info, int16_t* c)
+    {
+        br = BitReader{d + f.scan_offset, d + n};
+        const int nblk0 = f.ncomp == 1 ? 1 : f.comp[0].h * f.comp[0].v;   // as decode_scan
+        bpm = f.ncomp == 1 ? 1 : nblk0 + 2;
+        int j = 0;
+        for (int si = 0; si < f.ncomp; ++si) {
+            const int cc = f.scan_order[si];
+            const int nb = cc == 0 ? nblk0 : 1;
+            const int base = cc == 0 ? 0 : cc == 1 ? nblk0 : nblk0 + 1;
+            for (int b = 0; b < nb; ++b, ++j) {
+                dc[j] = &f.dc[f.comp[cc].td];
+                ac[j] = &f.ac[f.comp[cc].ta];
+                comp[j] = cc;
+                slot[j] = base + b;
+            }
+        }
+        nmcu = static_cast<int64_t>(info.mcu_w) * info.mcu_h;
+        ri = f.restart_interval;
+        coefs = c;
+        done = nmcu == 0;
+        if (!done) begin_mcu();
+    }
+    void fail(int code)
+    {
+        rc = code;
+        done = true;
+    }
+    void corrupt() { fail(set_error(HJD_E_INVALID, "corrupt entropy data in MCU %lld", static_cast<long long>(m))); }
+    void begin_block()
+    {
+        k = 0;
+        out = coefs + (m * bpm + slot[bi]) * 64;
+        memset(out, 0, 64 * sizeof(int16_t));
+    }
+    void begin_mcu()   // src/decoder.cpp:288-307
+    {
+        if (ri > 0 && since == ri) {
+            if (!br.restart(restarts))
+                return fail(set_error(HJD_E_INVALID, "expected RST%d before MCU %lld", restarts & 7,
+                                      static_cast<long long>(m)));
+            ++restarts;
+            since = 0;
+            pred[0] = pred[1] = pred[2] = 0;
+        }
+        ++since;
+        bi = 0;
+        begin_block();
+    }
+    void end_block()
+    {
+        if (++bi < bpm) return begin_block();
+        if (++m == nmcu) {
+            done = true;
+            return;
+        }
+        begin_mcu();
+    }
+    // one symbol: the DC difference of a block (k == 0) or one AC unit
+    __attribute__((always_inline)) void step()
+    {
+        if (br.nbits < 16) br.refill();
+        if (k == 0) {
+            int& p = pred[comp[bi]];
+            const int32_t fd = dc[bi]->fast_ac[br.peek(kFastBits)];
+            if (fd) {
+                br.skip(fd & 31);
+                p += fd >> 16;
+            } else {
+                const int sz = decode_symbol(br, *dc[bi]);
+                if (sz < 0 || sz > 11) return corrupt();
+                p += receive_extend(br, sz);
+            }
+            if (p < -32768 || p > 32767) return corrupt();
+            out[0] = static_cast<int16_t>(p);
+            k = 1;
+            return;
+        }
+        const int32_t fe = ac[bi]->fast_ac[br.peek(kFastBits)];
+        if (fe) {
+            br.skip(fe & 31);
+            if (fe & kFastEob) return end_block();
+            k += (fe >> 5) & 15;
+            if (k > 63) return corrupt();
+            out[k++] = static_cast<int16_t>(fe >> 16);
+            if (k == 64) end_block();
+            return;
+        }
+        const int rs = decode_symbol(br, *ac[bi]);
+        if (rs < 0) return corrupt();
+        const int r = rs >> 4, sz = rs & 15;
+        if (sz == 0) {
+            if (r != 15) return end_block();   // EOB
+            k += 16;                            // ZRL (a run to or past 64 ends the block, as decode_block)
+            if (k >= 64) end_block();
+            return;
+        }
+        k += r;
+        if (k > 63) return corrupt();
+        out[k++] = static_cast<int16_t>(receive_extend(br, sz));
+        if (k == 64) end_block();
+    }
+};
+
+// Two single-scan sequential files, interleaved; rc[i] as decode_scan returns.
+void decode_scan_pair(const uint8_t* const d[2], const size_t n[2], const Frame* const f[2],
+                      const hjd_jpeg_info* const info[2], int16_t* const coefs[2], int rc[2])
+{
+    SeqDec a, b;
+    a.init(d[0], n[0], *f[0], *info[0], coefs[0]);
+    b.init(d[1], n[1], *f[1], *info[1], coefs[1]);
+    while (!a.done && !b.done) {
+        a.step();
+        b.step();
+    }
+    while (!a.done) a.step();
+    while (!b.done) b.step();
+    rc[0] = a.rc;
+    rc[1] = b.rc;
+}
+
 // ---- several scans per frame: sequential multi-scan and progressive -------
 // (extensions; the reference decodes one interleaved sequential scan)
 
@@ -753,10 +897,10 @@ int decode_multiscan(const uint8_t* d, size_t n, Frame& f, hjd_jpeg_info* info, 
     return HJD_OK;
 }
 
-int decode_one(const uint8_t* data, size_t size, hjd_jpeg_info* info, int16_t* coefs, int64_t capacity)
+// Parse and check one file for decoding into `coefs`.
+int prepare_one(const uint8_t* data, size_t size, hjd_jpeg_info* info, int16_t* coefs, int64_t capacity, Frame& f)
 {
     if (!data || !info) return set_error(HJD_E_INVALID, "NULL argument");
-    Frame f;
     int rc = parse(data, size, f);
     if (rc) return rc;
     fill_info(f, info);
@@ -764,8 +908,37 @@ int decode_one(const uint8_t* data, size_t size, hjd_jpeg_info* info, int16_t* c
     if (capacity < info->nblocks)
         return set_error(HJD_E_INVALID, "capacity %lld < %lld blocks", static_cast<long long>(capacity),
                          static_cast<long long>(info->nblocks));
+    return HJD_OK;
+}
+
+int decode_prepared(const uint8_t* data, size_t size, Frame& f, hjd_jpeg_info* info, int16_t* coefs)
+{
     if (single_scan(f)) return decode_scan(data, size, f, *info, coefs);
     return decode_multiscan(data, size, f, info, coefs);
+}
+
+int decode_one(const uint8_t* data, size_t size, hjd_jpeg_info* info, int16_t* coefs, int64_t capacity)
+{
+    Frame f;
+    const int rc = prepare_one(data, size, info, coefs, capacity, f);
+    return rc ? rc : decode_prepared(data, size, f, info, coefs);
+}
+
+// Two files: interleaved when both are single-scan sequential files
+// (decode_scan_pair), else one after the other; rc[i] as decode_one returns.
+void decode_two(const uint8_t* const data[2], const size_t size[2], hjd_jpeg_info* const info[2],
+                int16_t* const coefs[2], const int64_t capacity[2], int rc[2])
+{
+    Frame f[2];
+    for (int i = 0; i < 2; ++i) rc[i] = prepare_one(data[i], size[i], info[i], coefs[i], capacity[i], f[i]);
+    if (rc[0] == HJD_OK && rc[1] == HJD_OK && single_scan(f[0]) && single_scan(f[1])) {
+        const Frame* fp[2] = {&f[0], &f[1]};
+        const hjd_jpeg_info* ip[2] = {info[0], info[1]};
+        decode_scan_pair(data, size, fp, ip, coefs, rc);
+        return;
+    }
+    for (int i = 0; i < 2; ++i)
+        if (rc[i] == HJD_OK) rc[i] = decode_prepared(data[i], size[i], f[i], info[i], coefs[i]);
 }
 
 }  // namespace
@@ -890,6 +1063,13 @@ int hjd_internal::parse_scan_headers(const uint8_t* data, size_t size, std::vect
     return HJD_OK;
 }
 
+int hjd_internal::jpeg_decode_coefs_two(const uint8_t* const data[2], const size_t size[2], hjd_jpeg_info* const info[2],
+                                        int16_t* const coefs[2], const int64_t capacity[2], int rc[2])
+{
+    decode_two(data, size, info, coefs, capacity, rc);
+    return rc[0] != HJD_OK ? rc[0] : rc[1];
+}
+
 extern "C" {
 
 int hjd_jpeg_parse(const uint8_t* data, size_t size, hjd_jpeg_info* info)
@@ -914,14 +1094,27 @@ int hjd_jpeg_decode_batch(const uint8_t* const* datas, const size_t* sizes, int 
 {
     if (n < 0 || (n > 0 && (!datas || !sizes || !coefs))) return set_error(HJD_E_INVALID, "invalid arguments");
     if (nthreads <= 0) nthreads = static_cast<int>(std::max(1u, std::thread::hardware_concurrency()));
-    nthreads = std::min(nthreads, std::max(n, 1));
+    // each thread takes two files at a time (decode_two: interleaved symbol steps)
+    nthreads = std::min(nthreads, std::max((n + 1) / 2, 1));
     std::atomic<int> next{0}, failed{0};
     auto work = [&]() {
-        hjd_jpeg_info info;
-        for (int i = next++; i < n; i = next++) {
-            const int rc = decode_one(datas[i], sizes[i], &info, coefs[i], capacity_blocks);
-            if (status) status[i] = rc;
-            if (rc) failed++;
+        hjd_jpeg_info info[2];
+        for (int i = next.fetch_add(2); i < n; i = next.fetch_add(2)) {
+            int rc[2] = {HJD_OK, HJD_OK};
+            if (i + 1 < n) {
+                const uint8_t* d[2] = {datas[i], datas[i + 1]};
+                const size_t sz[2] = {sizes[i], sizes[i + 1]};
+                hjd_jpeg_info* ip[2] = {&info[0], &info[1]};
+                int16_t* const c[2] = {coefs[i], coefs[i + 1]};
+                const int64_t cap[2] = {capacity_blocks, capacity_blocks};
+                decode_two(d, sz, ip, c, cap, rc);
+            } else {
+                rc[0] = decode_one(datas[i], sizes[i], &info[0], coefs[i], capacity_blocks);
+            }
+            for (int j = 0; j < 2 && i + j < n; ++j) {
+                if (status) status[i + j] = rc[j];
+                if (rc[j]) failed++;
+            }
         }
     };
     std::vector<std::thread> pool;

@@ -1,0 +1,102 @@
+"""The host decoder's two-file interleaved decode (jpeg_host.cpp decode_two /
+decode_scan_pair), used by hjd_jpeg_decode_batch and the host-Huffman stream
+(hjd_stream workers take two jobs at a time): for every ordered pair of a
+corpus of files -- every sampling, restart intervals, 16-bit tables, the
+reference's sample, progressive and multi-scan files (which take the one-file
+path) and damaged files -- the pair decode must return each file's status and
+coefficients exactly as decoding that file alone does."""
+import ctypes
+import io
+import os
+
+import numpy as np
+import pytest
+
+import jpeg_writer as JW
+import oracle_py as O
+from test_jpeg_host import _pil_jpeg, _pil_smooth, decode
+
+FACTORS = {0: [(1, 1)] * 3, 1: [(2, 2), (1, 1), (1, 1)], 3: [(2, 1), (1, 1), (1, 1)],
+           5: [(4, 1), (1, 1), (1, 1)], 6: [(1, 2), (1, 1), (1, 1)]}
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from ocljpegdecoder_amd import _lib
+    return _lib.load()
+
+
+def _huff_src():
+    from PIL import Image
+    b = io.BytesIO()
+    Image.fromarray(np.zeros((16, 16, 3), np.uint8)).save(b, format="JPEG", quality=90)
+    return b.getvalue()
+
+
+def _damage(data: bytes, seed: int) -> bytes:
+    """Flip a few bytes inside the entropy-coded segment (after the SOS header)."""
+    rng = np.random.default_rng(seed)
+    d = bytearray(data)
+    sos = d.index(b"\xff\xda")
+    start = sos + 2 + ((d[sos + 2] << 8) | d[sos + 3])
+    for p in rng.integers(start, len(d) - 2, 3):
+        d[p] ^= int(rng.integers(1, 256))
+    return bytes(d)
+
+
+def _corpus():
+    files = [open(os.path.join(O.GOLDEN, n + ".jpg"), "rb").read() for n in O.golden_cases()]
+    files += [_pil_smooth(40, 24, 90, "L")[0], _pil_smooth(333, 77, 90, "L", restart_marker_blocks=5)[0],
+              _pil_smooth(333, 77, 90, "RGB", 1)[0], _pil_smooth(200, 40, 90, "RGB", 1, restart_marker_rows=1)[0],
+              _pil_jpeg(64, 48, 50, 0), _pil_jpeg(130, 66, 95, 2, restart_marker_blocks=3),
+              _pil_jpeg(96, 80, 85, 2, progressive=True)]
+    src = _huff_src()
+    for s in (5, 6, 3):
+        for w, h, dri in ((97, 41, 0), (64, 16, 1)):
+            coefs, qt = O.synthetic_coefs(w, h, s, seed=w + s)
+            files.append(JW.encode_frame(coefs, w, h, FACTORS[s], qt, src, restart_interval=dri))
+    coefs, qt = O.synthetic_coefs(80, 48, 1, seed=3)
+    base = JW.encode_frame(coefs, 80, 48, FACTORS[1], qt, src)
+    files.append(JW.rewrite_scans(base, coefs, [(0,), (1, 2)], 2)[0])        # sequential, two scans
+    good = _pil_jpeg(120, 72, 90, 2)
+    files += [_damage(good, k) for k in range(4)] + [good[: len(good) * 2 // 3]]
+    return files
+
+
+def _batch(lib, datas, cap, nthreads=1):
+    u8p, i16p = ctypes.POINTER(ctypes.c_uint8), ctypes.POINTER(ctypes.c_int16)
+    bufs = [(ctypes.c_uint8 * len(d)).from_buffer_copy(d) for d in datas]
+    outs = [np.full((cap, 64), 0x5A5A, np.int16) for _ in datas]
+    arr_d = (u8p * len(bufs))(*[ctypes.cast(b, u8p) for b in bufs])
+    arr_s = (ctypes.c_size_t * len(datas))(*[len(d) for d in datas])
+    arr_o = (i16p * len(outs))(*[o.ctypes.data_as(i16p) for o in outs])
+    status = (ctypes.c_int32 * len(datas))()
+    lib.hjd_jpeg_decode_batch(arr_d, arr_s, len(datas), arr_o, cap, nthreads, status)
+    return list(status), outs
+
+
+def test_pairs_equal_single_decodes(lib):
+    files = _corpus()
+    singles = [decode(lib, d) for d in files]
+    assert sum(rc == 0 for rc, _, _ in singles) >= len(files) - 5    # the damaged ones may fail
+    assert any(rc != 0 for rc, _, _ in singles)                        # ... and some do
+    cap = max(i.nblocks for _, i, _ in singles)
+    for a in range(len(files)):
+        for b in range(len(files)):
+            status, outs = _batch(lib, [files[a], files[b]], cap)      # one thread: files a, b as a pair
+            for k, i in ((0, a), (1, b)):
+                rc, info, coefs = singles[i]
+                assert (status[k] == 0) == (rc == 0), (a, b, k, status[k], rc)
+                if rc == 0:
+                    np.testing.assert_array_equal(outs[k][: info.nblocks], coefs, err_msg=f"pair ({a},{b}) file {k}")
+
+
+def test_odd_batch_and_many_threads(lib):
+    """Batches of odd length (the last file alone) over several threads."""
+    files = _corpus()[:13]
+    singles = [decode(lib, d) for d in files]
+    cap = max(i.nblocks for _, i, _ in singles)
+    status, outs = _batch(lib, files, cap, nthreads=3)
+    for k, (rc, info, coefs) in enumerate(singles):
+        assert status[k] == rc == 0
+        np.testing.assert_array_equal(outs[k][: info.nblocks], coefs)

@@ -1,7 +1,10 @@
 // Host-decoder robustness harness, built with AddressSanitizer + UBSan on the
 // CPU (tools/fuzz/run.sh): mutates the JPEG files named on the command line
 // (byte flips, truncation, marker-segment damage) and decodes every mutant
-// with hjd_jpeg_decode_coefs.  Any out-of-bounds access aborts the run.
+// with hjd_jpeg_decode_coefs, and every mutant together with the previous one
+// through the two-file interleaved decode (hjd_internal::jpeg_decode_coefs_two),
+// whose per-file results must equal the one-file decodes.  Any out-of-bounds
+// access aborts the run.
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -21,7 +24,11 @@ int main(int argc, char** argv)
     }
     const int iters = atoi(argv[1]);
     std::mt19937 rng(12345);
-    long ok = 0, bad = 0;
+    long ok = 0, bad = 0, pairs = 0;
+    std::vector<uint8_t> prev;   // the previous mutant (any source file), its one-file result
+    int prev_rc = 0;
+    int64_t prev_cap = 0;
+    std::vector<int16_t> prev_coefs;
     for (int a = 2; a < argc; ++a) {
         FILE* fp = fopen(argv[a], "rb");
         if (!fp) return 2;
@@ -31,7 +38,6 @@ int main(int argc, char** argv)
         hjd_jpeg_info info;
         if (hjd_jpeg_parse(src.data(), src.size(), &info)) return 3;
         const int64_t cap = info.nblocks + 64;
-        std::vector<int16_t> coefs(static_cast<size_t>(cap) * 64);
         for (int i = 0; i < iters; ++i) {
             std::vector<uint8_t> d = src;
             const int nflip = 1 + static_cast<int>(rng() % 8);
@@ -43,15 +49,45 @@ int main(int argc, char** argv)
             // exact-size heap copy so ASan sees reads past the end
             uint8_t* buf = static_cast<uint8_t*>(malloc(d.size()));
             std::copy(d.begin(), d.end(), buf);
+            // the one-file decode, into a fresh buffer
             hjd_jpeg_info mi;
-            if (hjd_jpeg_parse(buf, d.size(), &mi) == HJD_OK && mi.nblocks <= cap &&
-                hjd_jpeg_decode_coefs(buf, d.size(), &mi, coefs.data(), cap) == HJD_OK)
-                ++ok;
-            else
-                ++bad;
+            int rc = hjd_jpeg_parse(buf, d.size(), &mi);
+            const int64_t nb = rc == HJD_OK ? mi.nblocks : 0;
+            std::vector<int16_t> one(static_cast<size_t>(cap) * 64, 0);
+            if (rc == HJD_OK) rc = hjd_jpeg_decode_coefs(buf, d.size(), &mi, one.data(), cap);
+            if (rc == HJD_OK) ++ok; else ++bad;
+            one.resize(rc == HJD_OK ? static_cast<size_t>(nb) * 64 : 0);
+            if (!prev.empty()) {
+                // (previous mutant, this one) through the two-file decode on one thread
+                uint8_t* pbuf = static_cast<uint8_t*>(malloc(prev.size()));
+                std::copy(prev.begin(), prev.end(), pbuf);
+                std::vector<int16_t> c0(static_cast<size_t>(prev_cap) * 64, 0), c1(static_cast<size_t>(cap) * 64, 0);
+                hjd_jpeg_info i0, i1;
+                const uint8_t* dd[2] = {pbuf, buf};
+                const size_t nn[2] = {prev.size(), d.size()};
+                hjd_jpeg_info* ii[2] = {&i0, &i1};
+                int16_t* const cc[2] = {c0.data(), c1.data()};
+                const int64_t caps[2] = {prev_cap, cap};
+                int prc[2];
+                hjd_internal::jpeg_decode_coefs_two(dd, nn, ii, cc, caps, prc);
+                c0.resize(prc[0] == HJD_OK ? prev_coefs.size() : 0);
+                c1.resize(prc[1] == HJD_OK ? one.size() : 0);
+                if ((prc[0] == HJD_OK) != (prev_rc == HJD_OK) || (prc[1] == HJD_OK) != (rc == HJD_OK) ||
+                    c0 != prev_coefs || c1 != one) {
+                    fprintf(stderr, "pair decode differs from the one-file decodes (iteration %d of %s)\n", i,
+                            argv[a]);
+                    return 4;
+                }
+                ++pairs;
+                free(pbuf);
+            }
+            prev = d;
+            prev_rc = rc;
+            prev_cap = cap;
+            prev_coefs.swap(one);
             free(buf);
         }
     }
-    printf("mutants decoded: %ld ok, %ld rejected\n", ok, bad);
+    printf("mutants decoded: %ld ok, %ld rejected; %ld pairs equal to their one-file decodes\n", ok, bad, pairs);
     return 0;
 }
