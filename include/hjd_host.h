@@ -214,6 +214,11 @@ int hjd_bmp_header(int32_t width, int32_t height, uint8_t header[54]);
  * HJD_OUT_BGR24 image at pitch (3*W+3)&~3. */
 int hjd_bmp_header_bgr24(int32_t width, int32_t height, uint8_t header[54]);
 
+/* Test hook: the reader of the host decoder's single-scan files, process-wide.
+ * 0 (default) the de-stuffed reader wherever the scan admits it, 1 the
+ * byte-wise reader always (the cross-check); -1 queries.  Returns the previous
+ * mode. */
+int hjd_debug_host_reader(int mode);
 /* Test hook (no GPU): runs the same parallel algorithm on the host, one frame,
  * and writes its coefficients.  Not a decode path. */
 /* Destuff step alone (test hooks): the host routine, and the device kernels on

@@ -7,8 +7,10 @@
 // lookup per Huffman table (canonical MAXCODE/VALPTR search for longer codes,
 // JPEG Annex F.2.2.3), restart-marker resynchronisation, and a thread pool
 // that decodes independent files in parallel.
+#include <algorithm>
 #include <atomic>
 #include <cstring>
+#include <memory>
 #include <thread>
 #include <vector>
 
@@ -472,7 +474,7 @@ inline bool decode_block(BitReader& br, const HuffTable& dc, const HuffTable& ac
     return true;
 }
 
-int decode_scan(const uint8_t* d, size_t n, const Frame& f, const hjd_jpeg_info& info, int16_t* coefs)
+int decode_scan_bytewise(const uint8_t* d, size_t n, const Frame& f, const hjd_jpeg_info& info, int16_t* coefs)
 {
     BitReader br{d + f.scan_offset, d + n};
     int pred[3] = {0, 0, 0};
@@ -633,8 +635,8 @@ struct SeqDec {
     }
 };
 
-// Two single-scan sequential files, interleaved; rc[i] as decode_scan returns.
-void decode_scan_pair(const uint8_t* const d[2], const size_t n[2], const Frame* const f[2],
+// Two single-scan sequential files, interleaved; rc[i] as decode_scan_bytewise returns.
+void decode_scan_pair_bytewise(const uint8_t* const d[2], const size_t n[2], const Frame* const f[2],
                       const hjd_jpeg_info* const info[2], int16_t* const coefs[2], int rc[2])
 {
     SeqDec a, b;
@@ -648,6 +650,341 @@ void decode_scan_pair(const uint8_t* const d[2], const size_t n[2], const Frame*
     while (!b.done) b.step();
     rc[0] = a.rc;
     rc[1] = b.rc;
+}
+
+// ---- the de-stuffed reader (the single-scan hot path) ----------------------
+// BitReader pays a data-dependent branch per symbol (refill when fewer than
+// 16 bits are left) and a byte loop at every 0xFF.  The hot path instead
+// copies the scan's entropy-coded data once without its byte stuffing
+// (memchr-driven, a few % of the decode) into per-thread scratch, one segment
+// per restart interval, each followed by 8 zero bytes, and then reads it with
+// an unconditional branch-free refill before every symbol: a 64-bit load at
+// the byte cursor, shifted under the bits still buffered (the cursor moves by
+// the whole bytes taken and stops at the segment's end, so the reader sees
+// zeros past it, as BitReader does past a marker).  After a refill at least
+// 56 bits are buffered, enough for any one symbol (16-bit code + 11 extra
+// bits), so a step never refills again.
+//
+// The bits a decode sees are the BitReader's exactly: de-stuffed FF00, fill
+// bytes in front of a marker dropped, zeros after the marker or the end of
+// the data, and a restart moves to the next segment when the marker that ended
+// the current one is the expected RSTn.  The one difference would be fill
+// bytes INSIDE the data (FF FF 00: BitReader reads the FF00 after the fill
+// byte, its restart search stops at the FF FF): destuff_scan declines such a
+// scan and it takes the byte-wise path.  tests/test_jpeg_host_pair.py and the
+// fuzz harness (tools/fuzz/host_decode_fuzz.cpp) compare the two readers.
+struct CleanSeg {
+    size_t begin, end;   // bytes of CleanScan::buf; 8 zero bytes follow `end`
+    int marker;          // the marker byte that ended the segment; -1: the data ended
+};
+
+struct CleanScan {
+    std::unique_ptr<uint8_t[]> buf;
+    size_t cap = 0;
+    std::vector<CleanSeg> segs;
+};
+
+// De-stuff the entropy-coded data from s into cs: max_segs segments at most
+// (the scan's restart intervals), stopping at a marker that is not RSTn.
+// false: fill bytes inside the data (the byte-wise reader's case).
+bool destuff_scan(const uint8_t* s, const uint8_t* end, int64_t max_segs, CleanScan& cs)
+{
+    const size_t n = static_cast<size_t>(end - s);
+    max_segs = std::max<int64_t>(1, std::min<int64_t>(max_segs, static_cast<int64_t>(n / 2) + 1));
+    const size_t need = n + 8 * static_cast<size_t>(max_segs) + 8;
+    if (cs.cap < need) {
+        cs.buf.reset(new uint8_t[need]);
+        cs.cap = need;
+    }
+    cs.segs.clear();
+    uint8_t* const o0 = cs.buf.get();
+    uint8_t* o = o0;
+    size_t begin = 0;
+    for (;;) {
+        const uint8_t* f = static_cast<const uint8_t*>(memchr(s, 0xFF, static_cast<size_t>(end - s)));
+        const uint8_t* stop = f ? f : end;
+        memcpy(o, s, static_cast<size_t>(stop - s));
+        o += stop - s;
+        s = stop;
+        int marker = -1;
+        if (f) {
+            if (f + 1 < end && f[1] == 0x00) {   // stuffed FF
+                *o++ = 0xFF;
+                s = f + 2;
+                continue;
+            }
+            const uint8_t* g = f;
+            while (g < end && *g == 0xFF) ++g;   // marker prefix and fill bytes
+            if (g < end && *g == 0x00) return false;
+            if (g < end) marker = *g;
+            s = g < end ? g + 1 : end;
+        }
+        const size_t seg_end = static_cast<size_t>(o - o0);
+        memset(o, 0, 8);
+        o += 8;
+        cs.segs.push_back({begin, seg_end, marker});
+        begin = static_cast<size_t>(o - o0);
+        if (marker < 0xD0 || marker > 0xD7 || static_cast<int64_t>(cs.segs.size()) == max_segs) return true;
+    }
+}
+
+struct FastReader {
+    const uint8_t* p;
+    const uint8_t* lim;   // the segment's end (8 zero bytes follow)
+    uint64_t acc = 0;     // MSB-first; bits below the top nbits are zeros or the stream's next bits
+    int nbits = 0;
+
+    __attribute__((always_inline)) void refill()
+    {
+        uint64_t v;
+        memcpy(&v, p, 8);
+        acc |= __builtin_bswap64(v) >> nbits;
+        p += (63 - nbits) >> 3;
+        p = p < lim ? p : lim;
+        nbits |= 56;
+    }
+    uint32_t peek(int n) const { return static_cast<uint32_t>(acc >> (64 - n)); }
+    void skip(int n)
+    {
+        acc <<= n;
+        nbits -= n;
+    }
+};
+
+// decode_symbol without the refill (the step refilled: >= 56 bits)
+__attribute__((always_inline)) inline int fast_symbol(FastReader& br, const HuffTable& t)
+{
+    const uint16_t e = t.fast[br.peek(kFastBits)];
+    if (e) {
+        br.skip(e >> 8);
+        return e & 0xFF;
+    }
+    const uint32_t code16 = br.peek(16);
+    for (int len = kFastBits + 1; len <= 16; ++len) {
+        const int32_t c = static_cast<int32_t>(code16 >> (16 - len));
+        if (c <= t.maxcode[len]) {
+            br.skip(len);
+            return t.vals[t.valptr[len] + c - t.mincode[len]];
+        }
+    }
+    return -1;
+}
+
+__attribute__((always_inline)) inline int fast_extend(FastReader& br, int s)
+{
+    if (s == 0) return 0;
+    const int v = static_cast<int>(br.peek(s));
+    br.skip(s);
+    return v < (1 << (s - 1)) ? v - (1 << s) + 1 : v;
+}
+
+__attribute__((noinline, cold)) int report_error(int err, int64_t m, int restarts)
+{
+    if (err == 1) return set_error(HJD_E_INVALID, "corrupt entropy data in MCU %lld", static_cast<long long>(m));
+    if (err == 2) return set_error(HJD_E_INVALID, "expected RST%d before MCU %lld", restarts & 7, static_cast<long long>(m));
+    return HJD_OK;
+}
+
+// A file's block order and DC predictors (kept apart from FastDec, whose
+// scalars then stay in registers: no dynamically indexed member).
+struct BlockOrder {
+    const HuffTable* dc[kMaxBlocksPerMcu];
+    const HuffTable* ac[kMaxBlocksPerMcu];
+    int comp[kMaxBlocksPerMcu], slot[kMaxBlocksPerMcu];
+    int pred[3] = {0, 0, 0};
+};
+
+// SeqDec on the de-stuffed reader; errors are recorded and reported (set_error)
+// after the loop, so nothing on the step path calls out.
+struct FastDec {
+    FastReader br;
+    const CleanScan* cs = nullptr;
+    BlockOrder* o = nullptr;
+    size_t seg = 0;
+    int bpm = 0, bi = 0, k = 0;
+    int64_t nmcu = 0, m = 0;
+    int16_t* out = nullptr;
+    int16_t* coefs = nullptr;
+    int ri = 0, since = 0, restarts = 0;
+    bool done = false;
+    int err = 0;   // 1: corrupt entropy data in MCU m, 2: expected RSTn before MCU m
+
+    __attribute__((always_inline)) void init(const CleanScan& c, BlockOrder& ord, const Frame& f,
+                                             const hjd_jpeg_info& info, int16_t* co)
+    {
+        cs = &c;
+        o = &ord;
+        br.p = c.buf.get() + c.segs[0].begin;
+        br.lim = c.buf.get() + c.segs[0].end;
+        const int nblk0 = f.ncomp == 1 ? 1 : f.comp[0].h * f.comp[0].v;   // as decode_scan_bytewise
+        bpm = f.ncomp == 1 ? 1 : nblk0 + 2;
+        int j = 0;
+        for (int si = 0; si < f.ncomp; ++si) {
+            const int cc = f.scan_order[si];
+            const int nb = cc == 0 ? nblk0 : 1;
+            const int base = cc == 0 ? 0 : cc == 1 ? nblk0 : nblk0 + 1;
+            for (int b = 0; b < nb; ++b, ++j) {
+                ord.dc[j] = &f.dc[f.comp[cc].td];
+                ord.ac[j] = &f.ac[f.comp[cc].ta];
+                ord.comp[j] = cc;
+                ord.slot[j] = base + b;
+            }
+        }
+        nmcu = static_cast<int64_t>(info.mcu_w) * info.mcu_h;
+        ri = f.restart_interval;
+        coefs = co;
+        done = nmcu == 0;
+        if (!done) begin_mcu();
+    }
+    __attribute__((always_inline)) int report() const { return report_error(err, m, restarts); }
+    __attribute__((always_inline)) void fail(int e)
+    {
+        err = e;
+        done = true;
+    }
+    __attribute__((always_inline)) void begin_block()
+    {
+        k = 0;
+        out = coefs + (m * bpm + o->slot[bi]) * 64;
+        memset(out, 0, 64 * sizeof(int16_t));
+    }
+    __attribute__((always_inline)) void begin_mcu()   // src/decoder.cpp:288-307
+    {
+        if (ri > 0 && since == ri) {
+            const CleanSeg& s = cs->segs[seg];
+            if (s.marker != 0xD0 + (restarts & 7) || seg + 1 >= cs->segs.size()) return fail(2);
+            ++seg;
+            br.p = cs->buf.get() + cs->segs[seg].begin;
+            br.lim = cs->buf.get() + cs->segs[seg].end;
+            br.acc = 0;
+            br.nbits = 0;
+            ++restarts;
+            since = 0;
+            o->pred[0] = o->pred[1] = o->pred[2] = 0;
+        }
+        ++since;
+        bi = 0;
+        begin_block();
+    }
+    __attribute__((always_inline)) void end_block()
+    {
+        if (++bi < bpm) return begin_block();
+        if (++m == nmcu) {
+            done = true;
+            return;
+        }
+        begin_mcu();
+    }
+    // one symbol: the DC difference of a block (k == 0) or one AC unit
+    __attribute__((always_inline)) void step()
+    {
+        br.refill();
+        if (k == 0) {
+            int& p = o->pred[o->comp[bi]];
+            const HuffTable& dc = *o->dc[bi];
+            const int32_t fd = dc.fast_ac[br.peek(kFastBits)];
+            if (fd) {
+                br.skip(fd & 31);
+                p += fd >> 16;
+            } else {
+                const int sz = fast_symbol(br, dc);
+                if (sz < 0 || sz > 11) return fail(1);
+                p += fast_extend(br, sz);
+            }
+            if (p < -32768 || p > 32767) return fail(1);
+            out[0] = static_cast<int16_t>(p);
+            k = 1;
+            return;
+        }
+        const HuffTable& ac = *o->ac[bi];
+        const int32_t fe = ac.fast_ac[br.peek(kFastBits)];
+        if (fe) {
+            br.skip(fe & 31);
+            if (fe & kFastEob) return end_block();
+            k += (fe >> 5) & 15;
+            if (k > 63) return fail(1);
+            out[k++] = static_cast<int16_t>(fe >> 16);
+            if (k == 64) end_block();
+            return;
+        }
+        const int rs = fast_symbol(br, ac);
+        if (rs < 0) return fail(1);
+        const int r = rs >> 4, sz = rs & 15;
+        if (sz == 0) {
+            if (r != 15) return end_block();   // EOB
+            k += 16;                            // ZRL (a run to or past 64 ends the block, as decode_block)
+            if (k >= 64) end_block();
+            return;
+        }
+        k += r;
+        if (k > 63) return fail(1);
+        out[k++] = static_cast<int16_t>(fast_extend(br, sz));
+        if (k == 64) end_block();
+    }
+};
+
+// The reader of single-scan decodes: 0 the de-stuffed reader where the scan
+// admits it, 1 the byte-wise reader always (hjd_debug_host_reader: tests).
+std::atomic<int> g_host_reader{0};
+
+// Scratch of the de-stuffed reader, two per thread (the pair decode).
+CleanScan& clean_scratch(int i)
+{
+    thread_local CleanScan cs[2];
+    return cs[i];
+}
+
+int64_t scan_segments(const Frame& f, const hjd_jpeg_info& info)
+{
+    const int64_t nmcu = static_cast<int64_t>(info.mcu_w) * info.mcu_h;
+    return f.restart_interval > 0 ? (nmcu + f.restart_interval - 1) / f.restart_interval : 1;
+}
+
+bool destuff_for(const uint8_t* d, size_t n, const Frame& f, const hjd_jpeg_info& info, CleanScan& cs)
+{
+    return g_host_reader.load(std::memory_order_relaxed) == 0 && f.scan_offset <= n &&
+           destuff_scan(d + f.scan_offset, d + n, scan_segments(f, info), cs);
+}
+
+// One single-scan sequential file (src/decoder.cpp:262-358).
+int decode_scan(const uint8_t* d, size_t n, const Frame& f, const hjd_jpeg_info& info, int16_t* coefs)
+{
+    CleanScan& cs = clean_scratch(0);
+    if (!destuff_for(d, n, f, info, cs)) return decode_scan_bytewise(d, n, f, info, coefs);
+    BlockOrder oa;
+    FastDec a;
+    a.init(cs, oa, f, info, coefs);
+    while (!a.done) a.step();
+    return a.report();
+}
+
+// Two single-scan sequential files, interleaved; rc[i] as decode_scan returns
+// (errors recorded in the order they occurred).
+void decode_scan_pair(const uint8_t* const d[2], const size_t n[2], const Frame* const f[2],
+                      const hjd_jpeg_info* const info[2], int16_t* const coefs[2], int rc[2])
+{
+    CleanScan& c0 = clean_scratch(0);
+    CleanScan& c1 = clean_scratch(1);
+    if (!destuff_for(d[0], n[0], *f[0], *info[0], c0) || !destuff_for(d[1], n[1], *f[1], *info[1], c1))
+        return decode_scan_pair_bytewise(d, n, f, info, coefs, rc);
+    BlockOrder oa, ob;
+    FastDec a, b;
+    a.init(c0, oa, *f[0], *info[0], coefs[0]);
+    b.init(c1, ob, *f[1], *info[1], coefs[1]);
+    while (!a.done && !b.done) {
+        a.step();
+        b.step();
+    }
+    const bool b_first = b.done && !a.done;
+    while (!a.done) a.step();
+    while (!b.done) b.step();
+    if (b_first) {
+        rc[1] = b.report();
+        rc[0] = a.report();
+    } else {
+        rc[0] = a.report();
+        rc[1] = b.report();
+    }
 }
 
 // ---- several scans per frame: sequential multi-scan and progressive -------
@@ -1081,6 +1418,13 @@ int hjd_jpeg_parse(const uint8_t* data, size_t size, hjd_jpeg_info* info)
     if (rc) return rc;
     fill_info(f, info);
     return HJD_OK;
+}
+
+int hjd_debug_host_reader(int mode)
+{
+    if (mode < 0) return g_host_reader.load();
+    if (mode > 1) return set_error(HJD_E_INVALID, "host reader mode %d (0 de-stuffed, 1 byte-wise)", mode);
+    return g_host_reader.exchange(mode);
 }
 
 int hjd_jpeg_decode_coefs(const uint8_t* data, size_t size, hjd_jpeg_info* info, int16_t* coefs,

@@ -100,3 +100,49 @@ def test_odd_batch_and_many_threads(lib):
     for k, (rc, info, coefs) in enumerate(singles):
         assert status[k] == rc == 0
         np.testing.assert_array_equal(outs[k][: info.nblocks], coefs)
+
+
+def _fill_bytes(data: bytes, inside: bool) -> bytes:
+    """Insert a fill byte (0xFF) in front of the first RST marker (legal: the
+    readers skip it), or -- inside=True -- in front of the first stuffed FF00
+    of the entropy data (FF FF 00: the byte-wise reader's own case)."""
+    d = bytearray(data)
+    sos = d.index(b"\xff\xda")
+    start = sos + 2 + ((d[sos + 2] << 8) | d[sos + 3])
+    pat = b"\xff\x00" if inside else bytes([0xFF, 0xD0])
+    at = d.index(pat, start)
+    d[at:at] = b"\xff"
+    return bytes(d)
+
+
+def _wrong_rst(data: bytes) -> bytes:
+    d = bytearray(data)
+    sos = d.index(b"\xff\xda")
+    at = d.index(bytes([0xFF, 0xD1]), sos)
+    d[at + 1] = 0xD3
+    return bytes(d)
+
+
+def test_readers_agree(lib):
+    """The de-stuffed reader (the default for single-scan files) against the
+    byte-wise reader (hjd_debug_host_reader(1)): the same status, error text
+    and coefficients on the corpus, on fill bytes before a marker and inside
+    the data, on a wrong RST number and on cut files."""
+    rst = _pil_jpeg(130, 66, 95, 2, restart_marker_blocks=3)
+    files = _corpus() + [_fill_bytes(rst, False), _fill_bytes(rst, True), _fill_bytes(_pil_jpeg(64, 48, 95, 0), True),
+                         _wrong_rst(rst), rst[: len(rst) // 2], rst[: len(rst) // 2] + b"\xff"]
+    assert lib.hjd_debug_host_reader(-1) == 0
+    for i, d in enumerate(files):
+        res = []
+        for mode in (0, 1):
+            assert lib.hjd_debug_host_reader(mode) in (0, 1)
+            rc, info, coefs = decode(lib, d)
+            res.append((rc, lib.hjd_last_error() if rc else b"", coefs))
+        lib.hjd_debug_host_reader(0)
+        (r0, e0, c0), (r1, e1, c1) = res
+        assert r0 == r1 and e0 == e1, (i, r0, r1, e0, e1)
+        if r0 == 0 and c0 is not None:
+            np.testing.assert_array_equal(c0, c1, err_msg=f"file {i}")
+    assert decode(lib, _fill_bytes(rst, False))[0] == 0          # a fill byte before RSTn is legal
+    assert decode(lib, _wrong_rst(rst))[0] != 0
+    assert lib.hjd_debug_host_reader(2) != 0 and lib.hjd_debug_host_reader(-1) == 0

@@ -3,8 +3,9 @@
 // (byte flips, truncation, marker-segment damage) and decodes every mutant
 // with hjd_jpeg_decode_coefs, and every mutant together with the previous one
 // through the two-file interleaved decode (hjd_internal::jpeg_decode_coefs_two),
-// whose per-file results must equal the one-file decodes.  Any out-of-bounds
-// access aborts the run.
+// whose per-file results must equal the one-file decodes; the one-file decode
+// with the de-stuffed reader (default) must equal the byte-wise reader's
+// (hjd_debug_host_reader(1)).  Any out-of-bounds access aborts the run.
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -24,7 +25,7 @@ int main(int argc, char** argv)
     }
     const int iters = atoi(argv[1]);
     std::mt19937 rng(12345);
-    long ok = 0, bad = 0, pairs = 0;
+    long ok = 0, bad = 0, pairs = 0, readers = 0;
     std::vector<uint8_t> prev;   // the previous mutant (any source file), its one-file result
     int prev_rc = 0;
     int64_t prev_cap = 0;
@@ -57,6 +58,20 @@ int main(int argc, char** argv)
             if (rc == HJD_OK) rc = hjd_jpeg_decode_coefs(buf, d.size(), &mi, one.data(), cap);
             if (rc == HJD_OK) ++ok; else ++bad;
             one.resize(rc == HJD_OK ? static_cast<size_t>(nb) * 64 : 0);
+            if (nb > 0) {
+                // the same file through the byte-wise reader
+                std::vector<int16_t> bw(static_cast<size_t>(cap) * 64, 0);
+                hjd_debug_host_reader(1);
+                const int brc = hjd_jpeg_decode_coefs(buf, d.size(), &mi, bw.data(), cap);
+                hjd_debug_host_reader(0);
+                bw.resize(brc == HJD_OK ? static_cast<size_t>(nb) * 64 : 0);
+                if (brc != rc || bw != one) {
+                    fprintf(stderr, "de-stuffed and byte-wise readers differ (iteration %d of %s: rc %d vs %d)\n", i,
+                            argv[a], rc, brc);
+                    return 5;
+                }
+                ++readers;
+            }
             if (!prev.empty()) {
                 // (previous mutant, this one) through the two-file decode on one thread
                 uint8_t* pbuf = static_cast<uint8_t*>(malloc(prev.size()));
@@ -88,6 +103,7 @@ int main(int argc, char** argv)
             free(buf);
         }
     }
-    printf("mutants decoded: %ld ok, %ld rejected; %ld pairs equal to their one-file decodes\n", ok, bad, pairs);
+    printf("mutants decoded: %ld ok, %ld rejected; %ld pairs equal to their one-file decodes; %ld equal under both "
+           "readers\n", ok, bad, pairs, readers);
     return 0;
 }

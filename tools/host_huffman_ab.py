@@ -4,7 +4,9 @@ synthetic 4K q90 JPEGs (bench.encode_pool), 1 thread and N threads.
 
     python tools/host_huffman_ab.py product+build/variants/x/libhjd.so [--rounds 3] [--threads 16] [--sampling 1]
 
-("product" = the in-tree library; libraries separated by '+').
+("product" = the in-tree library; libraries separated by '+'; a "#bytewise"
+suffix runs that library with the byte-wise reader, hjd_debug_host_reader(1)).
+Outputs are preallocated and touched once, so no page faults are timed.
 """
 import argparse
 import json
@@ -15,22 +17,35 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 CHILD = r"""
-import json, sys, time
+import ctypes, json, sys, time
+import numpy as np
 sys.path.insert(0, REPO)
 import bench
-import ocljpegdecoder_amd as hjd
-s, nt = int(sys.argv[1]), int(sys.argv[2])
+from ocljpegdecoder_amd import _lib
+lib = _lib.load()
+s, nt, reader = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
+lib.hjd_debug_host_reader(reader)
 pool = bench.encode_pool(3840, 2160, s, 8, seed0=99)
-hjd.decode_coefs_batch(pool[:2], nthreads=1)
+u8p, i16p = ctypes.POINTER(ctypes.c_uint8), ctypes.POINTER(ctypes.c_int16)
+bufs = [(ctypes.c_uint8 * len(d)).from_buffer_copy(d) for d in pool]
+cap = 3840 * 2160 * 3 // 128 + 4096        # blocks of a 4K 4:4:4 frame and then some
+outs = [np.ones((cap, 64), np.int16) for _ in range(2 * nt)]   # touched once: no page faults timed
+
+def run(n, reps):
+    arr_d = (u8p * reps)(*[ctypes.cast(bufs[i % len(bufs)], u8p) for i in range(reps)])
+    arr_s = (ctypes.c_size_t * reps)(*[len(pool[i % len(pool)]) for i in range(reps)])
+    arr_o = (i16p * reps)(*[outs[i % len(outs)].ctypes.data_as(i16p) for i in range(reps)])
+    st = (ctypes.c_int32 * reps)()
+    t0 = time.perf_counter()
+    rc = lib.hjd_jpeg_decode_batch(arr_d, arr_s, reps, arr_o, cap, n, st)
+    dt = time.perf_counter() - t0
+    assert rc == 0 and not any(st)
+    return reps * 3840 * 2160 / dt / 1e6
+
+run(1, 2)
 res = {}
 for key, n, reps in (("one_thread", 1, 8), ("threads", nt, 8 * nt)):
-    best = 0.0
-    for _ in range(3):
-        datas = [pool[i % len(pool)] for i in range(reps)]
-        t0 = time.perf_counter()
-        hjd.decode_coefs_batch(datas, nthreads=n)
-        best = max(best, reps * 3840 * 2160 / (time.perf_counter() - t0) / 1e6)
-    res[key] = round(best, 1)
+    res[key] = round(max(run(n, reps) for _ in range(3)), 1)
 print(json.dumps(res))
 """.replace("REPO", repr(REPO))
 
@@ -46,9 +61,11 @@ def main():
     for r in range(a.rounds):
         for lib in a.libs.split("+"):
             env = dict(os.environ)
-            if lib != "product":
-                env["HJD_LIB"] = os.path.join(REPO, lib)
-            out = subprocess.run([sys.executable, "-c", CHILD, str(a.sampling), str(a.threads)], env=env,
+            path, _, reader = lib.partition("#")
+            if path != "product":
+                env["HJD_LIB"] = os.path.join(REPO, path)
+            out = subprocess.run([sys.executable, "-c", CHILD, str(a.sampling), str(a.threads),
+                                  "1" if reader == "bytewise" else "0"], env=env,
                                  capture_output=True, text=True, timeout=600)
             if out.returncode:
                 raise SystemExit(out.stderr[-2000:])
