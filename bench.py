@@ -555,7 +555,8 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
         stat_key = "host_prep_ns"
     else:
         # two jobs per worker in flight (hjd_stream pairs its Huffman decodes) + a few for the GPU side
-        st = hjd.JpegStream(ctx, max_blocks, nslots=2 * nthreads + 4, nthreads=nthreads)
+        st = hjd.JpegStream(ctx, max_blocks, nthreads=nthreads,
+                            nslots=int(os.environ.get("HJD_STREAM_HOST_SLOTS", 2 * nthreads + 4)))
         stat_key = "host_decode_ns"
 
     # the pool is held the way a loader would read files: into pinned host memory

@@ -858,6 +858,7 @@ struct FastDec {
             br.lim = cs->buf.get() + cs->segs[seg].end;
             br.acc = 0;
             br.nbits = 0;
+            br.refill();   // the step schedule assumes >= 56 bits after a restart
             ++restarts;
             since = 0;
             o->pred[0] = o->pred[1] = o->pred[2] = 0;
@@ -875,10 +876,13 @@ struct FastDec {
         }
         begin_mcu();
     }
-    // one symbol: the DC difference of a block (k == 0) or one AC unit
+    // One symbol: the DC difference of a block (k == 0) or one AC unit.  Needs
+    // kFastBits buffered bits; a one-lookup symbol takes at most kFastBits, and
+    // the other paths refill first (>= 56 bits) and take at most 31 (16-bit
+    // code + 15 extra bits), so three steps per refill never run short:
+    // 56 -> 45 -> 34 fast, or >= 25 after a refilled slow step -> >= 14.
     __attribute__((always_inline)) void step()
     {
-        br.refill();
         if (k == 0) {
             int& p = o->pred[o->comp[bi]];
             const HuffTable& dc = *o->dc[bi];
@@ -887,6 +891,7 @@ struct FastDec {
                 br.skip(fd & 31);
                 p += fd >> 16;
             } else {
+                br.refill();
                 const int sz = fast_symbol(br, dc);
                 if (sz < 0 || sz > 11) return fail(1);
                 p += fast_extend(br, sz);
@@ -907,6 +912,7 @@ struct FastDec {
             if (k == 64) end_block();
             return;
         }
+        br.refill();
         const int rs = fast_symbol(br, ac);
         if (rs < 0) return fail(1);
         const int r = rs >> 4, sz = rs & 15;
@@ -920,6 +926,18 @@ struct FastDec {
         if (k > 63) return fail(1);
         out[k++] = static_cast<int16_t>(fast_extend(br, sz));
         if (k == 64) end_block();
+    }
+    // the rest of the file: three steps per refill
+    __attribute__((always_inline)) void finish()
+    {
+        while (!done) {
+            br.refill();
+            step();
+            if (done) break;
+            step();
+            if (done) break;
+            step();
+        }
     }
 };
 
@@ -954,7 +972,7 @@ int decode_scan(const uint8_t* d, size_t n, const Frame& f, const hjd_jpeg_info&
     BlockOrder oa;
     FastDec a;
     a.init(cs, oa, f, info, coefs);
-    while (!a.done) a.step();
+    a.finish();
     return a.report();
 }
 
@@ -971,13 +989,21 @@ void decode_scan_pair(const uint8_t* const d[2], const size_t n[2], const Frame*
     FastDec a, b;
     a.init(c0, oa, *f[0], *info[0], coefs[0]);
     b.init(c1, ob, *f[1], *info[1], coefs[1]);
-    while (!a.done && !b.done) {
+    while (!a.done && !b.done) {   // three interleaved step pairs per refill
+        a.br.refill();
+        b.br.refill();
+        a.step();
+        b.step();
+        if (a.done | b.done) break;
+        a.step();
+        b.step();
+        if (a.done | b.done) break;
         a.step();
         b.step();
     }
     const bool b_first = b.done && !a.done;
-    while (!a.done) a.step();
-    while (!b.done) b.step();
+    a.finish();
+    b.finish();
     if (b_first) {
         rc[1] = b.report();
         rc[0] = a.report();
