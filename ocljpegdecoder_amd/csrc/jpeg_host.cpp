@@ -795,11 +795,14 @@ struct BlockOrder {
 };
 
 // SeqDec on the de-stuffed reader; errors are recorded and reported (set_error)
-// after the loop, so nothing on the step path calls out.
+// after the loop, so nothing on the step path calls out.  A block's DC
+// difference is decoded when the block begins (after a refill), so a step is
+// one AC unit of the current block's table.
 struct FastDec {
     FastReader br;
     const CleanScan* cs = nullptr;
     BlockOrder* o = nullptr;
+    const HuffTable* act = nullptr;   // the current block's AC table
     size_t seg = 0;
     int bpm = 0, bi = 0, k = 0;
     int64_t nmcu = 0, m = 0;
@@ -842,11 +845,28 @@ struct FastDec {
         err = e;
         done = true;
     }
+    // zero the block and decode its DC difference (refilled: >= 56 bits, a DC
+    // symbol takes at most 27, so >= 29 remain for the step schedule)
     __attribute__((always_inline)) void begin_block()
     {
-        k = 0;
         out = coefs + (m * bpm + o->slot[bi]) * 64;
         memset(out, 0, 64 * sizeof(int16_t));
+        act = o->ac[bi];
+        br.refill();
+        int& p = o->pred[o->comp[bi]];
+        const HuffTable& dc = *o->dc[bi];
+        const int32_t fd = dc.fast_ac[br.peek(kFastBits)];
+        if (fd) {
+            br.skip(fd & 31);
+            p += fd >> 16;
+        } else {
+            const int sz = fast_symbol(br, dc);
+            if (sz < 0 || sz > 11) return fail(1);
+            p += fast_extend(br, sz);
+        }
+        if (p < -32768 || p > 32767) return fail(1);
+        out[0] = static_cast<int16_t>(p);
+        k = 1;
     }
     __attribute__((always_inline)) void begin_mcu()   // src/decoder.cpp:288-307
     {
@@ -858,7 +878,6 @@ struct FastDec {
             br.lim = cs->buf.get() + cs->segs[seg].end;
             br.acc = 0;
             br.nbits = 0;
-            br.refill();   // the step schedule assumes >= 56 bits after a restart
             ++restarts;
             since = 0;
             o->pred[0] = o->pred[1] = o->pred[2] = 0;
@@ -876,33 +895,14 @@ struct FastDec {
         }
         begin_mcu();
     }
-    // One symbol: the DC difference of a block (k == 0) or one AC unit.  Needs
-    // kFastBits buffered bits; a one-lookup symbol takes at most kFastBits, and
-    // the other paths refill first (>= 56 bits) and take at most 31 (16-bit
-    // code + 15 extra bits), so three steps per refill never run short:
-    // 56 -> 45 -> 34 fast, or >= 25 after a refilled slow step -> >= 14.
+    // One AC unit.  Needs kFastBits buffered bits; a one-lookup unit takes at
+    // most kFastBits, a slow unit refills first (>= 56 bits) and takes at most
+    // 31 (16-bit code + 15 extra bits), and a unit that ends the block leaves
+    // >= 29 (begin_block).  So three steps per refill never run short:
+    // 56 -> 45 -> 34 fast, or >= 25 after a refilled step -> >= 14.
     __attribute__((always_inline)) void step()
     {
-        if (k == 0) {
-            int& p = o->pred[o->comp[bi]];
-            const HuffTable& dc = *o->dc[bi];
-            const int32_t fd = dc.fast_ac[br.peek(kFastBits)];
-            if (fd) {
-                br.skip(fd & 31);
-                p += fd >> 16;
-            } else {
-                br.refill();
-                const int sz = fast_symbol(br, dc);
-                if (sz < 0 || sz > 11) return fail(1);
-                p += fast_extend(br, sz);
-            }
-            if (p < -32768 || p > 32767) return fail(1);
-            out[0] = static_cast<int16_t>(p);
-            k = 1;
-            return;
-        }
-        const HuffTable& ac = *o->ac[bi];
-        const int32_t fe = ac.fast_ac[br.peek(kFastBits)];
+        const int32_t fe = act->fast_ac[br.peek(kFastBits)];
         if (fe) {
             br.skip(fe & 31);
             if (fe & kFastEob) return end_block();
@@ -913,7 +913,7 @@ struct FastDec {
             return;
         }
         br.refill();
-        const int rs = fast_symbol(br, ac);
+        const int rs = fast_symbol(br, *act);
         if (rs < 0) return fail(1);
         const int r = rs >> 4, sz = rs & 15;
         if (sz == 0) {
