@@ -41,6 +41,8 @@ struct HuffTable {
     uint16_t fast[kFast];    // (length << 8) | symbol for codes of <= kFastBits bits; 0 = slow path
     // AC: (value << 16) | (run << 5) | (code + extra bits) when those fit kFastBits, else 0
     int32_t fast_ac[kFast];
+    // AC tables: up to two units per lookup (build_pairs; the de-stuffed reader's steps)
+    uint32_t fast2[kFast];
     int32_t maxcode[18];     // largest code of each length (-1: none)
     int32_t valptr[17];
     int32_t mincode[17];
@@ -80,7 +82,64 @@ inline int be16(const uint8_t* p) { return (p[0] << 8) | p[1]; }
 
 // fast = false: the canonical tables only (header parses for the GPU entropy
 // path, which builds its own device tables from counts / symbols).
-int build_table(HuffTable& t, const uint8_t counts[16], const uint8_t* symbols, int nsym, bool fast)
+// fast2 entries: bits 0-4 the bits taken (0: not covered), bit 5 the block
+// ends after them (an end of block among the units), bits 6-9 the zero run
+// before the first coefficient, bits 10-13 the distance from the first
+// coefficient to the second (0: one coefficient, written twice), bits 14-22 and
+// 23-31 the two values (9-bit signed).  A lookup covers: an end of block; a
+// nonzero coefficient; a coefficient and an end of block; or two coefficients
+// (second run <= 14) -- whatever of that is complete within the kFastBits
+// looked at, with |value| <= 255.
+constexpr uint32_t kPairEnd = 1u << 5;
+
+inline uint32_t pair_entry(int bits, bool end, int run1, int dist, int v1, int v2)
+{
+    return static_cast<uint32_t>(bits) | (end ? kPairEnd : 0) | (static_cast<uint32_t>(run1) << 6) |
+           (static_cast<uint32_t>(dist) << 10) | ((static_cast<uint32_t>(v1) & 0x1FF) << 14) |
+           ((static_cast<uint32_t>(v2) & 0x1FF) << 23);
+}
+
+// One unit at the top of `bits` (kFastBits wide, `avail` of them real): its
+// symbol, code length and extended value, if code and value bits fit `avail`.
+inline bool unit_at(const HuffTable& t, uint32_t bits, int avail, int& rs, int& used, int& value)
+{
+    const uint16_t e = t.fast[bits & (kFast - 1)];
+    if (!e) return false;
+    const int len = e >> 8, size = (e & 0xFF) & 15;
+    rs = e & 0xFF;
+    if (len + size > avail) return false;
+    used = len + size;
+    const int v = static_cast<int>((bits >> (kFastBits - used)) & ((1u << size) - 1));
+    value = size == 0 ? 0 : v < (1 << (size - 1)) ? v - (1 << size) + 1 : v;
+    return true;
+}
+
+void build_pairs(HuffTable& t)
+{
+    for (int idx = 0; idx < kFast; ++idx) {
+        uint32_t& out = t.fast2[idx];
+        out = 0;
+        int rs1, u1, v1;
+        if (!unit_at(t, static_cast<uint32_t>(idx), kFastBits, rs1, u1, v1)) continue;
+        if (rs1 == 0) {   // end of block
+            out = pair_entry(u1, true, 0, 0, 0, 0);
+            continue;
+        }
+        if ((rs1 & 15) == 0 || v1 < -255 || v1 > 255) continue;   // ZRL / wide values: the one-unit path
+        const int r1 = rs1 >> 4;
+        out = pair_entry(u1, false, r1, 0, v1, v1);
+        int rs2, u2, v2;
+        const uint32_t rest = (static_cast<uint32_t>(idx) << u1) & (kFast - 1);
+        if (!unit_at(t, rest, kFastBits - u1, rs2, u2, v2)) continue;
+        if (rs2 == 0) {
+            out = pair_entry(u1 + u2, true, r1, 0, v1, v1);
+        } else if ((rs2 & 15) != 0 && (rs2 >> 4) <= 14 && v2 >= -255 && v2 <= 255) {
+            out = pair_entry(u1 + u2, false, r1, (rs2 >> 4) + 1, v1, v2);
+        }
+    }
+}
+
+int build_table(HuffTable& t, const uint8_t counts[16], const uint8_t* symbols, int nsym, bool fast, bool ac)
 {
     if (fast) memset(t.fast, 0, sizeof(t.fast));
     memcpy(t.counts, counts, 16);
@@ -122,6 +181,7 @@ int build_table(HuffTable& t, const uint8_t counts[16], const uint8_t* symbols, 
         const int value = bits < (1 << (size - 1)) ? bits - (1 << size) + 1 : bits;
         t.fast_ac[idx] = static_cast<int32_t>((static_cast<uint32_t>(value) << 16) | (run << 5) | (len + size));
     }
+    if (ac) build_pairs(t);
     return 0;
 }
 
@@ -276,7 +336,7 @@ int parse_segments(const uint8_t* d, size_t n, size_t* pp, Frame& f, bool after_
                 for (int i = 0; i < 16; ++i) nsym += s[q + 1 + i];
                 if (nsym > 256 || q + 17 + nsym > sl) return set_error(HJD_E_INVALID, "bad DHT size");
                 HuffTable& t = tc ? f.ac[th] : f.dc[th];
-                if (build_table(t, s + q + 1, s + q + 17, nsym, f.decode_tables))
+                if (build_table(t, s + q + 1, s + q + 17, nsym, f.decode_tables, tc == 1))
                     return set_error(HJD_E_INVALID, "invalid Huffman table");
                 q += 17 + nsym;
             }
@@ -902,7 +962,20 @@ struct FastDec {
     // 56 -> 45 -> 34 fast, or >= 25 after a refilled step -> >= 14.
     __attribute__((always_inline)) void step()
     {
-        const int32_t fe = act->fast_ac[br.peek(kFastBits)];
+        const uint32_t idx = br.peek(kFastBits);
+        const uint32_t e2 = act->fast2[idx];
+        const int p1 = k + static_cast<int>((e2 >> 6) & 15);
+        const int p2 = p1 + static_cast<int>((e2 >> 10) & 15);
+        if (e2 && p2 < 63) {   // up to two units in one lookup, not the block's last position
+            br.skip(static_cast<int>(e2 & 31));
+            out[p1] = static_cast<int16_t>(static_cast<int32_t>(e2 << 9) >> 23);
+            out[p2] = static_cast<int16_t>(static_cast<int32_t>(e2) >> 23);
+            k = p2 + 1;
+            if (e2 & kPairEnd) end_block();
+            return;
+        }
+        // one unit (near position 63, where a second unit may belong to the next block)
+        const int32_t fe = act->fast_ac[idx];
         if (fe) {
             br.skip(fe & 31);
             if (fe & kFastEob) return end_block();
