@@ -84,20 +84,30 @@ def decode_coefs_into(data: bytes, out: np.ndarray) -> JpegInfo:
     return JpegInfo.from_c(info)
 
 
-def decode_coefs_batch(datas: Sequence[bytes], nthreads: int = 0) -> List[np.ndarray]:
-    """Decode many files on a host thread pool."""
+def decode_coefs_batch(datas: Sequence[bytes], nthreads: int = 0,
+                       outs: Optional[Sequence[np.ndarray]] = None) -> List[np.ndarray]:
+    """Decode many files on a host thread pool.  `outs`: one C-contiguous
+    (>= nblocks, 64) int16 array per file to decode into (reused buffers: no
+    allocation or first-touch page faults in the call), else new arrays."""
     lib = _lib.load()
     infos = [parse(d) for d in datas]
-    outs = [np.empty((i.nblocks, 64), np.int16) for i in infos]
+    if outs is None:
+        outs = [np.empty((i.nblocks, 64), np.int16) for i in infos]
+    else:
+        outs = list(outs)
+        if len(outs) != len(datas) or any(o.dtype != np.int16 or o.ndim != 2 or o.shape[1] != 64
+                                          or not o.flags.c_contiguous for o in outs):
+            raise ValueError("outs: one C-contiguous (n, 64) int16 array per file")
     cap = max([i.nblocks for i in infos] or [0])
     bufs = [_buf(d) for d in datas]
     arr_d = (_u8p * len(bufs))(*[ctypes.cast(b, _u8p) for b in bufs])
     arr_s = (ctypes.c_size_t * len(datas))(*[len(d) for d in datas])
     arr_o = (_i16p * len(outs))(*[o.ctypes.data_as(_i16p) for o in outs])
     status = (ctypes.c_int32 * len(datas))()
-    # every output holds exactly its own file's blocks: capacity checked per file
+    # capacity checked per file (the library takes one capacity for the batch)
     for o, i in zip(outs, infos):
-        assert o.shape[0] >= i.nblocks
+        if o.shape[0] < i.nblocks:
+            raise ValueError(f"output of {o.shape[0]} blocks < {i.nblocks}")
     check(lib.hjd_jpeg_decode_batch(arr_d, arr_s, len(datas), arr_o, cap, nthreads, status),
           "hjd_jpeg_decode_batch")
     return outs

@@ -146,3 +146,20 @@ def test_readers_agree(lib):
     assert decode(lib, _fill_bytes(rst, False))[0] == 0          # a fill byte before RSTn is legal
     assert decode(lib, _wrong_rst(rst))[0] != 0
     assert lib.hjd_debug_host_reader(2) != 0 and lib.hjd_debug_host_reader(-1) == 0
+
+
+def test_batch_into_given_outputs():
+    """decode_coefs_batch(outs=...): caller buffers (larger than needed) get the
+    same coefficients as fresh ones; a short buffer is refused before decoding."""
+    import ocljpegdecoder_amd as hjd
+    files = _corpus()[:6]
+    fresh = hjd.decode_coefs_batch(files, nthreads=2)
+    outs = [np.full((c.shape[0] + 7, 64), 0x5A5A, np.int16) for c in fresh]
+    got = hjd.decode_coefs_batch(files, nthreads=2, outs=outs)
+    assert all(g is o for g, o in zip(got, outs))
+    for c, o in zip(fresh, outs):
+        np.testing.assert_array_equal(o[: c.shape[0]], c)
+    with pytest.raises(ValueError):
+        hjd.decode_coefs_batch(files[:1], outs=[np.zeros((1, 64), np.int16)])
+    with pytest.raises(ValueError):
+        hjd.decode_coefs_batch(files[:2], outs=outs[:1])
