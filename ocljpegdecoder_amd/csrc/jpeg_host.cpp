@@ -3,10 +3,12 @@
 // Produces the fused kernel's input (int16 quantised zigzag coefficients,
 // MCU-major) from a baseline JPEG.  Covers the reference's L2/L3
 // (src/parser.cpp:7-419, src/decoder.cpp:72-365) with a fresh table-driven
-// design: a 64-bit bit accumulator with byte de-stuffing, a kFastBits first-level
-// lookup per Huffman table (canonical MAXCODE/VALPTR search for longer codes,
-// JPEG Annex F.2.2.3), restart-marker resynchronisation, and a thread pool
-// that decodes independent files in parallel.
+// design: kFastBits first-level lookups per Huffman table (canonical
+// MAXCODE/VALPTR search for longer codes, JPEG Annex F.2.2.3), up to two AC
+// units per lookup, a de-stuffed copy of the scan read with a branch-free
+// refill (a byte-wise reader for the rest), restart-marker resynchronisation,
+// two files per thread with interleaved steps, and a thread pool that decodes
+// independent files in parallel.
 #include <algorithm>
 #include <atomic>
 #include <cstring>
@@ -569,149 +571,6 @@ int decode_scan_bytewise(const uint8_t* d, size_t n, const Frame& f, const hjd_j
     return HJD_OK;
 }
 
-// ---- two files on one thread: interleaved symbol steps ---------------------
-// A Huffman decode is one long dependent chain per file (peek -> table load ->
-// shift -> next peek), so one thread decoding two independent files with their
-// symbol steps interleaved keeps two chains in flight: +10 % per thread on the
-// GPU box's EPYC 9575F (profiles/r05i_host_huffman_two_stream_probe.txt;
-// three files gain no more).  SeqDec is decode_scan + decode_block restated as
-// a one-symbol step with the same checks, errors and output, so the pair
-// decode is byte-identical to two decode_scan calls (tests/test_jpeg_host.py).
-struct SeqDec {
-    BitReader br;
-    const HuffTable* dc[kMaxBlocksPerMcu];
-    const HuffTable* ac[kMaxBlocksPerMcu];
-    int comp[kMaxBlocksPerMcu], slot[kMaxBlocksPerMcu];
-    int bpm = 0, bi = 0, k = 0;
-    int64_t nmcu = 0, m = 0;
-    int16_t* out = nullptr;
-    int16_t* coefs = nullptr;
-    int pred[3] = {0, 0, 0};
-    int ri = 0, since = 0, restarts = 0;
-    bool done = false;
-    int rc = HJD_OK;
-
-    void init(const uint8_t* d, size_t n, const Frame& f, const hjd_jpeg_info& info, int16_t* c)
-    {
-        br = BitReader{d + f.scan_offset, d + n};
-        const int nblk0 = f.ncomp == 1 ? 1 : f.comp[0].h * f.comp[0].v;   // as decode_scan
-        bpm = f.ncomp == 1 ? 1 : nblk0 + 2;
-        int j = 0;
-        for (int si = 0; si < f.ncomp; ++si) {
-            const int cc = f.scan_order[si];
-            const int nb = cc == 0 ? nblk0 : 1;
-            const int base = cc == 0 ? 0 : cc == 1 ? nblk0 : nblk0 + 1;
-            for (int b = 0; b < nb; ++b, ++j) {
-                dc[j] = &f.dc[f.comp[cc].td];
-                ac[j] = &f.ac[f.comp[cc].ta];
-                comp[j] = cc;
-                slot[j] = base + b;
-            }
-        }
-        nmcu = static_cast<int64_t>(info.mcu_w) * info.mcu_h;
-        ri = f.restart_interval;
-        coefs = c;
-        done = nmcu == 0;
-        if (!done) begin_mcu();
-    }
-    void fail(int code)
-    {
-        rc = code;
-        done = true;
-    }
-    void corrupt() { fail(set_error(HJD_E_INVALID, "corrupt entropy data in MCU %lld", static_cast<long long>(m))); }
-    void begin_block()
-    {
-        k = 0;
-        out = coefs + (m * bpm + slot[bi]) * 64;
-        memset(out, 0, 64 * sizeof(int16_t));
-    }
-    void begin_mcu()   // src/decoder.cpp:288-307
-    {
-        if (ri > 0 && since == ri) {
-            if (!br.restart(restarts))
-                return fail(set_error(HJD_E_INVALID, "expected RST%d before MCU %lld", restarts & 7,
-                                      static_cast<long long>(m)));
-            ++restarts;
-            since = 0;
-            pred[0] = pred[1] = pred[2] = 0;
-        }
-        ++since;
-        bi = 0;
-        begin_block();
-    }
-    void end_block()
-    {
-        if (++bi < bpm) return begin_block();
-        if (++m == nmcu) {
-            done = true;
-            return;
-        }
-        begin_mcu();
-    }
-    // one symbol: the DC difference of a block (k == 0) or one AC unit
-    __attribute__((always_inline)) void step()
-    {
-        if (br.nbits < 16) br.refill();
-        if (k == 0) {
-            int& p = pred[comp[bi]];
-            const int32_t fd = dc[bi]->fast_ac[br.peek(kFastBits)];
-            if (fd) {
-                br.skip(fd & 31);
-                p += fd >> 16;
-            } else {
-                const int sz = decode_symbol(br, *dc[bi]);
-                if (sz < 0 || sz > 11) return corrupt();
-                p += receive_extend(br, sz);
-            }
-            if (p < -32768 || p > 32767) return corrupt();
-            out[0] = static_cast<int16_t>(p);
-            k = 1;
-            return;
-        }
-        const int32_t fe = ac[bi]->fast_ac[br.peek(kFastBits)];
-        if (fe) {
-            br.skip(fe & 31);
-            if (fe & kFastEob) return end_block();
-            k += (fe >> 5) & 15;
-            if (k > 63) return corrupt();
-            out[k++] = static_cast<int16_t>(fe >> 16);
-            if (k == 64) end_block();
-            return;
-        }
-        const int rs = decode_symbol(br, *ac[bi]);
-        if (rs < 0) return corrupt();
-        const int r = rs >> 4, sz = rs & 15;
-        if (sz == 0) {
-            if (r != 15) return end_block();   // EOB
-            k += 16;                            // ZRL (a run to or past 64 ends the block, as decode_block)
-            if (k >= 64) end_block();
-            return;
-        }
-        k += r;
-        if (k > 63) return corrupt();
-        out[k++] = static_cast<int16_t>(receive_extend(br, sz));
-        if (k == 64) end_block();
-    }
-};
-
-// Two single-scan sequential files, interleaved; rc[i] as decode_scan_bytewise returns.
-void decode_scan_pair_bytewise(const uint8_t* const d[2], const size_t n[2], const Frame* const f[2],
-                      const hjd_jpeg_info* const info[2], int16_t* const coefs[2], int rc[2])
-{
-    SeqDec a, b;
-    a.init(d[0], n[0], *f[0], *info[0], coefs[0]);
-    b.init(d[1], n[1], *f[1], *info[1], coefs[1]);
-    while (!a.done && !b.done) {
-        a.step();
-        b.step();
-    }
-    while (!a.done) a.step();
-    while (!b.done) b.step();
-    rc[0] = a.rc;
-    rc[1] = b.rc;
-}
-
 // ---- the de-stuffed reader (the single-scan hot path) ----------------------
 // BitReader pays a data-dependent branch per symbol (refill when fewer than
 // 16 bits are left) and a byte loop at every 0xFF.  The hot path instead
@@ -841,7 +700,8 @@ __attribute__((always_inline)) inline int fast_extend(FastReader& br, int s)
 __attribute__((noinline, cold)) int report_error(int err, int64_t m, int restarts)
 {
     if (err == 1) return set_error(HJD_E_INVALID, "corrupt entropy data in MCU %lld", static_cast<long long>(m));
-    if (err == 2) return set_error(HJD_E_INVALID, "expected RST%d before MCU %lld", restarts & 7, static_cast<long long>(m));
+    if (err == 2)
+        return set_error(HJD_E_INVALID, "expected RST%d before MCU %lld", restarts & 7, static_cast<long long>(m));
     return HJD_OK;
 }
 
@@ -854,8 +714,9 @@ struct BlockOrder {
     int pred[3] = {0, 0, 0};
 };
 
-// SeqDec on the de-stuffed reader; errors are recorded and reported (set_error)
-// after the loop, so nothing on the step path calls out.  A block's DC
+// decode_scan_bytewise restated as a one-unit step on the de-stuffed reader,
+// with the same checks, errors and output.  Errors are recorded and reported
+// (set_error) after the loop, so nothing on the step path calls out.  A block's DC
 // difference is decoded when the block begins (after a refill), so a step is
 // one AC unit of the current block's table.
 struct FastDec {
@@ -1037,11 +898,9 @@ bool destuff_for(const uint8_t* d, size_t n, const Frame& f, const hjd_jpeg_info
            destuff_scan(d + f.scan_offset, d + n, scan_segments(f, info), cs);
 }
 
-// One single-scan sequential file (src/decoder.cpp:262-358).
-int decode_scan(const uint8_t* d, size_t n, const Frame& f, const hjd_jpeg_info& info, int16_t* coefs)
+// One single-scan sequential file (src/decoder.cpp:262-358), de-stuffed into cs.
+int decode_clean(const CleanScan& cs, const Frame& f, const hjd_jpeg_info& info, int16_t* coefs)
 {
-    CleanScan& cs = clean_scratch(0);
-    if (!destuff_for(d, n, f, info, cs)) return decode_scan_bytewise(d, n, f, info, coefs);
     BlockOrder oa;
     FastDec a;
     a.init(cs, oa, f, info, coefs);
@@ -1049,15 +908,32 @@ int decode_scan(const uint8_t* d, size_t n, const Frame& f, const hjd_jpeg_info&
     return a.report();
 }
 
-// Two single-scan sequential files, interleaved; rc[i] as decode_scan returns
-// (errors recorded in the order they occurred).
+int decode_scan(const uint8_t* d, size_t n, const Frame& f, const hjd_jpeg_info& info, int16_t* coefs)
+{
+    CleanScan& cs = clean_scratch(0);
+    return destuff_for(d, n, f, info, cs) ? decode_clean(cs, f, info, coefs)
+                                          : decode_scan_bytewise(d, n, f, info, coefs);
+}
+
+// Two single-scan sequential files on one thread, their steps interleaved: a
+// decode is one dependent chain (peek -> table load -> shift), so two files
+// keep two chains in flight (+10 % per thread when introduced,
+// profiles/r05i_host_huffman_two_stream_probe.txt).  rc[i] as decode_scan
+// returns (errors recorded in the order they occurred); a file the de-stuffed
+// reader declines is decoded alone, as decode_scan does.
 void decode_scan_pair(const uint8_t* const d[2], const size_t n[2], const Frame* const f[2],
                       const hjd_jpeg_info* const info[2], int16_t* const coefs[2], int rc[2])
 {
     CleanScan& c0 = clean_scratch(0);
     CleanScan& c1 = clean_scratch(1);
-    if (!destuff_for(d[0], n[0], *f[0], *info[0], c0) || !destuff_for(d[1], n[1], *f[1], *info[1], c1))
-        return decode_scan_pair_bytewise(d, n, f, info, coefs, rc);
+    const bool ok0 = destuff_for(d[0], n[0], *f[0], *info[0], c0);
+    const bool ok1 = destuff_for(d[1], n[1], *f[1], *info[1], c1);
+    if (!ok0 || !ok1) {
+        for (int i = 0; i < 2; ++i)
+            rc[i] = (i ? ok1 : ok0) ? decode_clean(i ? c1 : c0, *f[i], *info[i], coefs[i])
+                                    : decode_scan_bytewise(d[i], n[i], *f[i], *info[i], coefs[i]);
+        return;
+    }
     BlockOrder oa, ob;
     FastDec a, b;
     a.init(c0, oa, *f[0], *info[0], coefs[0]);
