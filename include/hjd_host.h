@@ -60,7 +60,14 @@ int hjd_jpeg_parse(const uint8_t* data, size_t size, hjd_jpeg_info* info);
 int hjd_jpeg_decode_coefs(const uint8_t* data, size_t size, hjd_jpeg_info* info, int16_t* coefs,
                           int64_t capacity_blocks);
 
-/* Decode n files on `nthreads` host threads (0 = hardware concurrency);
+/* The calling process's CPU share: the CPUs in its affinity mask, capped by
+ * its cgroup's CPU quota (cgroup v2 cpu.max, rounded up).  A container granted
+ * 16 CPUs of time on a 256-CPU host gets 16, not 256.  The default thread count
+ * (nthreads = 0) of hjd_jpeg_decode_batch, hjd_stream_create and
+ * hjd_gstream_create. */
+int hjd_host_cpu_share(void);
+
+/* Decode n files on `nthreads` host threads (0 = hjd_host_cpu_share());
  * status[i] receives each file's return code.  Returns HJD_OK if all
  * succeeded. */
 int hjd_jpeg_decode_batch(const uint8_t* const* datas, const size_t* sizes, int n, int16_t* const* coefs,
@@ -70,7 +77,7 @@ int hjd_jpeg_decode_batch(const uint8_t* const* datas, const size_t* sizes, int 
 typedef struct hjd_stream hjd_stream;
 
 /* nslots pinned staging slots of max_blocks coefficient blocks each (>= 2;
- * 3 = triple buffering); nthreads host Huffman workers (0 = hw concurrency). */
+ * 3 = triple buffering); nthreads host Huffman workers (0 = hjd_host_cpu_share()). */
 int hjd_stream_create(hjd_ctx* ctx, int64_t max_blocks, int nslots, int nthreads, hjd_stream** out);
 int hjd_stream_destroy(hjd_stream* s);
 

@@ -182,6 +182,7 @@ def _bind_host(lib):
                                                ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(ctypes.c_int32),
                                                ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]),
         "hjd_debug_host_reader": (ctypes.c_int, [ctypes.c_int]),
+        "hjd_host_cpu_share": (ctypes.c_int, []),
         "hjd_debug_destuff_host": (ctypes.c_int, [u8p, ctypes.c_size_t, u8p, ctypes.c_size_t,
                                                   ctypes.POINTER(ctypes.c_uint32), ctypes.c_int,
                                                   ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int64)]),

@@ -9,8 +9,12 @@
 // refill (a byte-wise reader for the rest), restart-marker resynchronisation,
 // two files per thread with interleaved steps, and a thread pool that decodes
 // independent files in parallel.
+#include <sched.h>
+
 #include <algorithm>
 #include <atomic>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <thread>
@@ -1384,6 +1388,24 @@ int hjd_internal::jpeg_decode_coefs_two(const uint8_t* const data[2], const size
 
 extern "C" {
 
+int hjd_host_cpu_share(void)
+{
+    int n = 0;
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof(set), &set) == 0) n = CPU_COUNT(&set);
+    if (n <= 0) n = static_cast<int>(std::max(1u, std::thread::hardware_concurrency()));
+    if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {   // "max 100000" or "<quota> <period>"
+        char q[32] = {0};
+        long long period = 0;
+        if (fscanf(f, "%31s %lld", q, &period) == 2 && strcmp(q, "max") != 0 && period > 0) {
+            const long long quota = atoll(q);
+            if (quota > 0) n = std::min<long long>(n, (quota + period - 1) / period);
+        }
+        fclose(f);
+    }
+    return std::max(1, n);
+}
+
 int hjd_jpeg_parse(const uint8_t* data, size_t size, hjd_jpeg_info* info)
 {
     if (!data || !info) return set_error(HJD_E_INVALID, "NULL argument");
@@ -1412,7 +1434,7 @@ int hjd_jpeg_decode_batch(const uint8_t* const* datas, const size_t* sizes, int 
                           int64_t capacity_blocks, int nthreads, int32_t* status)
 {
     if (n < 0 || (n > 0 && (!datas || !sizes || !coefs))) return set_error(HJD_E_INVALID, "invalid arguments");
-    if (nthreads <= 0) nthreads = static_cast<int>(std::max(1u, std::thread::hardware_concurrency()));
+    if (nthreads <= 0) nthreads = hjd_host_cpu_share();
     // each thread takes two files at a time (decode_two: interleaved symbol steps)
     nthreads = std::min(nthreads, std::max((n + 1) / 2, 1));
     std::atomic<int> next{0}, failed{0};

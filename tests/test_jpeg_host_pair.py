@@ -163,3 +163,15 @@ def test_batch_into_given_outputs():
         hjd.decode_coefs_batch(files[:1], outs=[np.zeros((1, 64), np.int16)])
     with pytest.raises(ValueError):
         hjd.decode_coefs_batch(files[:2], outs=outs[:1])
+
+
+def test_cpu_share_is_the_default_pool_size(lib):
+    """hjd_host_cpu_share (the nthreads = 0 default of the host pools): the
+    affinity mask capped by the cgroup's cpu.max quota -- the rule bench.py's
+    host_cpu_share applies."""
+    import bench
+    share = lib.hjd_host_cpu_share()
+    assert 1 <= share <= len(os.sched_getaffinity(0))
+    assert share == bench.host_cpu_share()[0]
+    status, outs = _batch(lib, _corpus()[:3], 4096, nthreads=0)   # default pool
+    assert list(status) == [0, 0, 0]
