@@ -417,3 +417,29 @@ def test_damaged_files_on_device(hjd, ctx, pinned, multiscan):
             np.testing.assert_array_equal(host[o:o + info.nblocks], ref)
             checked += 1
     assert flagged + staged_out > 0 and checked >= 2 * 16, (flagged, staged_out, checked)
+
+
+@pytest.mark.parametrize("sub_bits", [32, 1024])
+def test_edge_coefficients_on_device(hjd, ctx, sub_bits):
+    """The host decoder's edge blocks (tests/test_jpeg_host_pair.py: a last
+    coefficient at 63, ZRL runs, magnitudes 255/256/1023, DC-only and dense
+    blocks; with and without restart markers) through the GPU Huffman decode:
+    a batch (round-based sync) and one file per decoder (speculative sync)
+    return exactly the encoded coefficients."""
+    import jpeg_writer as JW
+    from test_jpeg_host_pair import FACTORS, _edge_blocks, _huff_src
+    datas, expect = [], []
+    for sampling, dri in ((1, 0), (1, 3), (0, 0), (3, 2)):
+        w, h = 96, 64
+        c = _edge_blocks(O.frame_blocks(w, h, sampling), seed=100 + sampling * 10 + dri)
+        _, qt = O.synthetic_coefs(16, 16, sampling, seed=1)
+        datas.append(JW.encode_frame(c, w, h, FACTORS[sampling], qt, _huff_src(), restart_interval=dri))
+        expect.append(c)
+    got, status = _coefs_gpu(hjd, ctx, datas, sub_bits)
+    for i, (g, e, s) in enumerate(zip(got, expect, status)):
+        assert s & ~1 == 0, (i, s)
+        np.testing.assert_array_equal(g, e, err_msg=f"batch file {i} S={sub_bits}")
+    for i, (d, e) in enumerate(zip(datas, expect)):
+        (g,), (s,) = _coefs_gpu(hjd, ctx, [d], sub_bits)
+        assert s & ~1 == 0, (i, s)
+        np.testing.assert_array_equal(g, e, err_msg=f"lone file {i} S={sub_bits}")

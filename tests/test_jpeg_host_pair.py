@@ -175,3 +175,70 @@ def test_cpu_share_is_the_default_pool_size(lib):
     assert share == bench.host_cpu_share()[0]
     status, outs = _batch(lib, _corpus()[:3], 4096, nthreads=0)   # default pool
     assert list(status) == [0, 0, 0]
+
+
+def _edge_blocks(n, seed):
+    """Quantised zigzag blocks aimed at the host decoder's lookup tables: the
+    last coefficient at 63 (no EOB), coefficients at 61-63, zero runs of 14-47
+    (ZRL), magnitudes at the 9-bit entry limit (255/256) and the AC maximum
+    (1023), DC-only blocks and dense blocks."""
+    rng = np.random.default_rng(seed)
+    out = np.zeros((n, 64), np.int16)
+    mags = np.array([1, 2, 3, 7, 31, 127, 255, 256, 511, 512, 1023])
+    for i in range(n):
+        kind = i % 8
+        b = out[i]
+        b[0] = rng.integers(-1000, 1000)
+        if kind == 0:                      # DC only
+            continue
+        if kind == 1:                      # a coefficient at 63, no EOB
+            b[63] = rng.choice([-1, 1, 5, -300])
+            b[rng.integers(1, 40)] = rng.integers(-3, 4)
+        elif kind == 2:                    # 61, 62, 63 (pairs near the end)
+            b[61:64] = rng.choice(mags, 3) * rng.choice([-1, 1], 3)
+        elif kind == 3:                    # zero runs of 14..47 (ZRL)
+            k = 1 + int(rng.integers(14, 48))
+            b[min(k, 63)] = rng.choice([-1, 2, 300])
+            if k + 16 < 63:
+                b[k + 16] = 1
+        elif kind == 4:                    # entry limits and the AC maximum
+            pos = np.sort(rng.choice(np.arange(1, 64), 6, replace=False))
+            b[pos] = rng.choice(mags, 6) * rng.choice([-1, 1], 6)
+        elif kind == 5:                    # dense, small values
+            b[1:] = rng.integers(-3, 4, 63)
+        elif kind == 6:                    # runs of exactly 15 and 16 before a coefficient
+            b[16] = 2
+            b[33] = -1
+            b[63] = 1
+        else:                              # random sparse
+            pos = rng.choice(np.arange(1, 64), int(rng.integers(1, 12)), replace=False)
+            b[pos] = rng.integers(-60, 61, pos.size)
+    return out
+
+
+@pytest.mark.parametrize("sampling,dri", [(1, 0), (1, 3), (0, 0), (3, 2)])
+def test_edge_coefficients_round_trip(lib, sampling, dri):
+    """Encode the edge blocks (tests/jpeg_writer.py, standard tables) and decode
+    them: the default reader alone, in a pair, and the byte-wise reader all
+    return exactly the encoded coefficients."""
+    w, h = 96, 64
+    nblk = O.frame_blocks(w, h, sampling)
+    coefs = _edge_blocks(nblk, seed=sampling * 10 + dri)
+    _, qt = O.synthetic_coefs(16, 16, sampling, seed=1)
+    data = JW.encode_frame(coefs, w, h, FACTORS[sampling], qt, _huff_src(), restart_interval=dri)
+    rc, info, got = decode(lib, data)
+    assert rc == 0 and info.nblocks == nblk
+    np.testing.assert_array_equal(got, coefs)
+    other = _corpus()[0]
+    cap = max(nblk, decode(lib, other)[1].nblocks)
+    status, outs = _batch(lib, [data, other, data], cap)   # a pair, then a lone file
+    assert list(status) == [0, 0, 0]
+    np.testing.assert_array_equal(outs[0][:nblk], coefs)
+    np.testing.assert_array_equal(outs[2][:nblk], coefs)
+    lib.hjd_debug_host_reader(1)
+    try:
+        rc, _, got = decode(lib, data)
+    finally:
+        lib.hjd_debug_host_reader(0)
+    assert rc == 0
+    np.testing.assert_array_equal(got, coefs)
