@@ -96,14 +96,9 @@ int destuff(const uint8_t* p, const uint8_t* end, uint8_t* out, size_t cap, std:
     int nrst = 0;
     seg_end.clear();
     while (p < end) {
-        const uint8_t* f = static_cast<const uint8_t*>(memchr(p, 0xFF, static_cast<size_t>(end - p)));
-        const uint8_t* run_end = f ? f : end;
-        const size_t n = static_cast<size_t>(run_end - p);
-        if (q + n > qend) return set_error(HJD_E_INVALID, "scan larger than the staging capacity");
-        memcpy(q, p, n);
-        q += n;
-        p = run_end;
-        if (!f) break;
+        p = hjd_internal::copy_until_ff(p, end, q, qend);
+        if (p == end) break;
+        if (*p != 0xFF) return set_error(HJD_E_INVALID, "scan larger than the staging capacity");
         if (p + 1 >= end) break;                       // truncated at FF
         const uint8_t b = p[1];
         if (b == 0x00) {                               // stuffed FF
@@ -458,8 +453,11 @@ struct EntBatchDev {
     struct SpecRec* spec;        // [sub][kMaxBpm]
     struct CandRec* cand;        // [sub][kSlots]
     uint8_t* cmap;               // [sub][kSlotRow]
-    uint8_t* cslot;              // [sub] the verified chain's slot (ent_chain_kernel)
+    uint8_t* cslot;              // [sub] the verified chain's slot (ent_chain_scan_kernel / ent_chain_kernel)
     uint32_t spec_lead;          // lead-in of the spec runs (bits)
+    uint32_t* chainfn;           // [frame][chain_chunks][5] each chunk's composed slot map (ent_chain_fn_kernel)
+    uint32_t* chain_broken;      // [frame] 1: the chain leaves its slots somewhere (serial walk with repairs)
+    uint32_t chain_chunks;       // chunks of the frame with the most subsequences (grid width)
 };
 
 
@@ -1052,62 +1050,131 @@ __device__ __forceinline__ SlotRow row_compose(const SlotRow& f, const SlotRow& 
     return r;
 }
 
-__global__ __launch_bounds__(kChainThreads) void ent_chain_kernel(EntBatchDev b)
+__device__ __forceinline__ SlotRow slot_ident()
 {
-    __shared__ ChainLds L;
-    const int tid = threadIdx.x;
-    const uint32_t f = blockIdx.x;
-    const EntFrame F = b.frames[f];
-    const uint32_t n = F.nsub;
-    uint8_t* cm = b.cmap + static_cast<uint64_t>(F.sub_base) * kSlotRow;
-    if (tid == 0) {
-        L.carry = 0;
-        L.tables_loaded = 0;
-    }
     SlotRow ident;
 #pragma unroll
     for (int i = 0; i < kRowWords; ++i) ident.w[i] = 0xFFFFFFFFu;
 #pragma unroll
     for (int s = 0; s < kChainSlots; ++s)
         ident.w[s >> 2] = (ident.w[s >> 2] & ~(0xFFu << ((s & 3) * 8))) | (static_cast<uint32_t>(s) << ((s & 3) * 8));
+    return ident;
+}
+
+// Rows c0 .. c0 + cn of a frame's slot maps (cm) into rows[]: 4-byte words,
+// coalesced, all of a thread's loads in flight at once; rows past cn: none.
+__device__ __forceinline__ void chunk_load(uint32_t (*rows)[kRowWords], const uint8_t* cm, uint32_t c0, uint32_t cn,
+                                           int tid)
+{
+    constexpr int kWords = kChainChunk * kRowWords / kChainThreads;   // 40
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(cm + static_cast<uint64_t>(c0) * kSlotRow);
+    uint32_t* dst = &rows[0][0];
+    const uint32_t nw = cn * kRowWords;
+    uint32_t t[kWords];
+#pragma unroll
+    for (int i = 0; i < kWords; ++i) {
+        const uint32_t j = static_cast<uint32_t>(tid + i * kChainThreads);
+        t[i] = j < nw ? src[j] : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (int i = 0; i < kWords; ++i) dst[tid + i * kChainThreads] = t[i];
+}
+
+// Thread t composes its kChainRows rows of the loaded chunk; the group scans
+// the functions (inclusive: fn[cur][t] = thread 0's rows then ... then t's).
+// Call after the rows are visible (barrier); returns cur.
+__device__ __forceinline__ int chunk_scan(uint32_t (*rows)[kRowWords], uint32_t (*fn)[kChainThreads][kRowWords],
+                                          uint32_t cn, int tid)
+{
+    const uint32_t r0 = static_cast<uint32_t>(tid) * kChainRows;
+    SlotRow v = slot_ident();
+#pragma unroll 1
+    for (uint32_t r = r0; r < r0 + kChainRows && r < cn; ++r) v = row_compose(v, row_load(rows[r]));
+#pragma unroll
+    for (int i = 0; i < kRowWords; ++i) fn[0][tid][i] = v.w[i];
+    __syncthreads();
+    int cur = 0;
+#pragma unroll 1
+    for (int d = 1; d < kChainThreads; d <<= 1) {
+        const SlotRow mine = row_load(fn[cur][tid]);
+        const SlotRow o = tid >= d ? row_compose(row_load(fn[cur][tid - d]), mine) : mine;
+#pragma unroll
+        for (int i = 0; i < kRowWords; ++i) fn[cur ^ 1][tid][i] = o.w[i];
+        cur ^= 1;
+        __syncthreads();
+    }
+    return cur;
+}
+
+// This thread's rows' chain slots (entering at `slot`) into cslot; returns the
+// slot after its last row.
+__device__ __forceinline__ uint32_t chunk_write_slots(const uint32_t (*rows)[kRowWords], uint8_t* cslot, uint32_t base,
+                                                      uint32_t cn, int tid, uint32_t slot)
+{
+    const uint32_t r0 = static_cast<uint32_t>(tid) * kChainRows;
+    uint32_t s = slot;
+    uint32_t packed[kChainRows / 4] = {};
+#pragma unroll
+    for (int i = 0; i < kChainRows; ++i) {
+        packed[i >> 2] |= (s & 0xFFu) << ((i & 3) * 8);
+        if (r0 + i < cn) s = row_get(row_load(rows[r0 + i]), s);
+    }
+    uint8_t* out = cslot + base + r0;
+    if (r0 + kChainRows <= cn && ((base + r0) & 3) == 0) {
+#pragma unroll
+        for (int i = 0; i < kChainRows / 4; ++i) reinterpret_cast<uint32_t*>(out)[i] = packed[i];
+    } else {
+        for (uint32_t i = 0; i < kChainRows && r0 + i < cn; ++i) out[i] = static_cast<uint8_t>(packed[i >> 2] >> ((i & 3) * 8));
+    }
+    return s;
+}
+
+// Group g of frame F: the ordered reduction of its owned subsequences' chain
+// statistics (one wave; lane = its lane) into agg, and the group marked linked.
+__device__ __forceinline__ void group_agg(const EntBatchDev& b, const EntFrame& F, uint32_t g, int lane)
+{
+    const uint32_t w = F.wg_base + g;
+    const uint32_t end = (g + 1) * kOwn < F.nsub ? (g + 1) * kOwn : F.nsub;
+    SubStats q[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {   // 4 x 64 >= kOwn; the four loads in flight together
+        const uint32_t k = g * kOwn + static_cast<uint32_t>(lane) * 4 + i;
+        q[i] = k < end ? sub_stats(b, F, k) : stats_identity();
+    }
+    SubStats a = stats_identity();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a = stats_combine(a, q[i]);
+    a = wave_reduce_ordered(a, lane);
+    if (lane == 0) {
+        b.agg[w] = a;
+        b.linked[w] = 1u;
+    }
+}
+
+__global__ __launch_bounds__(kChainThreads) void ent_chain_kernel(EntBatchDev b)
+{
+    __shared__ ChainLds L;
+    const int tid = threadIdx.x;
+    const uint32_t f = blockIdx.x;
+    const EntFrame F = b.frames[f];
+    // the chain kernels ran every chunk in parallel; walk serially only a frame
+    // where the chain leaves its slots (the repairs need the order)
+    const uint32_t n = b.chain_broken && b.chain_broken[f] == 0 ? 0u : F.nsub;
+    uint8_t* cm = b.cmap + static_cast<uint64_t>(F.sub_base) * kSlotRow;
+    if (tid == 0) {
+        L.carry = 0;
+        L.tables_loaded = 0;
+    }
     for (uint32_t c0 = 0; c0 < n; c0 += kChainChunk) {
         const uint32_t cn = n - c0 < static_cast<uint32_t>(kChainChunk) ? n - c0 : kChainChunk;
         const uint32_t r0 = static_cast<uint32_t>(tid) * kChainRows;   // this thread's rows within the chunk
         uint32_t slot;
         for (;;) {
             __syncthreads();
-            {   // the chunk's rows, 4-byte words, coalesced; all of a thread's loads in flight at once
-                constexpr int kWords = kChainChunk * kRowWords / kChainThreads;   // 40
-                const uint32_t* src = reinterpret_cast<const uint32_t*>(cm + static_cast<uint64_t>(c0) * kSlotRow);
-                uint32_t* dst = &L.rows[0][0];
-                const uint32_t nw = cn * kRowWords;
-                uint32_t t[kWords];
-#pragma unroll
-                for (int i = 0; i < kWords; ++i) {
-                    const uint32_t j = static_cast<uint32_t>(tid + i * kChainThreads);
-                    t[i] = j < nw ? src[j] : 0xFFFFFFFFu;
-                }
-#pragma unroll
-                for (int i = 0; i < kWords; ++i) dst[tid + i * kChainThreads] = t[i];
-            }
+            chunk_load(L.rows, cm, c0, cn, tid);
             if (tid == 0) L.brk = ~0ull;
             __syncthreads();
-            SlotRow v = ident;
-#pragma unroll 1
-            for (uint32_t r = r0; r < r0 + kChainRows && r < cn; ++r) v = row_compose(v, row_load(L.rows[r]));
-#pragma unroll
-            for (int i = 0; i < kRowWords; ++i) L.fn[0][tid][i] = v.w[i];
-            __syncthreads();
-            int cur = 0;
-#pragma unroll 1
-            for (int d = 1; d < kChainThreads; d <<= 1) {   // inclusive: fn[t] = thread 0's rows then ... then t's
-                const SlotRow mine = row_load(L.fn[cur][tid]);
-                const SlotRow o = tid >= d ? row_compose(row_load(L.fn[cur][tid - d]), mine) : mine;
-#pragma unroll
-                for (int i = 0; i < kRowWords; ++i) L.fn[cur ^ 1][tid][i] = o.w[i];
-                cur ^= 1;
-                __syncthreads();
-            }
+            const int cur = chunk_scan(L.rows, L.fn, cn, tid);
             const uint32_t carry = L.carry;
             slot = tid == 0 ? carry : (carry == kNoCand ? kNoCand : row_get(row_load(L.fn[cur][tid - 1]), carry));
             // the first subsequence without a slot: the row whose map sends the
@@ -1136,44 +1203,94 @@ __global__ __launch_bounds__(kChainThreads) void ent_chain_kernel(EntBatchDev b)
                              static_cast<uint32_t>(brk & 0xFF));
         }
         // the chain's slot of each of this thread's rows
-        uint32_t s = slot;
-        uint32_t packed[kChainRows / 4] = {};
-#pragma unroll
-        for (int i = 0; i < kChainRows; ++i) {
-            packed[i >> 2] |= (s & 0xFFu) << ((i & 3) * 8);
-            if (r0 + i < cn) s = row_get(row_load(L.rows[r0 + i]), s);
-        }
-        uint8_t* out = b.cslot + F.sub_base + c0 + r0;
-        if (r0 + kChainRows <= cn && ((F.sub_base + c0 + r0) & 3) == 0) {
-#pragma unroll
-            for (int i = 0; i < kChainRows / 4; ++i) reinterpret_cast<uint32_t*>(out)[i] = packed[i];
-        } else {
-            for (uint32_t i = 0; i < kChainRows && r0 + i < cn; ++i) out[i] = static_cast<uint8_t>(packed[i >> 2] >> ((i & 3) * 8));
-        }
+        const uint32_t s = chunk_write_slots(L.rows, b.cslot, F.sub_base + c0, cn, tid, slot);
         __syncthreads();
         if (r0 < cn && (r0 + kChainRows >= cn)) L.carry = s;   // the thread holding the chunk's last row
     }
+    if (b.chain_broken) return;   // ent_chain_agg_kernel reduces the groups, all in parallel
     __syncthreads();
-    // per group: ordered reduction of the owned statistics (one wave per group)
     const int wv = tid >> 6, lane = tid & 63;
-    for (uint32_t g = wv; g < frame_groups(n); g += kChainThreads / 64) {
-        const uint32_t w = F.wg_base + g;
-        const uint32_t end = (g + 1) * kOwn < n ? (g + 1) * kOwn : n;
-        SubStats q[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {   // 4 x 64 >= kOwn; the four loads in flight together
-            const uint32_t k = g * kOwn + lane * 4 + i;
-            q[i] = k < end ? sub_stats(b, F, k) : stats_identity();
-        }
-        SubStats a = stats_identity();
-#pragma unroll
-        for (int i = 0; i < 4; ++i) a = stats_combine(a, q[i]);
-        a = wave_reduce_ordered(a, lane);
-        if (lane == 0) {
-            b.agg[w] = a;
-            b.linked[w] = 1u;
-        }
+    for (uint32_t g = wv; g < frame_groups(F.nsub); g += kChainThreads / 64) group_agg(b, F, g, lane);
+}
+
+// ---- the chain, chunks in parallel (the case without repairs) -----------------
+// ent_chain_kernel's walk takes its chunks one after another (~20 us each; a
+// lone FHD frame has four).  Where no repair is needed the chunks are
+// independent given their entering slot, so two kernels over (chunk, frame)
+// run them side by side: ent_chain_fn_kernel composes each chunk's maps into
+// one function (chainfn); ent_chain_scan_kernel enters chunk c at the slot that
+// the functions of chunks 0 .. c-1 give slot 0, scans as the walk does and
+// writes its rows' slots.  A chunk that finds the chain leaving every slot
+// marks its frame (chain_broken), and ent_chain_kernel then walks that frame
+// serially with its repairs, overwriting the slots; it skips every other
+// frame's walk.  Same functions, same compositions: the same slots.
+struct ChainParLds {
+    uint32_t rows[kChainChunk][kRowWords];
+    uint32_t fn[2][kChainThreads][kRowWords];
+    uint32_t carry, broken;
+};
+
+__global__ __launch_bounds__(kChainThreads) void ent_chain_fn_kernel(EntBatchDev b)
+{
+    __shared__ ChainParLds L;
+    const int tid = threadIdx.x;
+    const uint32_t c = blockIdx.x, f = blockIdx.y;
+    const EntFrame F = b.frames[f];
+    if (c == 0 && tid == 0) b.chain_broken[f] = 0;
+    const uint32_t c0 = c * kChainChunk;
+    if (c0 >= F.nsub) return;
+    const uint32_t cn = F.nsub - c0 < static_cast<uint32_t>(kChainChunk) ? F.nsub - c0 : kChainChunk;
+    chunk_load(L.rows, b.cmap + static_cast<uint64_t>(F.sub_base) * kSlotRow, c0, cn, tid);
+    __syncthreads();
+    const int cur = chunk_scan(L.rows, L.fn, cn, tid);
+    if (tid < kRowWords)   // the last thread's inclusive function: the whole chunk
+        b.chainfn[(static_cast<uint64_t>(f) * b.chain_chunks + c) * kRowWords + tid] = L.fn[cur][kChainThreads - 1][tid];
+}
+
+__global__ __launch_bounds__(kChainThreads) void ent_chain_scan_kernel(EntBatchDev b)
+{
+    __shared__ ChainParLds L;
+    const int tid = threadIdx.x;
+    const uint32_t c = blockIdx.x, f = blockIdx.y;
+    const EntFrame F = b.frames[f];
+    const uint32_t n = F.nsub, c0 = c * kChainChunk;
+    if (c0 >= n) return;
+    const uint32_t cn = n - c0 < static_cast<uint32_t>(kChainChunk) ? n - c0 : kChainChunk;
+    if (tid == 0) {   // the slot entering this chunk: slot 0 through chunks 0 .. c-1
+        uint32_t s = 0;
+        for (uint32_t i = 0; i < c && s != kNoCand; ++i)
+            s = row_get(row_load(b.chainfn + (static_cast<uint64_t>(f) * b.chain_chunks + i) * kRowWords), s);
+        L.carry = s;
+        L.broken = 0;
     }
+    chunk_load(L.rows, b.cmap + static_cast<uint64_t>(F.sub_base) * kSlotRow, c0, cn, tid);
+    __syncthreads();
+    const int cur = chunk_scan(L.rows, L.fn, cn, tid);
+    const uint32_t carry = L.carry;
+    const uint32_t slot = tid == 0 ? carry : (carry == kNoCand ? kNoCand : row_get(row_load(L.fn[cur][tid - 1]), carry));
+    // a row whose map sends the chain's slot to none, before the frame's last
+    // subsequence: the serial walk repairs it (chunks after it enter at none)
+    const uint32_t r0 = static_cast<uint32_t>(tid) * kChainRows;
+    uint32_t s = slot;
+    for (uint32_t r = r0; r < r0 + kChainRows && r < cn && s != kNoCand; ++r) {
+        const uint32_t nx = row_get(row_load(L.rows[r]), s);
+        if (nx == kNoCand && c0 + r + 1 < n) L.broken = 1;
+        s = nx;
+    }
+    chunk_write_slots(L.rows, b.cslot, F.sub_base + c0, cn, tid, slot);
+    __syncthreads();
+    if (tid == 0 && L.broken) b.chain_broken[f] = 1;
+}
+
+// Every group of the batch, one wave each (after the chain's slots are final).
+__global__ __launch_bounds__(kChainThreads) void ent_chain_agg_kernel(EntBatchDev b)
+{
+    const int lane = threadIdx.x & 63;
+    const uint32_t w = blockIdx.x * (kChainThreads / 64) + (threadIdx.x >> 6);
+    if (w >= b.nwg) return;
+    const EntFrame F = b.frames[b.wg_frame[w]];
+    const uint32_t g = w - F.wg_base;
+    if (g < frame_groups(F.nsub)) group_agg(b, F, g, lane);
 }
 
 __global__ __launch_bounds__(256) void ent_link_kernel(EntBatchDev b)
@@ -1905,6 +2022,9 @@ struct hjd_gdec {
     CandRec* d_cand = nullptr;
     uint8_t* d_cmap = nullptr;
     uint8_t* d_cslot = nullptr;
+    uint32_t* d_chainfn = nullptr;
+    uint32_t* d_chain_broken = nullptr;
+    int64_t chain_fn_rows = 0;      // capacity of d_chainfn in chunk functions
     uint8_t* d_steps = nullptr;         // [table][1 << kStepBits] (ent_steps_kernel)
     hipEvent_t staged = nullptr, done = nullptr;
     int64_t last_h2d = 0;               // bytes the last issue moved host -> device
@@ -2221,6 +2341,12 @@ int hjd_gdec::assemble(uint8_t* blob, int16_t* coefs, int64_t* block_offsets, vo
     }
 
     d.ntiles = static_cast<uint32_t>(ntiles);
+    uint32_t max_nsub = 0;
+    for (int e = 0; e < ne; ++e) max_nsub = ef[e].nsub > max_nsub ? ef[e].nsub : max_nsub;
+    d.chain_chunks = (max_nsub + kChainChunk - 1) / kChainChunk;
+    if (d.chain_chunks == 0) d.chain_chunks = 1;
+    d.chainfn = nullptr;
+    d.chain_broken = nullptr;
     d.spec = nullptr;
     d.cand = nullptr;
     d.cmap = nullptr;
@@ -2296,6 +2422,11 @@ int gdec_alloc(hjd_gdec* g)
         HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_cand), sizeof(CandRec) * kCandRow * n));
         HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_cmap), kSlotRow * n));
         HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_cslot), n + 16));
+        // chunk functions: [entropy frame][chunks of the largest frame]
+        const size_t ef = kMaxScans * static_cast<size_t>(g->caps.max_frames);
+        g->chain_fn_rows = static_cast<int64_t>(ef * (n / kChainChunk + 1));
+        HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_chainfn), 4 * kRowWords * static_cast<size_t>(g->chain_fn_rows)));
+        HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_chain_broken), 4 * ef));
     }
     HJD_HIP(hipEventCreateWithFlags(&g->staged, hipEventDisableTiming));
     HJD_HIP(hipEventCreateWithFlags(&g->done, hipEventDisableTiming));
@@ -2323,8 +2454,19 @@ int launch_entropy(hjd_gdec* g, const EntBatchDev& b, hipStream_t s)
         HJD_HIP(hipGetLastError());
         hipLaunchKernelGGL(ent_cand_kernel, dim3(b.nwg, kMaxBpm), dim3(kGroupSubs), tl, s, b);
         HJD_HIP(hipGetLastError());
+        if (b.chain_broken) {   // chunks in parallel; the walk below then only repairs
+            hipLaunchKernelGGL(ent_chain_fn_kernel, dim3(b.chain_chunks, b.nframes), dim3(kChainThreads), 0, s, b);
+            HJD_HIP(hipGetLastError());
+            hipLaunchKernelGGL(ent_chain_scan_kernel, dim3(b.chain_chunks, b.nframes), dim3(kChainThreads), 0, s, b);
+            HJD_HIP(hipGetLastError());
+        }
         hipLaunchKernelGGL(ent_chain_kernel, dim3(b.nframes), dim3(kChainThreads), 0, s, b);   // + group records
         HJD_HIP(hipGetLastError());
+        if (b.chain_broken) {
+            hipLaunchKernelGGL(ent_chain_agg_kernel, dim3((b.nwg + kChainThreads / 64 - 1) / (kChainThreads / 64)),
+                               dim3(kChainThreads), 0, s, b);
+            HJD_HIP(hipGetLastError());
+        }
     } else {
         hipLaunchKernelGGL(ent_sync_kernel, dim3(b.nwg), dim3(kGroupSubs), sync_lds_bytes(b.ntab_max), s, b);
         HJD_HIP(hipGetLastError());
@@ -2376,6 +2518,10 @@ int gdec_issue(hjd_gdec* g, void* const* d_outs, const int32_t* pitches, int16_t
         b.cmap = g->d_cmap;
         b.cslot = g->d_cslot;
         b.spec_lead = spec_lead_bits();
+        if (static_cast<int64_t>(b.chain_chunks) * b.nframes <= g->chain_fn_rows) {
+            b.chainfn = g->d_chainfn;
+            b.chain_broken = g->d_chain_broken;
+        }
     }
     // the device buffers are reused: order this call after the previous one
     // (which may have been issued on another stream)
@@ -2609,7 +2755,7 @@ int hjd_gdec_destroy(hjd_gdec* g)
     if (g->h_status) (void)hipHostFree(g->h_status);
     void* dev[] = {g->d_blob, g->d_entries, g->d_stats, g->d_mids, g->d_stats1, g->d_wentries, g->d_linked, g->d_agg,
                    g->d_status, g->d_coefs, g->d_raw, g->d_tiles, g->d_spec, g->d_cand, g->d_cmap, g->d_cslot,
-                   g->d_steps};
+                   g->d_steps, g->d_chainfn, g->d_chain_broken};
     for (void* p : dev)
         if (p) (void)hipFree(p);
     if (g->staged) (void)hipEventDestroy(g->staged);

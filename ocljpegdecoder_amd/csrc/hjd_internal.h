@@ -130,3 +130,58 @@ std::vector<int> bind_current_thread(const CpuSet& s);
 void restore_current_thread(const std::vector<int>& prev);
 
 }  // namespace hjd_internal
+
+#ifndef __HIP_DEVICE_COMPILE__   // host code only (the device pass parses, never emits, its callers)
+#include <immintrin.h>
+#endif
+
+namespace hjd_internal {
+
+// The scan-copy step of both host destuff routines (jpeg_host.cpp
+// destuff_scan, hjd_entropy.hip destuff): copy the bytes of [s, end) before
+// the first 0xFF to o (advanced) and return where that 0xFF is (or end).
+// AVX2 compares, 64 bytes per test while none is an 0xFF, instead of a memchr
+// + memcpy call pair per run: entropy-coded data has an 0xFF every ~200 bytes,
+// so the calls' overhead dominated.  Vector steps store whole vectors (bytes
+// past the 0xFF are overwritten later) only while they fit before oend; the
+// rest is copied bytewise.  Returns a position that is not an 0xFF and not
+// end only when the output is full (o == oend).
+#ifndef __HIP_DEVICE_COMPILE__
+__attribute__((target("avx2"))) inline const uint8_t* copy_until_ff_avx2(const uint8_t* s, const uint8_t* end,
+                                                                          uint8_t*& o, uint8_t* oend)
+{
+    const __m256i ff = _mm256_set1_epi8(static_cast<char>(0xFF));
+    while (end - s >= 64 && oend - o >= 64) {
+        const __m256i a = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s));
+        const __m256i b = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + 32));
+        const uint32_t ma = static_cast<uint32_t>(_mm256_movemask_epi8(_mm256_cmpeq_epi8(a, ff)));
+        const uint32_t mb = static_cast<uint32_t>(_mm256_movemask_epi8(_mm256_cmpeq_epi8(b, ff)));
+        _mm256_storeu_si256(reinterpret_cast<__m256i*>(o), a);
+        _mm256_storeu_si256(reinterpret_cast<__m256i*>(o + 32), b);
+        if (ma | mb) {
+            const uint64_t m = (static_cast<uint64_t>(mb) << 32) | ma;
+            const int k = __builtin_ctzll(m);
+            o += k;
+            return s + k;
+        }
+        s += 64;
+        o += 64;
+    }
+    return s;
+}
+#endif
+
+inline const uint8_t* copy_until_ff(const uint8_t* s, const uint8_t* end, uint8_t*& o, uint8_t* oend)
+{
+#ifndef __HIP_DEVICE_COMPILE__
+    static const bool avx2 = __builtin_cpu_supports("avx2");
+    if (avx2) {
+        s = copy_until_ff_avx2(s, end, o, oend);
+        if (s < end && *s == 0xFF) return s;
+    }
+#endif
+    while (s < end && *s != 0xFF && o < oend) *o++ = *s++;
+    return s;
+}
+
+}  // namespace hjd_internal

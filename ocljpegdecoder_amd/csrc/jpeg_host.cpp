@@ -579,7 +579,7 @@ int decode_scan_bytewise(const uint8_t* d, size_t n, const Frame& f, const hjd_j
 // BitReader pays a data-dependent branch per symbol (refill when fewer than
 // 16 bits are left) and a byte loop at every 0xFF.  The hot path instead
 // copies the scan's entropy-coded data once without its byte stuffing
-// (memchr-driven, a few % of the decode) into per-thread scratch, one segment
+// (copy_until_ff, a few % of the decode) into per-thread scratch, one segment
 // per restart interval, each followed by 8 zero bytes, and then reads it with
 // an unconditional branch-free refill before every symbol: a 64-bit load at
 // the byte cursor, shifted under the bits still buffered (the cursor moves by
@@ -614,7 +614,7 @@ bool destuff_scan(const uint8_t* s, const uint8_t* end, int64_t max_segs, CleanS
 {
     const size_t n = static_cast<size_t>(end - s);
     max_segs = std::max<int64_t>(1, std::min<int64_t>(max_segs, static_cast<int64_t>(n / 2) + 1));
-    const size_t need = n + 8 * static_cast<size_t>(max_segs) + 8;
+    const size_t need = n + 8 * static_cast<size_t>(max_segs) + 8 + 16;   // + copy_until_ff's 16-byte stores
     if (cs.cap < need) {
         cs.buf.reset(new uint8_t[need]);
         cs.cap = need;
@@ -623,12 +623,10 @@ bool destuff_scan(const uint8_t* s, const uint8_t* end, int64_t max_segs, CleanS
     uint8_t* const o0 = cs.buf.get();
     uint8_t* o = o0;
     size_t begin = 0;
+    uint8_t* const oend = o0 + cs.cap;
     for (;;) {
-        const uint8_t* f = static_cast<const uint8_t*>(memchr(s, 0xFF, static_cast<size_t>(end - s)));
-        const uint8_t* stop = f ? f : end;
-        memcpy(o, s, static_cast<size_t>(stop - s));
-        o += stop - s;
-        s = stop;
+        s = hjd_internal::copy_until_ff(s, end, o, oend);
+        const uint8_t* f = s < end ? s : nullptr;   // at an 0xFF (the scratch always has room)
         int marker = -1;
         if (f) {
             if (f + 1 < end && f[1] == 0x00) {   // stuffed FF
