@@ -28,12 +28,10 @@ using hjd_internal::set_error;
 
 namespace {
 
-#ifndef HJD_HOST_FAST_BITS
-#define HJD_HOST_FAST_BITS 11
-#endif
 // first-level lookup width: 11 bits, +10 % per thread over 9 (EPYC 9575F, 4K q90;
-// profiles/r05d_host_huffman_lookup_bits_ab.json: 10 and 12 gain less)
-constexpr int kFastBits = HJD_HOST_FAST_BITS;
+// profiles/r05d_host_huffman_lookup_bits_ab.json: 10 and 12 gain less; with the
+// two-unit table too, profiles/README.md r05r)
+constexpr int kFastBits = 11;
 constexpr int kFast = 1 << kFastBits;
 constexpr int kMaxBlocksPerMcu = 6;   // 4:2:0 and 4:1:1 (4 luma + 2 chroma)
 // fast_ac flag of symbol 0x00 (AC end of block; a zero DC difference), value 0:
