@@ -579,12 +579,11 @@ int decode_scan_bytewise(const uint8_t* d, size_t n, const Frame& f, const hjd_j
 // copies the scan's entropy-coded data once without its byte stuffing
 // (copy_until_ff, a few % of the decode) into per-thread scratch, one segment
 // per restart interval, each followed by 8 zero bytes, and then reads it with
-// an unconditional branch-free refill before every symbol: a 64-bit load at
-// the byte cursor, shifted under the bits still buffered (the cursor moves by
-// the whole bytes taken and stops at the segment's end, so the reader sees
-// zeros past it, as BitReader does past a marker).  After a refill at least
-// 56 bits are buffered, enough for any one symbol (16-bit code + 11 extra
-// bits), so a step never refills again.
+// a branch-free refill: a 64-bit load at the byte cursor, shifted under the
+// bits still buffered (the cursor moves by the whole bytes taken and stops at
+// the segment's end, so the reader sees zeros past it, as BitReader does past
+// a marker).  A refill leaves at least 56 bits, which is what lets FastDec run
+// three symbol steps per refill (the bit budget is at FastDec::step).
 //
 // The bits a decode sees are the BitReader's exactly: de-stuffed FF00, fill
 // bytes in front of a marker dropped, zeros after the marker or the end of
@@ -612,7 +611,8 @@ bool destuff_scan(const uint8_t* s, const uint8_t* end, int64_t max_segs, CleanS
 {
     const size_t n = static_cast<size_t>(end - s);
     max_segs = std::max<int64_t>(1, std::min<int64_t>(max_segs, static_cast<int64_t>(n / 2) + 1));
-    const size_t need = n + 8 * static_cast<size_t>(max_segs) + 8 + 16;   // + copy_until_ff's 16-byte stores
+    // + 64: copy_until_ff stores whole 64-byte vectors while that many fit
+    const size_t need = n + 8 * static_cast<size_t>(max_segs) + 8 + 64;
     if (cs.cap < need) {
         cs.buf.reset(new uint8_t[need]);
         cs.cap = need;
