@@ -174,7 +174,10 @@ __attribute__((target("avx2"))) inline const uint8_t* copy_until_ff_avx2(const u
 inline const uint8_t* copy_until_ff(const uint8_t* s, const uint8_t* end, uint8_t*& o, uint8_t* oend)
 {
 #ifndef __HIP_DEVICE_COMPILE__
-    static const bool avx2 = __builtin_cpu_supports("avx2");
+    static const bool avx2 = [] {
+        __builtin_cpu_init();
+        return __builtin_cpu_supports("avx2") != 0;
+    }();
     if (avx2) {
         s = copy_until_ff_avx2(s, end, o, oend);
         if (s < end && *s == 0xFF) return s;
