@@ -166,7 +166,8 @@ int hjd_plan_launch(hjd_plan* plan, const void* d_coefs, void* d_out, void* stre
 int hjd_plan_autotune(hjd_plan* plan, const void* d_coefs, void* d_out, void* stream, int rounds,
                       int32_t* tasks_per_wave, int32_t* variant);
 /* hjd_plan_autotune's choice is cached per process (device x sampling x
- * input format x output format x the other variant bits x floor(log2 tasks)):
+ * input format x output format x the other variant bits x frame count x
+ * task count):
  * a later plan of the same key takes it with no launch (and d_out is then NOT
  * written).  HJD_AUTOTUNE_CACHE=0 disables the cache; this empties it. */
 int hjd_autotune_cache_clear(void);

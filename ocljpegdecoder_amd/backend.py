@@ -240,7 +240,11 @@ class Plan:
 
     def autotune(self, coefs, out, stream=None, rounds: int = 2):
         """hjd_plan_autotune: time the launch shapes on these buffers and keep
-        the fastest for later launches; returns (tasks_per_wave, variant)."""
+        the fastest for later launches; returns (tasks_per_wave, variant).
+        The choice is cached per process by kernel and batch geometry
+        (include/hjd.h): on a cache hit nothing is launched and `out` is NOT
+        written -- call launch() for a decode (launch_shape()["autotune_cached"]
+        tells which happened)."""
         cp = self._check_tensor(coefs, "coefs", self.coef_elem_bytes, self.coef_elems_needed * self.coef_elem_bytes)
         op = self._check_tensor(out, "out", 0, self.out_bytes_needed)
         tpw, var = ctypes.c_int32(0), ctypes.c_int32(0)

@@ -550,26 +550,19 @@ int hjd_plan_launch(hjd_plan* plan, const void* d_coefs, void* d_out, void* stre
 // launch (the search cost ~1 s per plan).  HJD_AUTOTUNE_CACHE=0
 // disables the cache; hjd_autotune_cache_clear() empties it.
 namespace {
+// A cached choice applies to plans of the same kernel and batch geometry
+// (frame count and task count), not just the same size octave.
 struct TuneKey {
-    int device, sampling, input_format, out_format, keep_variant, octave;
+    int device, sampling, input_format, out_format, keep_variant, nframes;
+    int64_t tasks;
     bool operator<(const TuneKey& o) const
     {
-        return std::tie(device, sampling, input_format, out_format, keep_variant, octave) <
-               std::tie(o.device, o.sampling, o.input_format, o.out_format, o.keep_variant, o.octave);
+        return std::tie(device, sampling, input_format, out_format, keep_variant, nframes, tasks) <
+               std::tie(o.device, o.sampling, o.input_format, o.out_format, o.keep_variant, o.nframes, o.tasks);
     }
 };
 std::mutex g_tune_mu;
 std::map<TuneKey, std::pair<int, int>> g_tune;   // -> (tasks per wave, store bit)
-
-int octave_of(int64_t n)
-{
-    int k = 0;
-    while (n > 1) {
-        n >>= 1;
-        ++k;
-    }
-    return k;
-}
 
 bool tune_cache_enabled()
 {
@@ -601,8 +594,8 @@ int hjd_plan_autotune(hjd_plan* plan, const void* d_coefs, void* d_out, void* st
     plan->autotune_cached = 0;
     if (plan->tasks == 0 || !plan_is_persistent(plan)) return report();
     const int keep = plan->variant & ~1;
-    const TuneKey key{plan->ctx->device, plan->sampling, plan->input_format, plan->out_format, keep,
-                      octave_of(plan->tasks)};
+    const TuneKey key{plan->ctx->device, plan->sampling, plan->input_format, plan->out_format, keep, plan->nframes,
+                      plan->tasks};
     if (tune_cache_enabled()) {
         std::lock_guard<std::mutex> lock(g_tune_mu);
         auto it = g_tune.find(key);

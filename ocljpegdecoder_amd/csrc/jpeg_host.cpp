@@ -51,7 +51,26 @@ struct HuffTable {
     int32_t valptr[17];
     int32_t mincode[17];
     uint8_t vals[256];
+    // what the arrays above were last built from (counts / vals / nsym) and how:
+    // a DHT with the same spec reuses them (build_table)
+    bool built = false, built_fast = false, built_ac = false;
 };
+
+// A frame's eight Huffman tables (~165 KB with their lookup arrays) live in
+// per-thread heap storage, not in Frame on the stack, and stay built across
+// files: the config-5 pool repeats one set of tables in every file.  Set 0 and
+// 1 hold decode_two's two frames (decode_one uses 0), set 2 the header-only
+// parses, so a parse never clobbers the tables of a decode on the same thread.
+struct TableSet {
+    HuffTable dc[4], ac[4];
+};
+
+TableSet& table_set(int i)
+{
+    thread_local std::unique_ptr<TableSet> sets[3];
+    if (!sets[i]) sets[i].reset(new TableSet);
+    return *sets[i];
+}
 
 struct Component {
     int id = 0, h = 1, v = 1, tq = 0;
@@ -73,13 +92,25 @@ struct Frame {
     Component comp[3];
     int32_t qt[4][64] = {};
     int qt_prec[4] = {-1, -1, -1, -1};
-    HuffTable dc[4], ac[4];
+    HuffTable* dc;                   // [4] each, in table_set(set)
+    HuffTable* ac;
     int restart_interval = 0;
     int scan_order[3] = {0, 1, 2};   // frame component index of each scan component (first scan)
     size_t scan_offset = 0;
     int sampling = -1;
     ScanSpec scan;                   // the scan parse_segments stopped at
-    bool decode_tables = true;       // build the host decoder's lookup tables (false: header parse only)
+    bool decode_tables;              // build the host decoder's lookup tables (false: header parse only)
+
+    // decode: table set 0 or 1; header-only parse (no lookup tables): set 2
+    explicit Frame(int set, bool tables = true) : decode_tables(tables)
+    {
+        TableSet& ts = table_set(tables ? set : 2);
+        dc = ts.dc;
+        ac = ts.ac;
+        for (int i = 0; i < 4; ++i) dc[i].defined = ac[i].defined = false;
+    }
+    Frame(const Frame&) = delete;
+    Frame& operator=(const Frame&) = delete;
 };
 
 inline int be16(const uint8_t* p) { return (p[0] << 8) | p[1]; }
@@ -145,6 +176,12 @@ void build_pairs(HuffTable& t)
 
 int build_table(HuffTable& t, const uint8_t counts[16], const uint8_t* symbols, int nsym, bool fast, bool ac)
 {
+    if (t.built && t.built_fast == fast && t.built_ac == ac && t.nsym == nsym && memcmp(t.counts, counts, 16) == 0 &&
+        memcmp(t.vals, symbols, static_cast<size_t>(nsym)) == 0) {
+        t.defined = true;   // the spec these arrays were built from
+        return 0;
+    }
+    t.built = false;
     if (fast) memset(t.fast, 0, sizeof(t.fast));
     memcpy(t.counts, counts, 16);
     t.nsym = nsym;
@@ -168,6 +205,9 @@ int build_table(HuffTable& t, const uint8_t counts[16], const uint8_t* symbols, 
     }
     t.maxcode[17] = 0x7fffffff;
     t.defined = true;
+    t.built = true;
+    t.built_fast = fast;
+    t.built_ac = ac;
     if (!fast) return 0;
     // combined AC entries: symbol and its extra bits in one lookup (nonzero
     // coefficients whose code + magnitude bits fit the kFastBits index)
@@ -412,6 +452,7 @@ struct BitReader {
     uint64_t acc = 0;
     int nbits = 0;
     bool at_marker = false;
+    int64_t virt = 0;   // zero bits fed past the marker / the end of the data
 
     void refill()
     {
@@ -431,12 +472,15 @@ struct BitReader {
         }
         while (nbits <= 56) {
             uint64_t b = 0;
+            bool real = false;
             if (!at_marker && p < end) {
                 if (p[0] != 0xFF) {
                     b = *p++;
+                    real = true;
                 } else if (p + 1 < end && p[1] == 0x00) {
                     b = 0xFF;
                     p += 2;
+                    real = true;
                 } else if (p + 1 < end && p[1] == 0xFF) {
                     ++p;                // a fill byte: the pair starts at the next 0xFF
                     continue;           // (src/decoder.cpp:121-134, FF FF -> look at the next byte)
@@ -446,19 +490,32 @@ struct BitReader {
             }
             acc |= b << (56 - nbits);
             nbits += 8;
+            if (!real) virt += 8;
         }
     }
+    // The decode took bits past the data (the zeros fed after it): the
+    // reference's cacheEof (src/bitstream.h:322-331), checked as it does
+    // before every component after the first (src/decoder.cpp:310-314).
+    bool overrun() const { return virt > nbits; }
     uint32_t peek(int n) const { return static_cast<uint32_t>(acc >> (64 - n)); }
     void skip(int n) { acc <<= n; nbits -= n; }
 
-    // Restart: drop buffered bits, expect RSTn at the next marker.
+    // Restart: drop buffered bits, expect RSTn at the next marker.  The
+    // reference aligns to the next byte and reads it as the marker
+    // (src/decoder.cpp:295-302), so a whole byte of the interval left
+    // undecoded (or a decode past the interval's data) fails here too.
     bool restart(int expect)
     {
+        bool spare = nbits - virt >= 8 || virt > nbits;
         acc = 0;
         nbits = 0;
+        virt = 0;
         if (!at_marker) {
+            const uint8_t* q = p;
             while (p + 1 < end && !(p[0] == 0xFF && p[1] != 0x00)) ++p;
+            spare |= p != q;
         }
+        if (spare) return false;
         while (p < end && p[0] == 0xFF) ++p;   // marker prefix + fill bytes
         if (p >= end || *p != 0xD0 + (expect & 7)) return false;
         ++p;
@@ -538,6 +595,17 @@ inline bool decode_block(BitReader& br, const HuffTable& dc, const HuffTable& ac
     return true;
 }
 
+// The scan's data ended inside MCU m: the reference's "data incomplete"
+// (src/decoder.cpp:310-313; load_jpg then stops, src/parser.cpp:384-388).
+// One stricter case: the reference checks before each component but not after
+// the last one, so a file cut inside the last MCU's last component decodes
+// there from whatever its buffer holds past the data; this decoder rejects it.
+__attribute__((noinline, cold)) int report_incomplete(int64_t m, int64_t nmcu)
+{
+    return set_error(HJD_E_INVALID, "entropy data incomplete or truncated (MCU %lld of %lld)",
+                     static_cast<long long>(m), static_cast<long long>(nmcu));
+}
+
 int decode_scan_bytewise(const uint8_t* d, size_t n, const Frame& f, const hjd_jpeg_info& info, int16_t* coefs)
 {
     BitReader br{d + f.scan_offset, d + n};
@@ -552,6 +620,7 @@ int decode_scan_bytewise(const uint8_t* d, size_t n, const Frame& f, const hjd_j
     const int64_t nmcu = static_cast<int64_t>(info.mcu_w) * info.mcu_h;
     int restarts = 0, since = 0;
     for (int64_t m = 0; m < nmcu; ++m) {
+        if (br.overrun()) return report_incomplete(m - 1, nmcu);
         if (f.restart_interval > 0 && since == f.restart_interval) {   // src/decoder.cpp:288-307
             if (!br.restart(restarts)) return set_error(HJD_E_INVALID, "expected RST%d before MCU %lld", restarts & 7,
                                                       static_cast<long long>(m));
@@ -570,7 +639,7 @@ int decode_scan_bytewise(const uint8_t* d, size_t n, const Frame& f, const hjd_j
                     return set_error(HJD_E_INVALID, "corrupt entropy data in MCU %lld", static_cast<long long>(m));
         }
     }
-    return HJD_OK;
+    return br.overrun() ? report_incomplete(nmcu - 1, nmcu) : HJD_OK;
 }
 
 // ---- the de-stuffed reader (the single-scan hot path) ----------------------
@@ -656,12 +725,13 @@ struct FastReader {
     __attribute__((always_inline)) void refill()
     {
         uint64_t v;
-        memcpy(&v, p, 8);
+        memcpy(&v, p < lim ? p : lim, 8);   // at or past the end: the 8 zero bytes after it
         acc |= __builtin_bswap64(v) >> nbits;
-        p += (63 - nbits) >> 3;
-        p = p < lim ? p : lim;
+        p += (63 - nbits) >> 3;             // not clamped: p - lim counts the zero bytes taken
         nbits |= 56;
     }
+    // bits of the segment not taken yet; < 0: the decode read past its data
+    int64_t left() const { return 8 * (lim - p) + nbits; }
     uint32_t peek(int n) const { return static_cast<uint32_t>(acc >> (64 - n)); }
     void skip(int n)
     {
@@ -697,11 +767,12 @@ __attribute__((always_inline)) inline int fast_extend(FastReader& br, int s)
     return v < (1 << (s - 1)) ? v - (1 << s) + 1 : v;
 }
 
-__attribute__((noinline, cold)) int report_error(int err, int64_t m, int restarts)
+__attribute__((noinline, cold)) int report_error(int err, int64_t m, int64_t nmcu, int restarts)
 {
     if (err == 1) return set_error(HJD_E_INVALID, "corrupt entropy data in MCU %lld", static_cast<long long>(m));
     if (err == 2)
         return set_error(HJD_E_INVALID, "expected RST%d before MCU %lld", restarts & 7, static_cast<long long>(m));
+    if (err == 3) return report_incomplete(m - 1, nmcu);
     return HJD_OK;
 }
 
@@ -731,7 +802,7 @@ struct FastDec {
     int16_t* coefs = nullptr;
     int ri = 0, since = 0, restarts = 0;
     bool done = false;
-    int err = 0;   // 1: corrupt entropy data in MCU m, 2: expected RSTn before MCU m
+    int err = 0;   // 1: corrupt entropy data in MCU m, 2: expected RSTn before MCU m, 3: data ended in MCU m-1
 
     __attribute__((always_inline)) void init(const CleanScan& c, BlockOrder& ord, const Frame& f,
                                              const hjd_jpeg_info& info, int16_t* co)
@@ -760,7 +831,7 @@ struct FastDec {
         done = nmcu == 0;
         if (!done) begin_mcu();
     }
-    __attribute__((always_inline)) int report() const { return report_error(err, m, restarts); }
+    __attribute__((always_inline)) int report() const { return report_error(err, m, nmcu, restarts); }
     __attribute__((always_inline)) void fail(int e)
     {
         err = e;
@@ -789,11 +860,15 @@ struct FastDec {
         out[0] = static_cast<int16_t>(p);
         k = 1;
     }
-    __attribute__((always_inline)) void begin_mcu()   // src/decoder.cpp:288-307
+    __attribute__((always_inline)) void begin_mcu()   // src/decoder.cpp:288-314
     {
+        // the previous MCU read past the segment's data (BitReader::overrun)
+        if (br.left() < 0) return fail(3);
         if (ri > 0 && since == ri) {
+            // the reference reads the byte after the interval's last bits as the
+            // marker (src/decoder.cpp:295-302): a whole byte left is a mismatch
             const CleanSeg& s = cs->segs[seg];
-            if (s.marker != 0xD0 + (restarts & 7) || seg + 1 >= cs->segs.size()) return fail(2);
+            if (s.marker != 0xD0 + (restarts & 7) || seg + 1 >= cs->segs.size() || br.left() >= 8) return fail(2);
             ++seg;
             br.p = cs->buf.get() + cs->segs[seg].begin;
             br.lim = cs->buf.get() + cs->segs[seg].end;
@@ -811,6 +886,7 @@ struct FastDec {
     {
         if (++bi < bpm) return begin_block();
         if (++m == nmcu) {
+            if (br.left() < 0) return fail(3);
             done = true;
             return;
         }
@@ -879,11 +955,25 @@ struct FastDec {
 // admits it, 1 the byte-wise reader always (hjd_debug_host_reader: tests).
 std::atomic<int> g_host_reader{0};
 
-// Scratch of the de-stuffed reader, two per thread (the pair decode).
+// Scratch of the de-stuffed reader, two per thread (the pair decode).  A
+// buffer grows to the largest scan its thread has de-stuffed (a 4K q90 scan:
+// a few MB) and stays for the next file; one past kScratchKeep (an outlier
+// scan) is released after its decode, so a long-lived worker holds at most
+// 2 x kScratchKeep.
+constexpr size_t kScratchKeep = size_t{32} << 20;
+
 CleanScan& clean_scratch(int i)
 {
     thread_local CleanScan cs[2];
     return cs[i];
+}
+
+void trim_scratch(CleanScan& cs)
+{
+    if (cs.cap <= kScratchKeep) return;
+    cs.buf.reset();
+    cs.cap = 0;
+    std::vector<CleanSeg>().swap(cs.segs);
 }
 
 int64_t scan_segments(const Frame& f, const hjd_jpeg_info& info)
@@ -911,8 +1001,10 @@ int decode_clean(const CleanScan& cs, const Frame& f, const hjd_jpeg_info& info,
 int decode_scan(const uint8_t* d, size_t n, const Frame& f, const hjd_jpeg_info& info, int16_t* coefs)
 {
     CleanScan& cs = clean_scratch(0);
-    return destuff_for(d, n, f, info, cs) ? decode_clean(cs, f, info, coefs)
-                                          : decode_scan_bytewise(d, n, f, info, coefs);
+    const int rc = destuff_for(d, n, f, info, cs) ? decode_clean(cs, f, info, coefs)
+                                                  : decode_scan_bytewise(d, n, f, info, coefs);
+    trim_scratch(cs);
+    return rc;
 }
 
 // Two single-scan sequential files on one thread, their steps interleaved: a
@@ -932,6 +1024,8 @@ void decode_scan_pair(const uint8_t* const d[2], const size_t n[2], const Frame*
         for (int i = 0; i < 2; ++i)
             rc[i] = (i ? ok1 : ok0) ? decode_clean(i ? c1 : c0, *f[i], *info[i], coefs[i])
                                     : decode_scan_bytewise(d[i], n[i], *f[i], *info[i], coefs[i]);
+        trim_scratch(c0);
+        trim_scratch(c1);
         return;
     }
     BlockOrder oa, ob;
@@ -960,6 +1054,8 @@ void decode_scan_pair(const uint8_t* const d[2], const size_t n[2], const Frame*
         rc[0] = a.report();
         rc[1] = b.report();
     }
+    trim_scratch(c0);
+    trim_scratch(c1);
 }
 
 // ---- several scans per frame: sequential multi-scan and progressive -------
@@ -1149,6 +1245,7 @@ int decode_scan_any(const uint8_t* d, size_t n, const Frame& f, const CoefLayout
     };
     int restarts = 0, since = 0;
     for (int64_t u = 0; u < units; ++u) {
+        if (br.overrun()) return report_incomplete(u - 1, units);
         if (f.restart_interval > 0 && since == f.restart_interval) {
             if (!br.restart(restarts))
                 return set_error(HJD_E_INVALID, "expected RST%d before MCU %lld", restarts & 7, static_cast<long long>(u));
@@ -1171,6 +1268,7 @@ int decode_scan_any(const uint8_t* d, size_t n, const Frame& f, const CoefLayout
         }
         if (!ok) return set_error(HJD_E_INVALID, "corrupt entropy data in MCU %lld", static_cast<long long>(u));
     }
+    if (br.overrun()) return report_incomplete(units - 1, units);
     // next marker: the reader stops in front of one, or is short of it by the
     // bytes it has not needed yet (entropy data: 0xFF only as FF00 / RSTn)
     const uint8_t* q = br.p;
@@ -1231,7 +1329,7 @@ int decode_prepared(const uint8_t* data, size_t size, Frame& f, hjd_jpeg_info* i
 
 int decode_one(const uint8_t* data, size_t size, hjd_jpeg_info* info, int16_t* coefs, int64_t capacity)
 {
-    Frame f;
+    Frame f(0);
     const int rc = prepare_one(data, size, info, coefs, capacity, f);
     return rc ? rc : decode_prepared(data, size, f, info, coefs);
 }
@@ -1241,7 +1339,7 @@ int decode_one(const uint8_t* data, size_t size, hjd_jpeg_info* info, int16_t* c
 void decode_two(const uint8_t* const data[2], const size_t size[2], hjd_jpeg_info* const info[2],
                 int16_t* const coefs[2], const int64_t capacity[2], int rc[2])
 {
-    Frame f[2];
+    Frame f[2] = {Frame(0), Frame(1)};
     for (int i = 0; i < 2; ++i) rc[i] = prepare_one(data[i], size[i], info[i], coefs[i], capacity[i], f[i]);
     if (rc[0] == HJD_OK && rc[1] == HJD_OK && single_scan(f[0]) && single_scan(f[1])) {
         const Frame* fp[2] = {&f[0], &f[1]};
@@ -1333,8 +1431,7 @@ size_t scan_end(const uint8_t* d, size_t n, size_t p)
 int hjd_internal::parse_scan_header(const uint8_t* data, size_t size, ScanHeader* h)
 {
     if (!data || !h) return set_error(HJD_E_INVALID, "NULL argument");
-    Frame f;
-    f.decode_tables = false;
+    Frame f(2, false);
     int rc = parse(data, size, f);
     if (rc) return rc;
     if (f.process == 2)
@@ -1348,8 +1445,7 @@ int hjd_internal::parse_scan_headers(const uint8_t* data, size_t size, std::vect
 {
     if (!data || !hs) return set_error(HJD_E_INVALID, "NULL argument");
     hs->clear();
-    Frame f;
-    f.decode_tables = false;
+    Frame f(2, false);
     int rc = parse(data, size, f);
     if (rc) return rc;
     if (f.process == 2)
@@ -1405,8 +1501,7 @@ int hjd_host_cpu_share(void)
 int hjd_jpeg_parse(const uint8_t* data, size_t size, hjd_jpeg_info* info)
 {
     if (!data || !info) return set_error(HJD_E_INVALID, "NULL argument");
-    Frame f;
-    f.decode_tables = false;
+    Frame f(2, false);
     int rc = parse(data, size, f);
     if (rc) return rc;
     fill_info(f, info);

@@ -11,8 +11,9 @@
 // Slot reuse is ordered by events: the host waits for job j-nslots' upload
 // before refilling pinned slot s, and the upload of job j waits (on the GPU)
 // for job j-nslots' kernel before overwriting device slot s.
-// Every upload and kernel is bracketed by timing events, harvested when the
-// slot is reused (or at sync): hjd_stream_busy reports how long the copy
+// Every upload and kernel is bracketed by timing events (2 * nslots sets,
+// harvested by the job 2 * nslots later, whose kernel wait is long over, or
+// at sync; the ordering events carry no timing): hjd_stream_busy reports how long the copy
 // engine and the kernels were busy, i.e. how much of the wall time the
 // pipeline kept the GPU side fed (bench.py config5_stream_host).
 #include <hip/hip_runtime.h>
@@ -63,9 +64,12 @@ struct hjd_stream {
     int nslots = 0;
     std::vector<uint8_t*> host;      // pinned staging
     std::vector<uint8_t*> dev;       // device slots
-    std::vector<hipEvent_t> h2d_done, kernel_done;
-    std::vector<hipEvent_t> h2d_start, kernel_start;   // timing brackets of the slot's last job
-    std::vector<char> timed_pending;    // the slot's last job has unharvested timing events
+    std::vector<hipEvent_t> h2d_done, kernel_done;     // per slot, ordering only (no timing)
+    // Timing brackets of job j in set j % (2 * nslots): harvested when job
+    // j + 2 * nslots is issued, whose acquire() already waited for job j's
+    // kernel (job j + nslots's copy waits on it), so harvesting never blocks.
+    std::vector<hipEvent_t> t_h2d0, t_h2d1, t_k0, t_k1;
+    std::vector<char> timed_pending;    // the set holds a job's unharvested timing events
     std::vector<int64_t> slot_issued;   // last job index whose GPU work was issued on the slot
     hipStream_t copy = nullptr, compute = nullptr;
 
@@ -94,19 +98,19 @@ struct hjd_stream {
     int acquire(const Job& job);
     int issue(const Job& job, int rc, const hjd_jpeg_info& info);
     void worker();
-    void harvest(int s);
+    void harvest(int t);
 };
 
-// Add slot s's last job's copy and kernel durations to the busy totals.  The
-// caller owns the slot (its next job, or sync with every job finished).
-void hjd_stream::harvest(int s)
+// Add timing set t's job's copy and kernel durations to the busy totals.  The
+// caller owns the set (the job 2 * nslots later, or sync with every job
+// finished); the kernel it times has finished by then.
+void hjd_stream::harvest(int t)
 {
-    if (!timed_pending[s]) return;
-    timed_pending[s] = 0;
+    if (!timed_pending[t]) return;
+    timed_pending[t] = 0;
     float copy_ms = 0, kernel_ms = 0;
-    if (hipEventSynchronize(kernel_done[s]) != hipSuccess ||
-        hipEventElapsedTime(&copy_ms, h2d_start[s], h2d_done[s]) != hipSuccess ||
-        hipEventElapsedTime(&kernel_ms, kernel_start[s], kernel_done[s]) != hipSuccess) {
+    if (hipEventSynchronize(t_k1[t]) != hipSuccess || hipEventElapsedTime(&copy_ms, t_h2d0[t], t_h2d1[t]) != hipSuccess ||
+        hipEventElapsedTime(&kernel_ms, t_k0[t], t_k1[t]) != hipSuccess) {
         (void)hipGetLastError();
         return;
     }
@@ -148,17 +152,19 @@ int hjd_stream::issue(const Job& job, int rc, const hjd_jpeg_info& info)
             for (int k = 0; k < 64; ++k) qn[c * 64 + kZigzag[k]] = info.qt[c][k];
     }
 
-    harvest(s);   // the slot's previous job (issued nslots jobs ago)
+    const int t = static_cast<int>(job.index % (2 * nslots));
+    harvest(t);   // the job issued 2 * nslots ago (finished: see t_h2d0)
     // Issue the GPU work (also on failure, with nothing to do, so the slot's
     // event chain stays intact for the next job).
     const bool work = rc == HJD_OK && tasks > 0;
     hipError_t e = hipStreamWaitEvent(copy, kernel_done[s], 0);
-    if (e == hipSuccess && work) e = hipEventRecord(h2d_start[s], copy);
+    if (e == hipSuccess && work) e = hipEventRecord(t_h2d0[t], copy);
     if (e == hipSuccess && rc == HJD_OK)
         e = hipMemcpyAsync(dev[s], h, kHeader + coef_bytes, hipMemcpyHostToDevice, copy);
+    if (e == hipSuccess && work) e = hipEventRecord(t_h2d1[t], copy);
     if (e == hipSuccess) e = hipEventRecord(h2d_done[s], copy);
     if (e == hipSuccess) e = hipStreamWaitEvent(compute, h2d_done[s], 0);
-    if (e == hipSuccess && work) e = hipEventRecord(kernel_start[s], compute);
+    if (e == hipSuccess && work) e = hipEventRecord(t_k0[t], compute);
     int lrc = HJD_OK;
     if (e == hipSuccess && work) {
         lrc = hjd_internal::launch_decode(device, num_cu, info.sampling, HJD_IN_Q16_ZIGZAG, 0, dev[s] + kHeader,
@@ -167,8 +173,9 @@ int hjd_stream::issue(const Job& job, int rc, const hjd_jpeg_info& info)
                                           compute, 0, job.out_format);
         launches++;
     }
+    if (e == hipSuccess && work) e = hipEventRecord(t_k1[t], compute);
     if (e == hipSuccess) e = hipEventRecord(kernel_done[s], compute);
-    timed_pending[s] = e == hipSuccess && work && lrc == HJD_OK;
+    timed_pending[t] = e == hipSuccess && work && lrc == HJD_OK;
     {   // always marked issued, so the slot's next job never waits on a failed one
         std::lock_guard<std::mutex> g(mu);
         slot_issued[s] = job.index;
@@ -266,9 +273,8 @@ int hjd_stream_create(hjd_ctx* ctx, int64_t max_blocks, int nslots, int nthreads
     st->dev.assign(nslots, nullptr);
     st->h2d_done.assign(nslots, nullptr);
     st->kernel_done.assign(nslots, nullptr);
-    st->h2d_start.assign(nslots, nullptr);
-    st->kernel_start.assign(nslots, nullptr);
-    st->timed_pending.assign(nslots, 0);
+    for (auto* v : {&st->t_h2d0, &st->t_h2d1, &st->t_k0, &st->t_k1}) v->assign(2 * nslots, nullptr);
+    st->timed_pending.assign(2 * nslots, 0);
     st->slot_issued.assign(nslots, 0);
     for (int s = 0; s < nslots; ++s) {
         st->slot_issued[s] = s - nslots;
@@ -277,11 +283,13 @@ int hjd_stream_create(hjd_ctx* ctx, int64_t max_blocks, int nslots, int nthreads
             return bail("hipHostMalloc", e);
         if ((e = hipMalloc(reinterpret_cast<void**>(&st->dev[s]), st->slot_bytes)) != hipSuccess)
             return bail("hipMalloc", e);
-        if ((e = hipEventCreate(&st->h2d_done[s])) != hipSuccess) return bail("event", e);
-        if ((e = hipEventCreate(&st->kernel_done[s])) != hipSuccess) return bail("event", e);
-        if ((e = hipEventCreate(&st->h2d_start[s])) != hipSuccess) return bail("event", e);
-        if ((e = hipEventCreate(&st->kernel_start[s])) != hipSuccess) return bail("event", e);
+        if ((e = hipEventCreateWithFlags(&st->h2d_done[s], hipEventDisableTiming)) != hipSuccess) return bail("event", e);
+        if ((e = hipEventCreateWithFlags(&st->kernel_done[s], hipEventDisableTiming)) != hipSuccess)
+            return bail("event", e);
     }
+    for (int t = 0; t < 2 * nslots; ++t)
+        for (auto* v : {&st->t_h2d0, &st->t_h2d1, &st->t_k0, &st->t_k1})
+            if ((e = hipEventCreate(&(*v)[t])) != hipSuccess) return bail("event", e);
     // NUMA-local workers; HJD_NUMA=0 disables
     const char* numa_env = getenv("HJD_NUMA");
     const hjd_internal::CpuSet local = (numa_env && numa_env[0] == '0') ? hjd_internal::CpuSet{}
@@ -313,9 +321,10 @@ int hjd_stream_destroy(hjd_stream* st)
         if (st->dev[s]) (void)hipFree(st->dev[s]);
         if (st->h2d_done[s]) (void)hipEventDestroy(st->h2d_done[s]);
         if (st->kernel_done[s]) (void)hipEventDestroy(st->kernel_done[s]);
-        if (st->h2d_start[s]) (void)hipEventDestroy(st->h2d_start[s]);
-        if (st->kernel_start[s]) (void)hipEventDestroy(st->kernel_start[s]);
     }
+    for (auto* v : {&st->t_h2d0, &st->t_h2d1, &st->t_k0, &st->t_k1})
+        for (hipEvent_t ev : *v)
+            if (ev) (void)hipEventDestroy(ev);
     if (st->copy) (void)hipStreamDestroy(st->copy);
     if (st->compute) (void)hipStreamDestroy(st->compute);
     delete st;
@@ -355,7 +364,7 @@ int hjd_stream_sync(hjd_stream* st, int64_t stats[5])
     if (e == hipSuccess) e = hipStreamSynchronize(st->compute);
     if (e == hipSuccess) e = hipStreamSynchronize(st->copy);
     if (e == hipSuccess)
-        for (int s = 0; s < st->nslots; ++s) st->harvest(s);   // every job is finished
+        for (int t = 0; t < 2 * st->nslots; ++t) st->harvest(t);   // every job is finished
     if (stats) {
         stats[0] = st->images;
         stats[1] = st->pixels;

@@ -248,6 +248,11 @@ def test_autotune_keeps_pixels(hjd, ctx, s):
     assert shape["autotune_launches"] == 0 and shape["autotune_cached"] == 1, shape
     assert shape["tasks_per_wave"] == plan.launch_shape()["tasks_per_wave"]
     assert shape["grid"] == plan.launch_shape()["grid"]
+    # another batch geometry (half the frames) is another key: it tunes afresh
+    half = hjd.Plan(ctx, specs[: nf // 2], hjd.IN_Q16_ZIGZAG, qtables=qt)
+    if half.tasks > 1024:
+        half.autotune(d_coefs, out)
+        assert half.launch_shape()["autotune_cached"] == 0 and half.launch_shape()["autotune_launches"] > 0
     out.zero_()
     again.launch(d_coefs, out)
     torch.cuda.synchronize()

@@ -78,6 +78,48 @@ def test_stream_reports_bad_file_and_continues(hjd, ctx):
     st.close()
 
 
+def test_stream_truncated_scan_reported(hjd, ctx):
+    """A file whose scan is cut short (the reference's "data incomplete",
+    src/decoder.cpp:310-313) fails in the host-Huffman stream with that error;
+    its output stays untouched, the files around it decode exactly, and so do
+    later submits.  Cuts: half the scan with an EOI appended, and 90 % without
+    one, of a 4:2:0, a 4:4:4 and a restart-interval file."""
+    import torch
+    names = ["JPEG_example_JPG_RIP_050", "syn444_64x40_q90", "syn420_160x48_q95_dri"]
+    goods, bads = [], []
+    for n in names:
+        data = open(os.path.join(O.GOLDEN, n + ".jpg"), "rb").read()
+        so = hjd.parse(data).scan_offset
+        goods.append((data, O.load_case(n)["bgrx"]))
+        bads.append(data[: so + (len(data) - 2 - so) // 2] + b"\xff\xd9")
+        bads.append(data[: so + (len(data) - 2 - so) * 9 // 10])
+    max_blocks = max(hjd.parse(d).nblocks for d, _ in goods)
+    order = []   # good, bad, good, bad, ...
+    for i, b in enumerate(bads):
+        order.append(("good", goods[i % len(goods)]))
+        order.append(("bad", (b, goods[(i // 2) % len(goods)][1].shape)))
+    order.append(("good", goods[0]))
+    outs = []
+    for kind, (d, e) in order:
+        shape = e.shape if kind == "good" else e
+        outs.append(torch.full(shape, 0x5A5A5A5A, dtype=torch.int32, device="cuda"))
+    with hjd.JpegStream(ctx, max_blocks, nslots=3, nthreads=4) as st:
+        for (kind, (d, _)), o in zip(order, outs):
+            st.submit(d, o)
+        with pytest.raises(hjd._lib.HjdError, match="incomplete"):
+            st.sync()
+        for (kind, (d, e)), o in zip(order, outs):
+            got = o.cpu().numpy().view(np.uint32)
+            if kind == "good":
+                np.testing.assert_array_equal(got, e)
+            else:
+                assert (got == 0x5A5A5A5A).all()
+        again = torch.zeros(goods[1][1].shape, dtype=torch.int32, device="cuda")
+        st.submit(goods[1][0], again)
+        st.sync()
+        np.testing.assert_array_equal(again.cpu().numpy().view(np.uint32), goods[1][1])
+
+
 def test_4k_jpeg_end_to_end(hjd, ctx):
     import torch
     data = _pil(3840, 2160, 90, 2, seed=4)
