@@ -521,7 +521,11 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
     from ocljpegdecoder_amd import shard
     w, h, s, nf = wl["width"], wl["height"], wl["sampling"], wl["frames"]
     share = host_cpu_share()[0]
-    nthreads = int(os.environ.get("HJD_STREAM_THREADS", max(1, min(16, share // max(1, world)))))
+    # the GPU's CPU slice (its NUMA node's CPUs split over the node's GPUs),
+    # every logical CPU of it (SMT: profiles/r06a_smt_probe.json), within this
+    # rank's part of the process CPU share
+    slice_cpus = len(hjd.device_worker_cpus(dev.index))
+    nthreads = int(os.environ.get("HJD_STREAM_THREADS", hjd.stream_worker_threads(share, world, slice_cpus)))
     npool = int(os.environ.get("HJD_STREAM_POOL", STREAM_POOL))
     pool = encode_pool(w, h, s, npool, seed0=7919)       # identical on every rank: ids map to the same files
     infos = [hjd.parse(d) for d in pool]
@@ -649,6 +653,12 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
     weights = torch.randint(1, CHECK_PRIME, (nwords,), generator=g, device=dev, dtype=torch.int64)
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_py as O
+    import scale_pins as SP
+    # the pool's host coefficients against the reference's own mcu_data hashes
+    # (tests/scale_pins.py; the manifest pins config 5's 64-file 4K pool)
+    pins = SP.manifest_scale().get("bench_pool_4k420_q90", {}).get("files", []) \
+        if (w, h, s, npool) == (3840, 2160, 1, STREAM_POOL) else []
+    pin_count = {"pinned": 0, "unpinned": 0, "MISMATCH": 0}
     exp_cs = {}
     got = exp = id_sum = nchecked = 0
     for k, o in checks:
@@ -657,6 +667,8 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
             f = ids[i] % npool
             if f not in exp_cs:
                 coefs, info = hjd.decode_coefs(pool[f])
+                pin_count[SP.check_coefs(pins[f], pool[f], coefs, info.qt, info.sampling) if f < len(pins)
+                          else "unpinned"] += 1
                 e = O.decode_q16(coefs, info.qt, info.width, info.height, info.sampling)
                 if ofmt != hjd.OUT_BGRX:
                     e = np.zeros((h, pitch), np.uint8)
@@ -688,6 +700,7 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
                     f"ranks, cycled over a global frame-id list",
             "config": {"workload": wl["desc"], "frames_per_gpu_per_step": nf, "width": w, "height": h,
                        "sampling": SAMPLING_NAMES[s], "host_threads_per_gpu": nthreads,
+                       "host_cpu_share": share, "gpu_cpu_slice": slice_cpus,
                        "entropy_decode": "gpu" if gpu_entropy else "host", "mean_jpeg_bytes": jpeg_bytes,
                        "output": ("pinned host memory (D2H-on)" if d2h else "in HBM (D2H-off)") +
                                  (", BGR24" if ofmt == hjd.OUT_BGR24 else ", BGRX"),
@@ -720,7 +733,11 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
                            "returns frames: 2, 4 and the stream's slot count of concurrent streams, one frame's "
                            "output per copy (plus one stream of 256 MiB copies); the best rate is the ceiling"},
                 "pipeline": busy,
-                "output_checked_vs_oracle": bool(ok)},
+                "output_checked_vs_oracle": bool(ok),
+                "coefs_vs_reference_mcu_data": dict(pin_count, how="sha256 of each checked pool file's host "
+                                                    "coefficients (and their dequantised natural-order form) vs the "
+                                                    "reference's own mcu_data hashes, tests/golden/manifest.json "
+                                                    "scale.bench_pool_4k420_q90 (rank 0's files)")},
             "hbm_at_start": {"wait_s_max_over_ranks": round(released["hbm_wait_s"], 2),
                              "busy_GiB_max_over_ranks": round(released["hbm_busy_GiB"], 2),
                              "how": "hipMemGetInfo polled before the first allocation until at most "
@@ -741,6 +758,9 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
         dist.destroy_process_group()
     if not ok:
         log("FATAL: stream output differs from the oracle")
+        sys.exit(1)
+    if pin_count["MISMATCH"]:
+        log("FATAL: host Huffman coefficients differ from the reference's mcu_data")
         sys.exit(1)
 
 
@@ -1217,7 +1237,13 @@ def _stream_summary(leg, ceiling_key=None):
         r.update({"host_Mpx_s_per_core": p["host_huffman_Mpx_per_core_s"], "cores": p["host_threads"],
                   "h2d_GBps": p["h2d_GBps"], "kernel_busy": p["kernel_busy_frac"], "h2d_busy": p["h2d_busy_frac"],
                   "kernel_only_Mpx_s": p.get("kernel_only_Mpx_s"), "pcie_ceiling_Mpx_s": p.get("pcie_ceiling_Mpx_s")})
+    if leg.get("gpu_cpu_slice") is not None:
+        r["cpu_slice"] = leg["gpu_cpu_slice"]
+        r["cpu_share"] = leg["host_cpu_share"]
     r["ok"] = leg["output_checked_vs_oracle"]
+    pins = leg.get("coefs_vs_reference_mcu_data")
+    if pins:
+        r["ref_pinned"] = f"{pins['pinned']}/{pins['pinned'] + pins['unpinned'] + pins['MISMATCH']}"
     return r
 
 
@@ -1541,8 +1567,10 @@ def config5_stream_leg(world, dist_backend, frame_ids=100000, workload="stream4k
             "d2h_ceiling": d["end_to_end"].get("d2h_ceiling"),
             "pipeline": d["end_to_end"].get("pipeline"),
             "host_threads_per_gpu": d["config"]["host_threads_per_gpu"],
+            "host_cpu_share": d["config"].get("host_cpu_share"), "gpu_cpu_slice": d["config"].get("gpu_cpu_slice"),
             "output": d["config"]["output"],
             "output_checked_vs_oracle": d["end_to_end"]["output_checked_vs_oracle"],
+            "coefs_vs_reference_mcu_data": d["end_to_end"].get("coefs_vs_reference_mcu_data"),
             "steps_checked": d["stream_check"]["steps_checked"],
             "parent_ranks_alive_at_start": siblings_alive, "hbm_at_start": d.get("hbm_at_start"),
             "command": " ".join(["python"] + [os.path.basename(c) if c.endswith("bench.py") else c

@@ -61,11 +61,21 @@ int hjd_jpeg_decode_coefs(const uint8_t* data, size_t size, hjd_jpeg_info* info,
                           int64_t capacity_blocks);
 
 /* The calling process's CPU share: the CPUs in its affinity mask, capped by
- * its cgroup's CPU quota (cgroup v2 cpu.max, rounded up).  A container granted
- * 16 CPUs of time on a 256-CPU host gets 16, not 256.  The default thread count
- * (nthreads = 0) of hjd_jpeg_decode_batch, hjd_stream_create and
- * hjd_gstream_create. */
+ * its cgroup's CPU quota, rounded up (the cgroup of /proc/self/cgroup and its
+ * ancestors; v2 cpu.max or v1 cpu.cfs_quota_us / cpu.cfs_period_us; computed
+ * once per process).  A container granted 16 CPUs of time on a 256-CPU host
+ * gets 16, not 256.  The default thread count (nthreads = 0) of
+ * hjd_jpeg_decode_batch; hjd_stream_create and hjd_gstream_create cap it by
+ * the device's CPU slice (hjd_device_worker_cpus). */
 int hjd_host_cpu_share(void);
+/* hjd_host_cpu_share computed from the tree at `root` ("/proc/self/cgroup",
+ * "/sys/fs/cgroup/..." under it; NULL = the real one, not cached): tests. */
+int hjd_debug_cpu_share(const char* root);
+/* The host CPUs the stream workers of HIP device `device` bind to: its NUMA
+ * node's CPUs this process may use, split evenly among the node's visible
+ * GPUs (hjd_debug_worker_cpus on the real topology).  Writes up to `capacity`
+ * ids; *ncpus = how many (0: unknown topology, no binding). */
+int hjd_device_worker_cpus(int device, int32_t* cpus, int capacity, int32_t* ncpus);
 
 /* Decode n files on `nthreads` host threads (0 = hjd_host_cpu_share());
  * status[i] receives each file's return code.  Returns HJD_OK if all
@@ -77,7 +87,8 @@ int hjd_jpeg_decode_batch(const uint8_t* const* datas, const size_t* sizes, int 
 typedef struct hjd_stream hjd_stream;
 
 /* nslots pinned staging slots of max_blocks coefficient blocks each (>= 2;
- * 3 = triple buffering); nthreads host Huffman workers (0 = hjd_host_cpu_share()). */
+ * 3 = triple buffering); nthreads host Huffman workers (0 = hjd_host_cpu_share()
+ * capped by the device's CPU slice, hjd_device_worker_cpus). */
 int hjd_stream_create(hjd_ctx* ctx, int64_t max_blocks, int nslots, int nthreads, hjd_stream** out);
 int hjd_stream_destroy(hjd_stream* s);
 

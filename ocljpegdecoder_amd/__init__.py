@@ -29,13 +29,16 @@ from .backend import (  # noqa: E402
     autotune_cache_clear,
     block_components,
     Context,
+    cpu_share,
     FrameSpec,
     Plan,
     decode_frame,
     default_pitch,
     device_count,
+    device_worker_cpus,
     frame_blocks,
     mcu_geometry,
+    stream_worker_threads,
     worker_cpus,
 )
 
@@ -47,6 +50,7 @@ __all__ = [
     "GpuDecoder", "GpuJpegStream", "JpegInfo", "JpegStream", "bmp_bytes", "bmp_header", "decode_coefs",
     "decode_coefs_batch", "decode_coefs_into", "decode_jpeg", "emulate_entropy",
     "parse", "pinned_bytes",
-    "Context", "FrameSpec", "Plan", "autotune_cache_clear", "decode_frame", "device_count", "frame_blocks", "mcu_geometry", "worker_cpus",
+    "Context", "FrameSpec", "Plan", "autotune_cache_clear", "decode_frame", "device_count", "frame_blocks", "mcu_geometry", "worker_cpus", "cpu_share",
+    "device_worker_cpus", "stream_worker_threads",
     "YUV444", "YUV420", "YUV422", "GRAY", "YUV411_H4V1", "YUV440", "OTHER", "block_components", "KERNEL_AUTO", "KERNEL_PERSISTENT", "KERNEL_LATENCY", "OUT_BGRX", "OUT_BGR24", "OUT_BYTES", "default_pitch", "IN_Q16_ZIGZAG", "IN_I32_NATURAL",
 ]

@@ -183,6 +183,8 @@ def _bind_host(lib):
                                                ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]),
         "hjd_debug_host_reader": (ctypes.c_int, [ctypes.c_int]),
         "hjd_host_cpu_share": (ctypes.c_int, []),
+        "hjd_debug_cpu_share": (ctypes.c_int, [ctypes.c_char_p]),
+        "hjd_device_worker_cpus": (ctypes.c_int, [ctypes.c_int, c_i32p, ctypes.c_int, c_i32p]),
         "hjd_debug_destuff_host": (ctypes.c_int, [u8p, ctypes.c_size_t, u8p, ctypes.c_size_t,
                                                   ctypes.POINTER(ctypes.c_uint32), ctypes.c_int,
                                                   ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int64)]),

@@ -296,6 +296,35 @@ def worker_cpus(bus: str, gpus: Sequence[str], sysfs_root: Optional[str] = None,
     return list(out[:min(n.value, cap)])
 
 
+def device_worker_cpus(device: int):
+    """hjd_device_worker_cpus: the host CPUs the stream workers of HIP device
+    `device` bind to (its share of its NUMA node; [] = unknown topology)."""
+    lib = _lib.load()
+    if getattr(lib, "hjd_device_worker_cpus", None) is None:   # an older HJD_LIB tuning build
+        return []
+    cap = 4096
+    out = (ctypes.c_int32 * cap)()
+    n = ctypes.c_int32(0)
+    check(lib.hjd_device_worker_cpus(int(device), out, cap, ctypes.byref(n)), "hjd_device_worker_cpus")
+    return list(out[:min(n.value, cap)])
+
+
+def cpu_share(root: Optional[str] = None) -> int:
+    """hjd_host_cpu_share (root None) or hjd_debug_cpu_share on a fake tree:
+    affinity CPUs capped by the cgroup's CPU quota."""
+    lib = _lib.load()
+    return lib.hjd_host_cpu_share() if root is None else lib.hjd_debug_cpu_share(root.encode())
+
+
+def stream_worker_threads(share: int, world: int, slice_cpus: int) -> int:
+    """Host worker threads per GPU of a multi-rank stream job (bench.py config
+    5): the process's CPU share split over the ranks on the host, capped by the
+    GPU's CPU slice when the topology is known (every logical CPU of the slice:
+    SMT pays for the Huffman decode, profiles/r06a_smt_probe.json)."""
+    per_rank = max(1, share // max(1, world))
+    return min(per_rank, slice_cpus) if slice_cpus > 0 else per_rank
+
+
 def autotune_cache_clear():
     """Forget every cached hjd_plan_autotune choice of this process."""
     check(_lib.load().hjd_autotune_cache_clear(), "hjd_autotune_cache_clear")

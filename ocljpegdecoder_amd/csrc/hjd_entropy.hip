@@ -3288,7 +3288,7 @@ int hjd_gstream_create(hjd_ctx* ctx, int max_frames, int64_t max_scan_bytes, int
 {
     if (!ctx || !out || nslots < 2 || nslots > 16) return set_error(HJD_E_INVALID, "invalid gstream arguments (nslots 2..16)");
     *out = nullptr;
-    if (nthreads <= 0) nthreads = hjd_host_cpu_share();
+    if (nthreads <= 0) nthreads = hjd_internal::default_worker_threads(hjd_ctx_device(ctx));
     hjd_gstream* st = new (std::nothrow) hjd_gstream;
     if (!st) return set_error(HJD_E_NOMEM, "gstream allocation");
     st->ctx = ctx;

@@ -125,6 +125,10 @@ struct CpuSet {
     std::vector<int> cpus;
 };
 CpuSet device_local_cpus(int device);
+// Default host worker count of a stream on `device` (nthreads = 0): the
+// process's CPU share (hjd_host_cpu_share) capped by the device's CPU slice
+// (device_local_cpus; uncapped when the topology is unknown).
+int default_worker_threads(int device);
 CpuSet node_cpus(int node);   // CPUs of NUMA node `node` this process may use (empty: unknown)
 std::vector<int> bind_current_thread(const CpuSet& s);
 void restore_current_thread(const std::vector<int>& prev);

@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -67,9 +68,9 @@ struct TableSet {
 
 TableSet& table_set(int i)
 {
-    thread_local std::unique_ptr<TableSet> sets[3];
-    if (!sets[i]) sets[i].reset(new TableSet);
-    return *sets[i];
+    thread_local std::unique_ptr<TableSet[]> sets;
+    if (!sets) sets.reset(new TableSet[3]);
+    return sets[i];
 }
 
 struct Component {
@@ -647,12 +648,23 @@ int decode_scan_bytewise(const uint8_t* d, size_t n, const Frame& f, const hjd_j
 // 16 bits are left) and a byte loop at every 0xFF.  The hot path instead
 // copies the scan's entropy-coded data once without its byte stuffing
 // (copy_until_ff, a few % of the decode) into per-thread scratch, one segment
-// per restart interval, each followed by 8 zero bytes, and then reads it with
-// a branch-free refill: a 64-bit load at the byte cursor, shifted under the
-// bits still buffered (the cursor moves by the whole bytes taken and stops at
-// the segment's end, so the reader sees zeros past it, as BitReader does past
-// a marker).  A refill leaves at least 56 bits, which is what lets FastDec run
-// three symbol steps per refill (the bit budget is at FastDec::step).
+// per restart interval, each followed by kSegPad zero bytes, and then reads it
+// with a branch-free refill: a 64-bit load at the byte cursor, shifted under
+// the bits still buffered (the cursor moves by the whole bytes taken, so the
+// reader sees zeros past the data, as BitReader does past a marker, and
+// stops kSegPad - 8 bytes past it).  A refill leaves at least 56 bits, which
+// is what lets FastDec run three symbol steps per refill (the bit budget is at
+// FastDec::step).
+//
+// Reading past the data: while the cursor has not hit its stop, the bits taken
+// are exact (8 x bytes moved - bits buffered), and a cursor that moved more
+// than 8 bytes past the data means more bits were taken than buffered there;
+// so FastReader::left() < 0 exactly when the decode consumed bits past the
+// segment's data, the stop included (16 bytes past: left() <= 63 - 128).  The
+// check runs where an interval ends (the restart) and after the last MCU
+// (FastDec::report), none on the step path: a decode that runs out of data
+// goes on over zeros to the segment's end, is then rejected, and the
+// byte-wise reader re-runs it for the exact MCU of the error.
 //
 // The bits a decode sees are the BitReader's exactly: de-stuffed FF00, fill
 // bytes in front of a marker dropped, zeros after the marker or the end of
@@ -662,8 +674,10 @@ int decode_scan_bytewise(const uint8_t* d, size_t n, const Frame& f, const hjd_j
 // byte, its restart search stops at the FF FF): destuff_scan declines such a
 // scan and it takes the byte-wise path.  tests/test_jpeg_host_pair.py and the
 // fuzz harness (tools/fuzz/host_decode_fuzz.cpp) compare the two readers.
+constexpr size_t kSegPad = 24;   // zero bytes after each segment: the cursor stops 16 past the data
+
 struct CleanSeg {
-    size_t begin, end;   // bytes of CleanScan::buf; 8 zero bytes follow `end`
+    size_t begin, end;   // bytes of CleanScan::buf; kSegPad zero bytes follow `end`
     int marker;          // the marker byte that ended the segment; -1: the data ended
 };
 
@@ -681,7 +695,7 @@ bool destuff_scan(const uint8_t* s, const uint8_t* end, int64_t max_segs, CleanS
     const size_t n = static_cast<size_t>(end - s);
     max_segs = std::max<int64_t>(1, std::min<int64_t>(max_segs, static_cast<int64_t>(n / 2) + 1));
     // + 64: copy_until_ff stores whole 64-byte vectors while that many fit
-    const size_t need = n + 8 * static_cast<size_t>(max_segs) + 8 + 64;
+    const size_t need = n + kSegPad * static_cast<size_t>(max_segs) + kSegPad + 64;
     if (cs.cap < need) {
         cs.buf.reset(new uint8_t[need]);
         cs.cap = need;
@@ -708,8 +722,8 @@ bool destuff_scan(const uint8_t* s, const uint8_t* end, int64_t max_segs, CleanS
             s = g < end ? g + 1 : end;
         }
         const size_t seg_end = static_cast<size_t>(o - o0);
-        memset(o, 0, 8);
-        o += 8;
+        memset(o, 0, kSegPad);
+        o += kSegPad;
         cs.segs.push_back({begin, seg_end, marker});
         begin = static_cast<size_t>(o - o0);
         if (marker < 0xD0 || marker > 0xD7 || static_cast<int64_t>(cs.segs.size()) == max_segs) return true;
@@ -718,20 +732,29 @@ bool destuff_scan(const uint8_t* s, const uint8_t* end, int64_t max_segs, CleanS
 
 struct FastReader {
     const uint8_t* p;
-    const uint8_t* lim;   // the segment's end (8 zero bytes follow)
-    uint64_t acc = 0;     // MSB-first; bits below the top nbits are zeros or the stream's next bits
+    const uint8_t* stop;   // the cursor's limit: the segment's end + kSegPad - 8
+    uint64_t acc = 0;      // MSB-first; bits below the top nbits are zeros or the stream's next bits
     int nbits = 0;
 
+    void seek(const CleanScan& cs, const CleanSeg& s)
+    {
+        p = cs.buf.get() + s.begin;
+        stop = cs.buf.get() + s.end + (kSegPad - 8);
+        acc = 0;
+        nbits = 0;
+    }
     __attribute__((always_inline)) void refill()
     {
         uint64_t v;
-        memcpy(&v, p < lim ? p : lim, 8);   // at or past the end: the 8 zero bytes after it
+        memcpy(&v, p, 8);
         acc |= __builtin_bswap64(v) >> nbits;
-        p += (63 - nbits) >> 3;             // not clamped: p - lim counts the zero bytes taken
+        p += (63 - nbits) >> 3;
+        p = p < stop ? p : stop;
         nbits |= 56;
     }
-    // bits of the segment not taken yet; < 0: the decode read past its data
-    int64_t left() const { return 8 * (lim - p) + nbits; }
+    // bits of the segment's data not taken yet; < 0: the decode took bits
+    // past its data (exact in sign, see above)
+    int64_t left() const { return 8 * (stop - static_cast<std::ptrdiff_t>(kSegPad - 8) - p) + nbits; }
     uint32_t peek(int n) const { return static_cast<uint32_t>(acc >> (64 - n)); }
     void skip(int n)
     {
@@ -809,8 +832,7 @@ struct FastDec {
     {
         cs = &c;
         o = &ord;
-        br.p = c.buf.get() + c.segs[0].begin;
-        br.lim = c.buf.get() + c.segs[0].end;
+        br.seek(c, c.segs[0]);
         const int nblk0 = f.ncomp == 1 ? 1 : f.comp[0].h * f.comp[0].v;   // as decode_scan_bytewise
         bpm = f.ncomp == 1 ? 1 : nblk0 + 2;
         int j = 0;
@@ -831,7 +853,12 @@ struct FastDec {
         done = nmcu == 0;
         if (!done) begin_mcu();
     }
-    __attribute__((always_inline)) int report() const { return report_error(err, m, nmcu, restarts); }
+    // After the decode: the last segment's end check (the data ran out before
+    // the last MCU's end) is made here, off the step path.
+    __attribute__((always_inline)) int report() const
+    {
+        return report_error(err == 0 && br.left() < 0 ? 3 : err, m, nmcu, restarts);
+    }
     __attribute__((always_inline)) void fail(int e)
     {
         err = e;
@@ -862,18 +889,14 @@ struct FastDec {
     }
     __attribute__((always_inline)) void begin_mcu()   // src/decoder.cpp:288-314
     {
-        // the previous MCU read past the segment's data (BitReader::overrun)
-        if (br.left() < 0) return fail(3);
         if (ri > 0 && since == ri) {
-            // the reference reads the byte after the interval's last bits as the
-            // marker (src/decoder.cpp:295-302): a whole byte left is a mismatch
+            // the interval's data ran out (BitReader::overrun); the reference
+            // reads the byte after the interval's last bits as the marker
+            // (src/decoder.cpp:295-302), so a whole byte left is a mismatch
             const CleanSeg& s = cs->segs[seg];
+            if (br.left() < 0) return fail(3);
             if (s.marker != 0xD0 + (restarts & 7) || seg + 1 >= cs->segs.size() || br.left() >= 8) return fail(2);
-            ++seg;
-            br.p = cs->buf.get() + cs->segs[seg].begin;
-            br.lim = cs->buf.get() + cs->segs[seg].end;
-            br.acc = 0;
-            br.nbits = 0;
+            br.seek(*cs, cs->segs[++seg]);
             ++restarts;
             since = 0;
             o->pred[0] = o->pred[1] = o->pred[2] = 0;
@@ -886,8 +909,7 @@ struct FastDec {
     {
         if (++bi < bpm) return begin_block();
         if (++m == nmcu) {
-            if (br.left() < 0) return fail(3);
-            done = true;
+            done = true;   // report() checks the last segment's end
             return;
         }
         begin_mcu();
@@ -998,11 +1020,27 @@ int decode_clean(const CleanScan& cs, const Frame& f, const hjd_jpeg_info& info,
     return a.report();
 }
 
+// A file the de-stuffed reader rejected, decoded again by the byte-wise
+// reader, whose checks run per MCU: its error names the MCU where the data
+// ran out (or the first corrupt one), where the de-stuffed reader only
+// notices at the interval's end.  Errors are rare; the re-run costs one decode.
+__attribute__((noinline, cold)) int exact_error(const uint8_t* d, size_t n, const Frame& f,
+                                                 const hjd_jpeg_info& info, int16_t* coefs, int rc)
+{
+    const int rb = decode_scan_bytewise(d, n, f, info, coefs);
+    return rb != HJD_OK ? rb : rc;
+}
+
 int decode_scan(const uint8_t* d, size_t n, const Frame& f, const hjd_jpeg_info& info, int16_t* coefs)
 {
     CleanScan& cs = clean_scratch(0);
-    const int rc = destuff_for(d, n, f, info, cs) ? decode_clean(cs, f, info, coefs)
-                                                  : decode_scan_bytewise(d, n, f, info, coefs);
+    int rc;
+    if (destuff_for(d, n, f, info, cs)) {
+        rc = decode_clean(cs, f, info, coefs);
+        if (rc != HJD_OK) rc = exact_error(d, n, f, info, coefs, rc);
+    } else {
+        rc = decode_scan_bytewise(d, n, f, info, coefs);
+    }
     trim_scratch(cs);
     return rc;
 }
@@ -1021,9 +1059,14 @@ void decode_scan_pair(const uint8_t* const d[2], const size_t n[2], const Frame*
     const bool ok0 = destuff_for(d[0], n[0], *f[0], *info[0], c0);
     const bool ok1 = destuff_for(d[1], n[1], *f[1], *info[1], c1);
     if (!ok0 || !ok1) {
-        for (int i = 0; i < 2; ++i)
-            rc[i] = (i ? ok1 : ok0) ? decode_clean(i ? c1 : c0, *f[i], *info[i], coefs[i])
-                                    : decode_scan_bytewise(d[i], n[i], *f[i], *info[i], coefs[i]);
+        for (int i = 0; i < 2; ++i) {
+            if (i ? ok1 : ok0) {
+                rc[i] = decode_clean(i ? c1 : c0, *f[i], *info[i], coefs[i]);
+                if (rc[i] != HJD_OK) rc[i] = exact_error(d[i], n[i], *f[i], *info[i], coefs[i], rc[i]);
+            } else {
+                rc[i] = decode_scan_bytewise(d[i], n[i], *f[i], *info[i], coefs[i]);
+            }
+        }
         trim_scratch(c0);
         trim_scratch(c1);
         return;
@@ -1054,6 +1097,8 @@ void decode_scan_pair(const uint8_t* const d[2], const size_t n[2], const Frame*
         rc[0] = a.report();
         rc[1] = b.report();
     }
+    for (int i = 0; i < 2; ++i)
+        if (rc[i] != HJD_OK) rc[i] = exact_error(d[i], n[i], *f[i], *info[i], coefs[i], rc[i]);
     trim_scratch(c0);
     trim_scratch(c1);
 }
@@ -1428,6 +1473,89 @@ size_t scan_end(const uint8_t* d, size_t n, size_t p)
 
 }  // namespace
 
+namespace {
+
+std::string read_small_file(const std::string& path)
+{
+    FILE* f = fopen(path.c_str(), "r");
+    if (!f) return {};
+    char buf[4096];
+    const size_t n = fread(buf, 1, sizeof(buf) - 1, f);
+    fclose(f);
+    buf[n] = 0;
+    return buf;
+}
+
+// CPU quota of this process's cgroup, in CPUs rounded up (0: none).  The
+// cgroup comes from /proc/self/cgroup: cgroup v2 ("0::<path>", cpu.max =
+// "<quota> <period>" or "max ...") or v1 (a "cpu" controller line,
+// cpu.cfs_quota_us / cpu.cfs_period_us, quota -1 = none), and every ancestor
+// up to the mount root counts (a limit anywhere above applies too): the
+// smallest quota wins.  `root` is "" for the real filesystem (tests pass a
+// fake tree).
+int cgroup_quota_cpus(const std::string& root)
+{
+    const std::string self = read_small_file(root + "/proc/self/cgroup");
+    int best = 0;
+    auto consider = [&](long long quota, long long period) {
+        if (quota <= 0 || period <= 0) return;
+        const int n = static_cast<int>((quota + period - 1) / period);
+        if (n > 0 && (best == 0 || n < best)) best = n;
+    };
+    // walk a cgroup path and its ancestors under `mount`
+    auto walk = [&](const std::string& mount, std::string path, bool v2) {
+        for (;;) {
+            const std::string dir = root + mount + (path == "/" ? "" : path);
+            if (v2) {
+                const std::string m = read_small_file(dir + "/cpu.max");
+                char q[32] = {0};
+                long long per = 0;
+                if (!m.empty() && sscanf(m.c_str(), "%31s %lld", q, &per) == 2 && strcmp(q, "max") != 0)
+                    consider(atoll(q), per);
+            } else {
+                const std::string q = read_small_file(dir + "/cpu.cfs_quota_us"), per = read_small_file(dir + "/cpu.cfs_period_us");
+                if (!q.empty() && !per.empty()) consider(atoll(q.c_str()), atoll(per.c_str()));
+            }
+            if (path.empty() || path == "/") break;
+            const size_t k = path.find_last_of('/');
+            path = k == 0 || k == std::string::npos ? "/" : path.substr(0, k);
+        }
+    };
+    size_t i = 0;
+    while (i < self.size()) {
+        size_t e = self.find('\n', i);
+        if (e == std::string::npos) e = self.size();
+        const std::string line = self.substr(i, e - i);
+        i = e + 1;
+        const size_t c1 = line.find(':'), c2 = c1 == std::string::npos ? c1 : line.find(':', c1 + 1);
+        if (c2 == std::string::npos) continue;
+        const std::string ctrl = line.substr(c1 + 1, c2 - c1 - 1), path = line.substr(c2 + 1);
+        if (ctrl.empty()) {   // v2 unified hierarchy
+            walk("/sys/fs/cgroup", path, true);
+        } else if (("," + ctrl + ",").find(",cpu,") != std::string::npos) {   // v1 cpu controller
+            walk("/sys/fs/cgroup/" + ctrl, path, false);
+            walk("/sys/fs/cgroup/cpu", path, false);
+        }
+    }
+    if (best == 0) {   // no /proc/self/cgroup (or nothing under it): the v2 and v1 mount roots
+        walk("/sys/fs/cgroup", "/", true);
+        walk("/sys/fs/cgroup/cpu", "/", false);
+    }
+    return best;
+}
+
+int cpu_share(const std::string& root)
+{
+    int n = 0;
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof(set), &set) == 0) n = CPU_COUNT(&set);
+    if (n <= 0) n = 1;
+    const int q = cgroup_quota_cpus(root);
+    return std::max(1, q > 0 ? std::min(n, q) : n);
+}
+
+}  // namespace
+
 int hjd_internal::parse_scan_header(const uint8_t* data, size_t size, ScanHeader* h)
 {
     if (!data || !h) return set_error(HJD_E_INVALID, "NULL argument");
@@ -1482,21 +1610,11 @@ extern "C" {
 
 int hjd_host_cpu_share(void)
 {
-    int n = 0;
-    cpu_set_t set;
-    if (sched_getaffinity(0, sizeof(set), &set) == 0) n = CPU_COUNT(&set);
-    if (n <= 0) n = static_cast<int>(std::max(1u, std::thread::hardware_concurrency()));
-    if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {   // "max 100000" or "<quota> <period>"
-        char q[32] = {0};
-        long long period = 0;
-        if (fscanf(f, "%31s %lld", q, &period) == 2 && strcmp(q, "max") != 0 && period > 0) {
-            const long long quota = atoll(q);
-            if (quota > 0) n = std::min<long long>(n, (quota + period - 1) / period);
-        }
-        fclose(f);
-    }
-    return std::max(1, n);
+    static const int share = cpu_share("");   // once per process
+    return share;
 }
+
+int hjd_debug_cpu_share(const char* root) { return cpu_share(root ? root : ""); }
 
 int hjd_jpeg_parse(const uint8_t* data, size_t size, hjd_jpeg_info* info)
 {

@@ -140,6 +140,22 @@ hjd_internal::CpuSet hjd_internal::device_local_cpus(int device)
     return s;
 }
 
+extern "C" int hjd_device_worker_cpus(int device, int32_t* cpus, int capacity, int32_t* ncpus)
+{
+    if (capacity < 0 || (!cpus && capacity > 0) || !ncpus) return hjd_internal::set_error(HJD_E_INVALID, "invalid arguments");
+    const hjd_internal::CpuSet s = hjd_internal::device_local_cpus(device);
+    *ncpus = static_cast<int32_t>(s.cpus.size());
+    for (int i = 0; i < static_cast<int>(s.cpus.size()) && i < capacity; ++i) cpus[i] = s.cpus[i];
+    return 0;
+}
+
+int hjd_internal::default_worker_threads(int device)
+{
+    const int share = hjd_host_cpu_share();
+    const int slice = static_cast<int>(device_local_cpus(device).cpus.size());
+    return slice > 0 ? std::min(share, slice) : share;
+}
+
 extern "C" int hjd_debug_worker_cpus(const char* sysfs_root, const char* bus, const char* const* gpus, int ngpus,
                                      int only_allowed, int32_t* cpus, int capacity, int32_t* ncpus)
 {

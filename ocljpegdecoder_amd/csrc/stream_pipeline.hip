@@ -252,7 +252,7 @@ int hjd_stream_create(hjd_ctx* ctx, int64_t max_blocks, int nslots, int nthreads
 {
     if (!ctx || !out || max_blocks <= 0 || nslots < 2) return set_error(HJD_E_INVALID, "invalid stream arguments");
     *out = nullptr;
-    if (nthreads <= 0) nthreads = hjd_host_cpu_share();
+    if (nthreads <= 0) nthreads = hjd_internal::default_worker_threads(hjd_ctx_device(ctx));
     hjd_stream* st = new (std::nothrow) hjd_stream;
     if (!st) return set_error(HJD_E_NOMEM, "stream allocation");
     st->ctx = ctx;

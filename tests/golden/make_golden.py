@@ -106,6 +106,30 @@ class Ref:
             shutil.rmtree(tmp, ignore_errors=True)
         return cap_in, cap_out, bmp
 
+    def try_decode(self, jpg_path):
+        """Decode in a forked child (the reference may abort on a file it
+        rejects); returns (accepted, its stdout log).  load_jpg returns true
+        whatever happened (src/parser.cpp:416-418): accepted = it wrote its BMP."""
+        tmp = tempfile.mkdtemp(prefix="hjd_ref_")
+        try:
+            log = os.path.join(tmp, "log.txt")
+            pid = os.fork()
+            if pid == 0:
+                try:
+                    os.chdir(tmp)
+                    fd = os.open(log, os.O_WRONLY | os.O_CREAT)
+                    os.dup2(fd, 1)
+                    self.lib.ref_load_jpg(os.path.abspath(jpg_path).encode(), None, None)
+                    libc = ctypes.CDLL(None)
+                    libc.fflush(None)
+                finally:
+                    os._exit(0)
+            _, st = os.waitpid(pid, 0)
+            ok = st == 0 and os.path.exists(os.path.join(tmp, "m:\\output.bmp"))
+            return ok, open(log, errors="replace").read()
+        finally:
+            shutil.rmtree(tmp, ignore_errors=True)
+
     def fast_idct(self, blocks):
         b = np.ascontiguousarray(blocks, dtype=np.int32).copy()
         self.lib.ref_fast_idct_n(b.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), b.shape[0])
@@ -235,7 +259,83 @@ def csc_exhaustive(ref: Ref):
             "csc_order": "index = ((Y+256)<<18) | ((U+256)<<9) | (V+256), uint32 little-endian"}
 
 
+def q16_of_mcu_data(cap_in, jpg_bytes):
+    """The reference's mcu_data (int32 natural, dequantised) as int16 zigzag
+    quantised coefficients (exact: src/decoder.cpp:340 multiplied them)."""
+    (w, h), comps, qts = parse_headers(jpg_bytes)
+    sampling = sampling_of(comps)
+    bpm = 6 if sampling == 1 else 3
+    qt = np.stack([qts[c[2]] for c in comps]).astype(np.int32)
+    comp_of_blk = np.array(([0] * (bpm - 2) + [1, 2]) * (cap_in.shape[0] // bpm))
+    nat = cap_in[:, ZIGZAG]
+    q = qt[comp_of_blk]
+    assert (nat % q == 0).all()
+    return (nat // q).astype(np.int16), (w, h, sampling)
+
+
+def scale_pins(ref: Ref):
+    """Config-5 scale: the reference's mcu_data hashes of seeded files that are
+    regenerated rather than committed (tests/scale_pins.py), and the
+    restart-marker read-boundary case (src/decoder.cpp:122-146)."""
+    sys.path.insert(0, os.path.dirname(HERE))
+    import scale_pins as SP
+    out = {}
+    tmp = tempfile.mkdtemp(prefix="hjd_scale_")
+    try:
+        for name, (kind, params) in SP.SCALE_CASES.items():
+            files = []
+            for k, jpg in enumerate(SP.generate(name)):
+                path = os.path.join(tmp, "f.jpg")
+                with open(path, "wb") as f:
+                    f.write(jpg)
+                cap_in, _, _ = ref.decode(path)
+                q16, (w, h, sampling) = q16_of_mcu_data(cap_in, jpg)
+                files.append({"jpeg_sha256": SP.sha(jpg), "jpeg_bytes": len(jpg), "blocks": int(cap_in.shape[0]),
+                              "mcu_data_sha256": SP.sha(np.ascontiguousarray(cap_in, dtype="<i4")),
+                              "coefs_q16_sha256": SP.sha(np.ascontiguousarray(q16, dtype="<i2"))})
+            out[name] = {"generator": kind, "params": params, "width": w, "height": h, "sampling": sampling,
+                         "files": files}
+            print(f"scale {name}: {len(files)} file(s) {w}x{h} samp={sampling}")
+        # DRI read boundary: FHD q50 bases (seed 501, 601, ...) until the
+        # reference loses an RST marker on the DRI re-encode
+        for seed in [501] + list(range(601, 640)):
+            base = SP.encode_jpeg(SP.synthetic_rgb(1920, 1080, seed), 50, 2)
+            path = os.path.join(tmp, "base.jpg")
+            with open(path, "wb") as f:
+                f.write(base)
+            cap_in, _, _ = ref.decode(path)
+            q16, _ = q16_of_mcu_data(cap_in, base)
+            dri = SP.dri_file(base, q16)
+            with open(path, "wb") as f:
+                f.write(dri)
+            ok, log = ref.try_decode(path)
+            line = next((ln for ln in log.splitlines() if "expected RST" in ln), "")
+            print(f"dri seed {seed}: reference {'accepts' if ok else 'rejects'} {line.strip()[:80]}")
+            if not ok and line:
+                out["dri_read_boundary"] = {
+                    "base": {"generator": "synthetic", "w": 1920, "h": 1080, "quality": 50, "subsampling": 2,
+                             "seed": seed},
+                    "restart_interval": SP.DRI_INTERVAL, "base_jpeg_sha256": SP.sha(base),
+                    "jpeg_sha256": SP.sha(dri), "jpeg_bytes": len(dri),
+                    "mcu_data_sha256": SP.sha(np.ascontiguousarray(cap_in, dtype="<i4")),
+                    "coefs_q16_sha256": SP.sha(np.ascontiguousarray(q16, dtype="<i2")),
+                    "reference_log": line.strip()}
+                break
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    return out
+
+
 def main():
+    if "--scale-only" in sys.argv:   # refresh manifest["scale"] only
+        ref = Ref()
+        path = os.path.join(HERE, "manifest.json")
+        manifest = json.load(open(path))
+        manifest["scale"] = scale_pins(ref)
+        with open(path, "w") as f:
+            json.dump(manifest, f, indent=1, sort_keys=True)
+        print("wrote", path)
+        return
     if not os.path.exists(REF_LIB):
         sys.exit("build the reference first: make -C oracle")
     ref = Ref()
@@ -249,6 +349,7 @@ def main():
         manifest["cases"][name] = golden_case(ref, name, jpg, {"source": f"Pillow q={qual} subsampling={sub} {kw}"})
     manifest.update(idct_vectors(ref))
     manifest.update(csc_exhaustive(ref))
+    manifest["scale"] = scale_pins(ref)
     with open(os.path.join(HERE, "manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1, sort_keys=True)
     print("wrote", os.path.join(HERE, "manifest.json"))

@@ -242,3 +242,35 @@ def test_edge_coefficients_round_trip(lib, sampling, dri):
         lib.hjd_debug_host_reader(0)
     assert rc == 0
     np.testing.assert_array_equal(got, coefs)
+
+
+def test_small_thread_stack(lib):
+    """The Huffman tables live in per-thread heap sets, not on the stack
+    (ADVICE r05): the pair decode, the one-file decode and a header parse run
+    on a thread with a 256 KiB stack (the r05 Frame alone was ~165 KB)."""
+    import threading
+    files = _corpus()[:4]
+    singles = [decode(lib, d) for d in files]
+    cap = max(i.nblocks for _, i, _ in singles)
+    res = {}
+
+    def body():
+        try:
+            res["pair"] = _batch(lib, files, cap, nthreads=1)   # the calling thread decodes the pairs
+            res["one"] = decode(lib, files[0])
+        except BaseException as e:   # noqa: BLE001 -- reported by the main thread
+            res["error"] = e
+
+    old = threading.stack_size(256 * 1024)
+    try:
+        t = threading.Thread(target=body)
+        t.start()
+        t.join()
+    finally:
+        threading.stack_size(old)
+    assert "error" not in res, res.get("error")
+    status, outs = res["pair"]
+    for k, (rc, info, coefs) in enumerate(singles):
+        assert status[k] == rc == 0
+        np.testing.assert_array_equal(outs[k][: info.nblocks], coefs)
+    np.testing.assert_array_equal(res["one"][2], singles[0][2])

@@ -121,9 +121,14 @@ def test_stream_truncated_scan_reported(hjd, ctx):
 
 
 def test_4k_jpeg_end_to_end(hjd, ctx):
+    """Config 5's first pool file: its host coefficients hash to the
+    reference's mcu_data (tests/scale_pins.py), its pixels are the oracle's."""
     import torch
-    data = _pil(3840, 2160, 90, 2, seed=4)
+    import scale_pins as SP
+    data = SP.generate_one("bench_pool_4k420_q90", 0)
     coefs, info = hjd.decode_coefs(data)
+    rec = SP.manifest_scale()["bench_pool_4k420_q90"]["files"][0]
+    assert SP.check_coefs(rec, data, coefs, info.qt, info.sampling) == "pinned"
     out = hjd.decode_jpeg(ctx, data)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), O.decode_q16(coefs, info.qt, 3840, 2160, 1))

@@ -127,15 +127,16 @@ def test_vacuous_truncation_case_now_rejected(lib):
     assert decode(lib, good[: len(good) // 2] + b"\xff\xd9")[0] != 0
 
 
-def test_spare_byte_before_rst_rejected(lib):
+def test_spare_byte_before_rst_rejected(lib, hjd):
     """The reference reads the byte after an interval's last bits as the RSTn
     marker (src/decoder.cpp:295-302): a whole extra byte in front of the
-    marker is a mismatch there, and here (both readers)."""
+    marker is a mismatch there, and here (both readers, the GPU algorithm)."""
     data = bytearray(_golden("syn420_160x48_q95_dri"))
     at = data.index(b"\xff\xd0")
     bad = bytes(data[:at] + b"\x5a" + data[at:])
     for rc, err, _, _ in host_status(lib, bad):
         assert rc != 0 and b"expected RST0" in err, err
+    assert not emulated_ok(hjd, bad)
 
 
 # ---- live comparison with the compiled reference (this container only) ------

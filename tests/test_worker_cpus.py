@@ -76,3 +76,50 @@ def test_allowed_cpus_intersection(tmp_path):
     root = _tree(tmp_path, {0: f"0-{hi + 64}"}, {GPUS8[0]: 0})
     assert hjd.worker_cpus(GPUS8[0], GPUS8[:1], root, only_allowed=True) == allowed
     assert len(hjd.worker_cpus(GPUS8[0], GPUS8[:1], root)) == hi + 65
+
+
+def test_stream_threads_eight_gpu_node(tmp_path):
+    """bench.py config 5's per-GPU host worker count on the 8-GPU node's
+    topology (2 NUMA nodes x 128 logical CPUs, 4 GPUs each): with no cgroup
+    quota every rank uses its whole 32-CPU slice (SMT siblings included); a
+    quota splits over the ranks first; a one-GPU 16-CPU box keeps 16."""
+    nodes = {0: "0-63,128-191", 1: "64-127,192-255"}
+    root = _tree(tmp_path, nodes, {g: (0 if i < 4 else 1) for i, g in enumerate(GPUS8)})
+    slices = [len(hjd.worker_cpus(g, GPUS8, root)) for g in GPUS8]
+    assert slices == [32] * 8
+    assert [hjd.stream_worker_threads(256, 8, n) for n in slices] == [32] * 8      # no quota
+    assert [hjd.stream_worker_threads(128, 8, n) for n in slices] == [16] * 8      # quota 128 CPUs
+    assert hjd.stream_worker_threads(16, 1, 128) == 16                             # the one-GPU box
+    assert hjd.stream_worker_threads(256, 8, 0) == 32                              # unknown topology
+
+
+def _cgroup_tree(tmp_path, self_cgroup, files):
+    root = tmp_path / "cg"
+    (root / "proc" / "self").mkdir(parents=True)
+    (root / "proc" / "self" / "cgroup").write_text(self_cgroup)
+    for rel, text in files.items():
+        f = root / rel
+        f.parent.mkdir(parents=True, exist_ok=True)
+        f.write_text(text)
+    return str(root)
+
+
+def test_cpu_share_cgroup_versions(tmp_path):
+    """hjd_host_cpu_share's quota on fake trees: v2 at the root and nested (an
+    ancestor's smaller limit wins), v1 cpu,cpuacct, and no quota at all."""
+    aff = len(os.sched_getaffinity(0))
+    cases = [
+        ("0::/\n", {"sys/fs/cgroup/cpu.max": "300000 100000\n"}, 3),
+        ("0::/a/b\n", {"sys/fs/cgroup/a/b/cpu.max": "max 100000\n", "sys/fs/cgroup/a/cpu.max": "250000 100000\n"}, 3),
+        ("0::/a/b\n", {"sys/fs/cgroup/a/b/cpu.max": "100000 100000\n", "sys/fs/cgroup/a/cpu.max": "800000 100000\n"}, 1),
+        ("12:cpu,cpuacct:/docker/x\n3:memory:/docker/x\n",
+         {"sys/fs/cgroup/cpu,cpuacct/docker/x/cpu.cfs_quota_us": "200000\n",
+          "sys/fs/cgroup/cpu,cpuacct/docker/x/cpu.cfs_period_us": "100000\n"}, 2),
+        ("12:cpu,cpuacct:/\n", {"sys/fs/cgroup/cpu,cpuacct/cpu.cfs_quota_us": "-1\n",
+                                "sys/fs/cgroup/cpu,cpuacct/cpu.cfs_period_us": "100000\n"}, None),
+        ("0::/\n", {"sys/fs/cgroup/cpu.max": "max 100000\n"}, None),
+    ]
+    for i, (self_cg, files, quota) in enumerate(cases):
+        root = _cgroup_tree(tmp_path / str(i), self_cg, files)
+        want = min(aff, quota) if quota else aff
+        assert hjd.cpu_share(root) == want, (i, hjd.cpu_share(root), want)
