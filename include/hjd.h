@@ -209,7 +209,9 @@ int hjd_debug_csc_exhaustive(hjd_ctx* ctx, uint32_t* d_out, int mode, void* stre
  * (timing only).  stages: 80 = memory only (coefficient loads, staging, LDS
  * reads and BGRX stores kept; no IDCT, no colour math), 4 = no stores,
  * 16 = no IDCT, 64 = no colour math, 20 = no IDCT and no stores, 8 = no colour
- * stage, 24 = neither IDCT nor colour stage.  4:2:0 / 4:4:4, int16 zigzag
+ * stage, 24 = neither IDCT nor colour stage, 256 = every lane gathers row 0
+ * of its block (the product's instructions without the zigzag gather's LDS
+ * bank conflicts).  4:2:0 / 4:4:4, int16 zigzag
  * input, BGRX output only.  grid_blocks as hjd_plan_launch (0 = the plan's launch shape,
  * hjd_plan_autotune's if it ran). */
 int hjd_debug_plan_launch_stages(hjd_plan* plan, int stages, const void* d_coefs, void* d_out, void* stream,

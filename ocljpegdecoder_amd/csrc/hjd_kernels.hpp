@@ -187,6 +187,10 @@ constexpr int kOutBgr24 = 32;
 // Gather pairs as ds_read_u16 | ds_read_u16_d16_hi (load_round_pk_d16): only
 // valid where d16 loads zero the other half (sramecc+), chosen at launch.
 constexpr int kVarD16 = 128;
+// kAblGatherBroadcast: every lane gathers row 0 of its block (lanes of a
+// block read the same words: no LDS bank conflicts), the same instructions as
+// the product -- what the zigzag gather's conflicts cost.
+constexpr int kAblGatherBroadcast = 256;
 template <int kVariant>
 constexpr int kOutBytes = (kVariant & kOutBgr24) != 0 ? 3 : 4;
 
@@ -789,7 +793,8 @@ __global__ __launch_bounds__(kGroupThreads, KLayout::min_waves) void decode_kern
 
     int zoff[8];
 #pragma unroll
-    for (int c = 0; c < 8; ++c) zoff[c] = 2 * zz_of_natural(r * 8 + c);
+    for (int c = 0; c < 8; ++c)
+        zoff[c] = (kVariant & kAblGatherBroadcast) != 0 ? 2 * zz_of_natural(c) : 2 * zz_of_natural(r * 8 + c);
 
     uint32_t q[3][4];   // this lane's row of each component's qtable, 16-bit pairs
     int q_tables[3] = {-1, -1, -1};

@@ -217,18 +217,18 @@ int hjd_internal::launch_decode(int device, int num_cu, int sampling, int input_
     }
     if (fmt == 0 && (variant >> kStageShift) != 0) {   // stage-skipping measurement variants
         if (sg.index > 1) return hjd_internal::set_error(HJD_E_INVALID, "ablation variants are 4:4:4/4:2:0 only");
-        constexpr int kStages[7] = {4, 8, 16, 20, 24, 64, 80};
+        constexpr int kStages[8] = {4, 8, 16, 20, 24, 64, 80, 256};
         const int stages = variant >> kStageShift;
         int si = -1;
-        for (int i = 0; i < 7; ++i)
+        for (int i = 0; i < 8; ++i)
             if (kStages[i] == stages) si = i;
         if (si < 0) return hjd_internal::set_error(HJD_E_INVALID, "unknown ablation variant %d", stages);
 #define HJD_ST(S, B) {hjd::decode_kernel<S, 0, 4 | (B)>, hjd::decode_kernel<S, 0, 8 | (B)>,                  \
                       hjd::decode_kernel<S, 0, 16 | (B)>, hjd::decode_kernel<S, 0, 20 | (B)>,                \
                       hjd::decode_kernel<S, 0, 24 | (B)>, hjd::decode_kernel<S, 0, 64 | (B)>,                \
-                      hjd::decode_kernel<S, 0, 80 | (B)>}
+                      hjd::decode_kernel<S, 0, 80 | (B)>, hjd::decode_kernel<S, 0, 256 | (B)>}
         // [4:2:0, 4:4:4, 4:4:4 d16 gather][stages]
-        static const KP kStageK[3][7] = {HJD_ST(1, 0), HJD_ST(0, 0), HJD_ST(0, hjd::kVarD16)};
+        static const KP kStageK[3][8] = {HJD_ST(1, 0), HJD_ST(0, 0), HJD_ST(0, hjd::kVarD16)};
 #undef HJD_ST
         const int col = sampling == HJD_YUV420 ? 0 : device_d16_gather(device) ? 2 : 1;   // as the product gathers
         const KP k = kStageK[col][si];
@@ -704,7 +704,8 @@ int hjd_debug_plan_launch_stages(hjd_plan* plan, int stages, const void* d_coefs
                                  int grid_blocks)
 {
     if (!plan) return fail(HJD_E_INVALID, "plan is NULL");
-    if (stages != 4 && stages != 16 && stages != 20 && stages != 64 && stages != 80 && stages != 8 && stages != 24)
+    if (stages != 4 && stages != 16 && stages != 20 && stages != 64 && stages != 80 && stages != 8 && stages != 24 &&
+        stages != 256)
         return fail(HJD_E_INVALID, "unknown stage variant %d", stages);
     if (plan->input_format != HJD_IN_Q16_ZIGZAG || plan->out_format != HJD_OUT_BGRX ||
         (plan->sampling != HJD_YUV420 && plan->sampling != HJD_YUV444))

@@ -2,7 +2,9 @@
 plan of synthetic 3840x2160 frames (default 4:4:4, 64 frames), launched as
 the product kernel and as the stage-ablation variants (hjd_debug_plan_launch_
 stages: 16 no IDCT -- no zigzag gather, transpose or sample write-back --,
-8 no colour stage, 64 no colour math), each `--reps` times.  Run under
+8 no colour stage, 64 no colour math, 256 the gather without bank conflicts),
+each `--reps` times, and then `--timed` interleaved rounds of the product
+and the conflict-free gather timed with HIP events (what the conflicts cost).  Run under
 
     rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_LDS SQ_WAVES --kernel-trace \
         --output-format csv -d <dir> -o lds -- python3 tools/lds_conflict_probe.py
@@ -22,7 +24,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "tests"))
 
-VARIANTS = [(0, "product"), (16, "no_idct"), (8, "no_colour"), (64, "no_csc")]
+VARIANTS = [(0, "product"), (16, "no_idct"), (8, "no_colour"), (64, "no_csc"), (256, "broadcast_gather")]
 
 
 def run(a):
@@ -50,8 +52,19 @@ def run(a):
         if st == 0:   # the product's output is right
             got = out[0].cpu().numpy().view("uint32")
             assert (got == O.decode_q16(coefs, qt, w, h, s)).all()
+    timed = {"product": [], "broadcast_gather": []}
+    for _ in range(a.timed):
+        for st, name in ((0, "product"), (256, "broadcast_gather")):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(5):
+                plan.launch(d_coefs, out) if st == 0 else plan.launch_stages(st, d_coefs, out)
+            e1.record()
+            torch.cuda.synchronize()
+            timed[name].append(round(e0.elapsed_time(e1) / 5, 4))
     print(json.dumps({"order": order, "tasks": plan.tasks, "frames": nf, "sampling": s,
-                      "shape": plan.launch_shape()}))
+                      "shape": plan.launch_shape(), "ms_per_launch": timed,
+                      "how": "HIP events around 5 launches, interleaved rounds (no profiler when --timed runs alone)"}))
     plan.close()
     ctx.close()
 
@@ -88,6 +101,7 @@ if __name__ == "__main__":
     ap.add_argument("--sampling", type=int, default=0)
     ap.add_argument("--frames", type=int, default=64)
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--timed", type=int, default=0)
     ap.add_argument("--summarise")
     a = ap.parse_args()
     summarise(a.summarise) if a.summarise else run(a)
