@@ -1555,7 +1555,9 @@ def config5_stream_leg(world, dist_backend, frame_ids=100000, workload="stream4k
         return {"error": "timeout after 900 s"}
     line = next((l for l in reversed(out.splitlines()) if l.startswith("{")), None)
     if p.returncode != 0 or line is None:
-        return {"error": f"rc {p.returncode}", "stderr_tail": err[-400:]}
+        # the child ranks' own error lines (torchrun's summary fills the tail)
+        errs = [ln[-300:] for ln in err.splitlines() if "Error" in ln or "FATAL" in ln or "error:" in ln][-6:]
+        return {"error": f"rc {p.returncode}", "stderr_tail": err[-400:], "error_lines": errs}
     d = json.loads(line)
     return {"value": d["value"], "unit": d["unit"], "n_gpus": d["n_gpus"], "ms_per_step": d["ms_per_step"],
             "steps": d["steps"], "frames_per_gpu_per_step": d["config"]["frames_per_gpu_per_step"],

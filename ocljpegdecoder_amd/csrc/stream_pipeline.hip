@@ -234,6 +234,11 @@ void hjd_stream::worker()
                     rc[i] = hjd_jpeg_decode_coefs(jobs[i].data, jobs[i].size, &info[i], coefs[i], max_blocks);
         }
         decode_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+        // In a pair whose files both failed, the thread's last error is the
+        // second file's: decode the first alone again (errors are rare) so the
+        // stream records the first failing job's own message.
+        if (n == 2 && rc[0] != HJD_OK && rc[1] != HJD_OK && rc[0] != HJD_E_HIP)
+            (void)hjd_jpeg_decode_coefs(jobs[0].data, jobs[0].size, &info[0], coefs[0], max_blocks);
         for (int i = 0; i < n; ++i) {
             rc[i] = issue(jobs[i], rc[i], info[i]);
             if (rc[i] != HJD_OK) record_error(rc[i], hjd_last_error());

@@ -120,6 +120,22 @@ def test_stream_truncated_scan_reported(hjd, ctx):
         np.testing.assert_array_equal(again.cpu().numpy().view(np.uint32), goods[1][1])
 
 
+def test_stream_error_names_the_first_failing_job(hjd, ctx):
+    """Two truncated files decoded as one worker's pair: the stream reports
+    the first one's error (its MCU count), not the second's."""
+    import torch
+    a = open(os.path.join(O.GOLDEN, "JPEG_example_JPG_RIP_050.jpg"), "rb").read()   # 300 MCUs
+    b = open(os.path.join(O.GOLDEN, "syn444_64x40_q90.jpg"), "rb").read()           # 40 MCUs
+    cut = [d[: hjd.parse(d).scan_offset + (len(d) - hjd.parse(d).scan_offset) // 2] + b"\xff\xd9" for d in (a, b)]
+    outs = [torch.zeros((234, 313), dtype=torch.int32, device="cuda"), torch.zeros((40, 64), dtype=torch.int32,
+                                                                                     device="cuda")]
+    with hjd.JpegStream(ctx, 2048, nslots=4, nthreads=1) as st:
+        for d, o in zip(cut, outs):
+            st.submit(d, o)
+        with pytest.raises(hjd._lib.HjdError, match="of 300"):
+            st.sync()
+
+
 def test_4k_jpeg_end_to_end(hjd, ctx):
     """Config 5's first pool file: its host coefficients hash to the
     reference's mcu_data (tests/scale_pins.py), its pixels are the oracle's."""
