@@ -1473,6 +1473,57 @@ size_t scan_end(const uint8_t* d, size_t n, size_t p)
 
 }  // namespace
 
+int hjd_internal::parse_scan_header(const uint8_t* data, size_t size, ScanHeader* h)
+{
+    if (!data || !h) return set_error(HJD_E_INVALID, "NULL argument");
+    Frame f(2, false);
+    int rc = parse(data, size, f);
+    if (rc) return rc;
+    if (f.process == 2)
+        return set_error(HJD_E_INVALID, "progressive JPEG: the GPU entropy decoder takes sequential scans "
+                         "(decode it with the host decoder, hjd_jpeg_decode_coefs / hjd_stream)");
+    fill_scan_header(f, h);
+    return HJD_OK;
+}
+
+int hjd_internal::parse_scan_headers(const uint8_t* data, size_t size, std::vector<ScanHeader>* hs)
+{
+    if (!data || !hs) return set_error(HJD_E_INVALID, "NULL argument");
+    hs->clear();
+    Frame f(2, false);
+    int rc = parse(data, size, f);
+    if (rc) return rc;
+    if (f.process == 2)
+        return set_error(HJD_E_INVALID, "progressive JPEG: the GPU entropy decoder takes sequential scans "
+                         "(decode it with the host decoder, hjd_jpeg_decode_coefs / hjd_stream)");
+    bool seen[3] = {false, false, false};
+    for (;;) {
+        for (int i = 0; i < f.scan.ns; ++i) {
+            if (seen[f.scan.comp[i]])   // T.81 B.2.3: a sequential frame codes each component in one scan
+                return set_error(HJD_E_INVALID, "component %d in two sequential scans", f.scan.comp[i]);
+            seen[f.scan.comp[i]] = true;
+        }
+        hs->emplace_back();
+        fill_scan_header(f, &hs->back());
+        size_t p = scan_end(data, size, f.scan.offset);
+        bool eoi = false;
+        rc = parse_segments(data, size, &p, f, true, &eoi);
+        if (rc) return rc;
+        if (eoi) break;
+    }
+    for (int c = 0; c < f.ncomp; ++c)
+        if (!seen[c]) return set_error(HJD_E_INVALID, "component %d is in no scan", c);
+    return HJD_OK;
+}
+
+int hjd_internal::jpeg_decode_coefs_two(const uint8_t* const data[2], const size_t size[2], hjd_jpeg_info* const info[2],
+                                        int16_t* const coefs[2], const int64_t capacity[2], int rc[2])
+{
+    decode_two(data, size, info, coefs, capacity, rc);
+    return rc[0] != HJD_OK ? rc[0] : rc[1];
+}
+
+// ---- the process's CPU share (hjd_host_cpu_share) --------------------------
 namespace {
 
 std::string read_small_file(const std::string& path)
@@ -1555,56 +1606,6 @@ int cpu_share(const std::string& root)
 }
 
 }  // namespace
-
-int hjd_internal::parse_scan_header(const uint8_t* data, size_t size, ScanHeader* h)
-{
-    if (!data || !h) return set_error(HJD_E_INVALID, "NULL argument");
-    Frame f(2, false);
-    int rc = parse(data, size, f);
-    if (rc) return rc;
-    if (f.process == 2)
-        return set_error(HJD_E_INVALID, "progressive JPEG: the GPU entropy decoder takes sequential scans "
-                         "(decode it with the host decoder, hjd_jpeg_decode_coefs / hjd_stream)");
-    fill_scan_header(f, h);
-    return HJD_OK;
-}
-
-int hjd_internal::parse_scan_headers(const uint8_t* data, size_t size, std::vector<ScanHeader>* hs)
-{
-    if (!data || !hs) return set_error(HJD_E_INVALID, "NULL argument");
-    hs->clear();
-    Frame f(2, false);
-    int rc = parse(data, size, f);
-    if (rc) return rc;
-    if (f.process == 2)
-        return set_error(HJD_E_INVALID, "progressive JPEG: the GPU entropy decoder takes sequential scans "
-                         "(decode it with the host decoder, hjd_jpeg_decode_coefs / hjd_stream)");
-    bool seen[3] = {false, false, false};
-    for (;;) {
-        for (int i = 0; i < f.scan.ns; ++i) {
-            if (seen[f.scan.comp[i]])   // T.81 B.2.3: a sequential frame codes each component in one scan
-                return set_error(HJD_E_INVALID, "component %d in two sequential scans", f.scan.comp[i]);
-            seen[f.scan.comp[i]] = true;
-        }
-        hs->emplace_back();
-        fill_scan_header(f, &hs->back());
-        size_t p = scan_end(data, size, f.scan.offset);
-        bool eoi = false;
-        rc = parse_segments(data, size, &p, f, true, &eoi);
-        if (rc) return rc;
-        if (eoi) break;
-    }
-    for (int c = 0; c < f.ncomp; ++c)
-        if (!seen[c]) return set_error(HJD_E_INVALID, "component %d is in no scan", c);
-    return HJD_OK;
-}
-
-int hjd_internal::jpeg_decode_coefs_two(const uint8_t* const data[2], const size_t size[2], hjd_jpeg_info* const info[2],
-                                        int16_t* const coefs[2], const int64_t capacity[2], int rc[2])
-{
-    decode_two(data, size, info, coefs, capacity, rc);
-    return rc[0] != HJD_OK ? rc[0] : rc[1];
-}
 
 extern "C" {
 
