@@ -582,8 +582,7 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
             pool_c.append(arena[pos:pos + len(d)])
             pos += len(d)
     else:
-        from ocljpegdecoder_amd.jpeg import _buf
-        pool_c = [_buf(d) for d in pool]
+        pool_c = pool   # the bytes themselves: submit passes their address, no copy
     G = nf * world
 
     def step(k):
