@@ -666,8 +666,8 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
             f = ids[i] % npool
             if f not in exp_cs:
                 coefs, info = hjd.decode_coefs(pool[f])
-                pin_count[SP.check_coefs(pins[f], pool[f], coefs, info.qt, info.sampling) if f < len(pins)
-                          else "unpinned"] += 1
+                pin_count[SP.check_coefs(pins[f], pool[f], coefs, info.qt, info.sampling, natural=False)
+                          if f < len(pins) else "unpinned"] += 1
                 e = O.decode_q16(coefs, info.qt, info.width, info.height, info.sampling)
                 if ofmt != hjd.OUT_BGRX:
                     e = np.zeros((h, pitch), np.uint8)

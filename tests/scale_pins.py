@@ -112,13 +112,18 @@ def manifest_scale():
         return json.load(f).get("scale", {})
 
 
-def check_coefs(rec: dict, jpeg: bytes, coefs_q16: np.ndarray, qt: np.ndarray, sampling: int) -> str:
+def check_coefs(rec: dict, jpeg: bytes, coefs_q16: np.ndarray, qt: np.ndarray, sampling: int,
+                natural: bool = True) -> str:
     """'pinned' (the coefficients hash to the reference's), 'unpinned' (this
-    box generated a different JPEG, so the pin does not apply) or 'MISMATCH'."""
+    box generated a different JPEG, so the pin does not apply) or 'MISMATCH'.
+    natural=False checks the int16 form only (bench.py: it is the reference's
+    mcu_data divided by the file's tables, exactly, so it pins the same data)."""
     if sha(jpeg) != rec["jpeg_sha256"]:
         return "unpinned"
     if sha(np.ascontiguousarray(coefs_q16, dtype="<i2")) != rec["coefs_q16_sha256"]:
         return "MISMATCH"
+    if not natural:
+        return "pinned"
     bpm = 6 if sampling == 1 else 3
     comp = np.array(([0] * (bpm - 2) + [1, 2]) * (coefs_q16.shape[0] // bpm))
     nat = np.zeros(coefs_q16.shape, np.int32)
