@@ -193,3 +193,38 @@ def test_cut_sweep_matches_reference(lib, hjd, name):
             np.testing.assert_array_equal(cap[:-1], full[:-1], err_msg=label)
             stats["last_component"] += 1
     assert stats["both_accept"] >= 2 and stats["both_reject"] >= 90, stats
+
+
+def _with_com_after_scan(data: bytes) -> bytes:
+    """A COM segment between the scan and EOI (legal: T.81 B.2.4.5 tables/misc.)."""
+    assert data[-2:] == b"\xff\xd9"
+    return data[:-2] + b"\xff\xfe\x00\x06test" + b"\xff\xd9"
+
+
+@pytest.mark.parametrize("name", FILES)
+def test_marker_after_scan_decodes(lib, hjd, name):
+    """A marker segment after the scan ends the entropy data: both readers, the
+    pair decode and the GPU entropy algorithm give the golden coefficients."""
+    d = _with_com_after_scan(_golden(name))
+    exp = O.load_case(name)["coefs_q16"]
+    for rc, err, coefs, _ in host_status(lib, d):
+        assert rc == 0, err
+        np.testing.assert_array_equal(coefs, exp)
+    status, outs = _batch(lib, [d, d], exp.shape[0])
+    assert list(status) == [0, 0]
+    np.testing.assert_array_equal(outs[1], exp)
+    emu, st = hjd.emulate_entropy(d, 256)
+    assert st & ~1 == 0
+    np.testing.assert_array_equal(emu, exp)
+
+
+@pytest.mark.skipif(not O.ref_available(), reason="needs oracle/_ref/libref.so (make -C oracle)")
+def test_marker_after_scan_reference_defect():
+    """The reference drops the data in front of an unknown marker within one
+    of its 2,048-byte reads (read_more_data's default case returns without
+    appending, src/decoder.cpp:147-148), so it rejects the sample with a COM
+    segment after its scan: "data incomplete" (INTEGRATION.md s4)."""
+    ok, _ = _ref_decode(_with_com_after_scan(_golden("JPEG_example_JPG_RIP_050")))
+    assert not ok
+    ok, _ = _ref_decode(_golden("JPEG_example_JPG_RIP_050"))
+    assert ok
