@@ -599,7 +599,7 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
             const int32_t v = bits <= (m >> 1) ? static_cast<int32_t>(bits - m) : static_cast<int32_t>(bits);
             pos += total;
             const uint32_t zn = z + zk;
-            if (zn > 64 && s != 0) flags |= kError;   // AC coefficient past index 63
+            if (zn > 64 && zk != 64) flags |= kError;   // AC coefficient or ZRL past index 63 (not EOB)
             // DC unit: a block starts (per-component sums by 0/1 multipliers, no branch)
             const int32_t dv = dc ? v : 0;
             nblk += dc ? 1 : 0;

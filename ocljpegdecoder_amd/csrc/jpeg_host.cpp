@@ -586,7 +586,8 @@ inline bool decode_block(BitReader& br, const HuffTable& dc, const HuffTable& ac
         const int r = rs >> 4, sz = rs & 15;
         if (sz == 0) {
             if (r != 15) break;   // EOB
-            k += 16;              // ZRL
+            k += 16;              // ZRL; one past index 63 is corrupt (the reference
+            if (k > 64) return false;   // asserts count + 1 <= 64, src/decoder.cpp:244-245)
             continue;
         }
         k += r;
@@ -950,8 +951,9 @@ struct FastDec {
         const int r = rs >> 4, sz = rs & 15;
         if (sz == 0) {
             if (r != 15) return end_block();   // EOB
-            k += 16;                            // ZRL (a run to or past 64 ends the block, as decode_block)
-            if (k >= 64) end_block();
+            k += 16;                            // ZRL: to 64 ends the block, past it is corrupt (decode_block)
+            if (k > 64) return fail(1);
+            if (k == 64) end_block();
             return;
         }
         k += r;
