@@ -22,6 +22,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <new>
@@ -411,16 +413,19 @@ Caps make_caps(int max_frames, int64_t max_scan_bytes, int64_t max_blocks, int s
     // gray file) with Ri = 1 has one per block, so blocks + one per entropy frame
     c.max_segs = max_blocks + ef;
     c.max_tiles = max_scan_bytes / kTileBytes + max_frames;
-    const size_t per_frame = (sizeof(EntFrame) + sizeof(HuffLut) * kMaxTables) * kMaxScans + sizeof(FrameRecord) +
+    const size_t per_frame = (sizeof(EntFrame) + sizeof(HuffLut) * kMaxTables + 4) * kMaxScans + sizeof(FrameRecord) +
                              192 * 4 + sizeof(RawFrame);
     c.hdr_cap = align_up(per_frame * max_frames + 4 * static_cast<size_t>(c.max_segs + c.max_wgs + c.max_tiles) +
                              10 * kAlign, kAlign);
     c.data = c.hdr_cap;
+#ifdef HJD_TMP_DATA_SKEW
+    c.data += HJD_TMP_DATA_SKEW;
+#endif
     return c;
 }
 
 struct HdrOffsets {
-    size_t frames, tabs, seg, wg, recs, qt, rawf, tilef, used;
+    size_t frames, tabs, seg, wg, recs, qt, rawf, tilef, status, used;
 };
 
 // Device-side view of a batch (kernel argument).
@@ -437,6 +442,7 @@ struct EntBatchDev {
     uint64_t* wentries;   // [group][kWarm] warm-up entries
     uint32_t* linked;     // [group] 1 if joined to the previous group's chain
     SubStats* agg;
+    SubStats* agg2;       // [group] null, or the rest of agg: a group's statistics in the next chain chunk
     uint32_t* status;
     int16_t* coefs;
     uint32_t nframes, nwg, sub_bits, ntab_max;   // ntab_max: tables of the largest frame (dynamic LDS)
@@ -453,11 +459,12 @@ struct EntBatchDev {
     struct SpecRec* spec;        // [sub][kMaxBpm]
     struct CandRec* cand;        // [sub][kSlots]
     uint8_t* cmap;               // [sub][kSlotRow]
-    uint8_t* cslot;              // [sub] the verified chain's slot (ent_chain_scan_kernel / ent_chain_kernel)
+    uint8_t* cslot;              // [sub] the verified chain's slot (ent_chain_lb_kernel / ent_chain_kernel)
     uint32_t spec_lead;          // lead-in of the spec runs (bits)
-    uint32_t* chainfn;           // [frame][chain_chunks][5] each chunk's composed slot map (ent_chain_fn_kernel)
-    uint32_t* chain_broken;      // [frame] 1: the chain leaves its slots somewhere (serial walk with repairs)
+    uint32_t* chainfn;           // [frame][chain_chunks][5] look-back words of the chunks (ent_chain_lb_kernel)
+    uint32_t* chain_broken;      // [frame] chain_epoch: the chain leaves its slots somewhere (serial walk with repairs)
     uint32_t chain_chunks;       // chunks of the frame with the most subsequences (grid width)
+    uint32_t chain_epoch;        // 1 .. 2^24 - 1, new per launch: tags the look-back words (no clearing)
 };
 
 
@@ -546,18 +553,31 @@ __host__ __device__ __forceinline__ int64_t group_sub(uint32_t gl, int t)
 // The chain is exact by construction (every record comes from a real run of
 // its subsequence from the entry it names, starting at the frame start); a
 // chain that leaves all slots (none seen) falls back to the sequential repair.
+// The write kernel decodes a verified subsequence as four quarters, each from
+// the state at its first unit boundary >= k*S + q*S/4 (q = 0: the entry):
+// the runs below stop there on the way and keep those states.
+__host__ __device__ __forceinline__ uint32_t quarter_stop(uint32_t k, uint32_t S, uint32_t q)
+{
+    return k * S + (q * S) / 4;
+}
 struct SpecRec {          // spec run of subsequence k from guess (k*S - W, j, 0)
     uint64_t cp;          // state at the first unit boundary >= k*S + S/2
     uint64_t x;           // exit
     SubStats s2;          // statistics cp -> x
+    SubStats s3;          // statistics cp -> q3
+    uint64_t q3, pad;     // state at the third quarter (as cp at the middle)
 };
-static_assert(sizeof(SpecRec) == 32, "SpecRec layout");
+static_assert(sizeof(SpecRec) == 64, "SpecRec layout");
 struct CandRec {          // subsequence k run from the entry of one of its slots
-    SubStats s1, s;       // statistics entry -> mid and entry -> exit
-    uint64_t e, mid, y;   // entry, mid-state, exit
-    uint64_t pad;
+    SubStats s1, s;       // [0] [1] statistics entry -> mid and entry -> exit
+    uint64_t e, mid;      // [2] entry, mid-state
+    uint64_t y, q1;       // [3] exit, first-quarter state
+    SubStats sq1;         // [4] statistics entry -> q1
+    SubStats sq3;         // [5] statistics mid -> q3
+    uint64_t q3, pad0;    // [6] third-quarter state
+    uint64_t pad1, pad2;  // [7]
 };
-static_assert(sizeof(CandRec) == 64, "CandRec layout");
+static_assert(sizeof(CandRec) == 128, "CandRec layout");
 constexpr uint32_t kNoCand = 0xFF;                   // no slot
 constexpr int kOvfLevels = 2;                        // overflow slots: P per level
 constexpr int kSlots = (1 + kOvfLevels) * kMaxBpm;   // candidate and overflow slots per subsequence
@@ -573,10 +593,16 @@ __host__ __device__ __forceinline__ SpecRec spec_run(const RunCtx& c, uint32_t k
     const uint32_t start = k * S > lead ? k * S - lead : 0u;
     const uint64_t g = guess_entry(c, start);
     SpecRec r;
-    SubStats s1 = stats_identity();
-    r.cp = run<false>(c, pack_state(st_pos(g), j, 0, st_seg(g)), k * S + S / 2, s1, nullptr);
-    r.s2 = stats_identity();
-    r.x = run<false>(c, r.cp, (k + 1) * S, r.s2, nullptr);
+    // one run through the middle (cp) and the third quarter (q3) to the exit
+    const uint32_t mpos[2] = {quarter_stop(k, S, 2), quarter_stop(k, S, 3)};
+    uint64_t ms[2];
+    SubStats mst[2], s4 = stats_identity();
+    r.x = run<false, 2>(c, pack_state(st_pos(g), j, 0, st_seg(g)), (k + 1) * S, s4, nullptr, mpos, ms, mst);
+    r.cp = ms[0];
+    r.q3 = ms[1];
+    r.s3 = mst[1];
+    r.s2 = stats_combine(r.s3, s4);
+    r.pad = 0;
     return r;
 }
 
@@ -587,19 +613,23 @@ __host__ __device__ __forceinline__ uint32_t cand_run(const RunCtx& c, uint32_t 
                                                       const SpecRec* sk, uint32_t P, CandRec& out)
 {
     out.e = e;
-    out.pad = 0;
-    out.s1 = stats_identity();
-    out.mid = run<false>(c, e, k * S + S / 2, out.s1, nullptr);
+    out.pad0 = out.pad1 = out.pad2 = 0;
+    const uint32_t m1 = quarter_stop(k, S, 1), m3 = quarter_stop(k, S, 3);
+    SubStats s12 = stats_identity();
+    out.mid = run<false, 1>(c, e, quarter_stop(k, S, 2), s12, nullptr, &m1, &out.q1, &out.sq1);
+    out.s1 = stats_combine(out.sq1, s12);
     uint32_t jm = kNoCand;
     for (uint32_t j = 0; j < P; ++j)
         if (jm == kNoCand && same_state(out.mid, sk[j].cp)) jm = j;
     if (jm != kNoCand) {
         out.y = sk[jm].x;
+        out.q3 = sk[jm].q3;
+        out.sq3 = sk[jm].s3;
         out.s = stats_combine(out.s1, sk[jm].s2);
     } else {
-        SubStats s2 = stats_identity();
-        out.y = run<false>(c, out.mid, (k + 1) * S, s2, nullptr);
-        out.s = stats_combine(out.s1, s2);
+        SubStats s4 = stats_identity();
+        out.y = run<false, 1>(c, out.mid, (k + 1) * S, s4, nullptr, &m3, &out.q3, &out.sq3);
+        out.s = stats_combine(out.s1, stats_combine(out.sq3, s4));
     }
     uint32_t idx = kNoCand;
     for (uint32_t j = 0; j < P; ++j)
@@ -692,6 +722,51 @@ __host__ __device__ __forceinline__ uint64_t sub_mid(const EntBatchDev& b, const
     if (!b.spec) return b.mids[F.sub_base + k];
     const u32x4 v = sub_rec(b, F, k)[2];
     return static_cast<uint64_t>(v.z) | static_cast<uint64_t>(v.w) << 32;
+}
+// Speculative sync only: the quarter states and statistics (CandRec).
+__host__ __device__ __forceinline__ uint64_t sub_q1(const EntBatchDev& b, const EntFrame& F, uint32_t k)
+{
+    const u32x4 v = sub_rec(b, F, k)[3];
+    return static_cast<uint64_t>(v.z) | static_cast<uint64_t>(v.w) << 32;
+}
+__host__ __device__ __forceinline__ uint64_t sub_q3(const EntBatchDev& b, const EntFrame& F, uint32_t k)
+{
+    const u32x4 v = sub_rec(b, F, k)[6];
+    return static_cast<uint64_t>(v.x) | static_cast<uint64_t>(v.y) << 32;
+}
+__host__ __device__ __forceinline__ SubStats sub_sq1(const EntBatchDev& b, const EntFrame& F, uint32_t k)
+{
+    return stats_of(sub_rec(b, F, k)[4]);
+}
+__host__ __device__ __forceinline__ SubStats sub_sq3(const EntBatchDev& b, const EntFrame& F, uint32_t k)
+{
+    return stats_of(sub_rec(b, F, k)[5]);
+}
+// Piece p of the write kernel's split of subsequence k (pieces: 2 halves, or
+// 4 quarters under the speculative sync): its entry state, its stop, and the
+// statistics from k's entry to that state.
+__host__ __device__ __forceinline__ uint32_t write_pieces(const EntBatchDev& b) { return b.spec ? 4u : 2u; }
+__host__ __device__ __forceinline__ uint64_t piece_entry(const EntBatchDev& b, const EntFrame& F, uint32_t k,
+                                                        uint32_t p, SubStats& pre)
+{
+    pre = stats_identity();
+    if (p == 0) return sub_entry(b, F, k);
+    if (!b.spec) {
+        pre = sub_stats1(b, F, k);
+        return sub_mid(b, F, k);
+    }
+    if (p == 1) {
+        pre = sub_sq1(b, F, k);
+        return sub_q1(b, F, k);
+    }
+    pre = sub_stats1(b, F, k);
+    if (p == 2) return sub_mid(b, F, k);
+    pre = stats_combine(pre, sub_sq3(b, F, k));
+    return sub_q3(b, F, k);
+}
+__host__ __device__ __forceinline__ uint32_t piece_stop(const EntBatchDev& b, uint32_t k, uint32_t p)
+{
+    return quarter_stop(k, b.sub_bits, (p + 1) * (4 / write_pieces(b)));
 }
 
 // ---------------------------------------------------------------------------
@@ -1157,9 +1232,9 @@ __global__ __launch_bounds__(kChainThreads) void ent_chain_kernel(EntBatchDev b)
     const int tid = threadIdx.x;
     const uint32_t f = blockIdx.x;
     const EntFrame F = b.frames[f];
-    // the chain kernels ran every chunk in parallel; walk serially only a frame
-    // where the chain leaves its slots (the repairs need the order)
-    const uint32_t n = b.chain_broken && b.chain_broken[f] == 0 ? 0u : F.nsub;
+    // the look-back kernel ran every chunk in parallel; walk serially only a
+    // frame where the chain leaves its slots (the repairs need the order)
+    const uint32_t n = b.chain_broken && b.chain_broken[f] != b.chain_epoch ? 0u : F.nsub;
     uint8_t* cm = b.cmap + static_cast<uint64_t>(F.sub_base) * kSlotRow;
     if (tid == 0) {
         L.carry = 0;
@@ -1207,47 +1282,61 @@ __global__ __launch_bounds__(kChainThreads) void ent_chain_kernel(EntBatchDev b)
         __syncthreads();
         if (r0 < cn && (r0 + kChainRows >= cn)) L.carry = s;   // the thread holding the chunk's last row
     }
-    if (b.chain_broken) return;   // ent_chain_agg_kernel reduces the groups, all in parallel
+    if (n == 0) return;   // not walked: the look-back kernel's group statistics stand
     __syncthreads();
     const int wv = tid >> 6, lane = tid & 63;
-    for (uint32_t g = wv; g < frame_groups(F.nsub); g += kChainThreads / 64) group_agg(b, F, g, lane);
+    for (uint32_t g = wv; g < frame_groups(F.nsub); g += kChainThreads / 64) {
+        group_agg(b, F, g, lane);
+        if (b.agg2 && lane == 0) b.agg2[F.wg_base + g] = stats_identity();
+    }
 }
 
 // ---- the chain, chunks in parallel (the case without repairs) -----------------
 // ent_chain_kernel's walk takes its chunks one after another (~20 us each; a
 // lone FHD frame has four).  Where no repair is needed the chunks are
-// independent given their entering slot, so two kernels over (chunk, frame)
-// run them side by side: ent_chain_fn_kernel composes each chunk's maps into
-// one function (chainfn); ent_chain_scan_kernel enters chunk c at the slot that
-// the functions of chunks 0 .. c-1 give slot 0, scans as the walk does and
-// writes its rows' slots.  A chunk that finds the chain leaving every slot
-// marks its frame (chain_broken), and ent_chain_kernel then walks that frame
-// serially with its repairs, overwriting the slots; it skips every other
-// frame's walk.  Same functions, same compositions: the same slots.
+// independent given their entering slot, so one kernel over (chunk, frame)
+// runs them side by side with a decoupled look-back: every chunk composes its
+// maps into one function (the scan), then thread 0 waits for its predecessor's
+// exit slot (a look-back word tagged with the launch's epoch, so nothing is
+// cleared between launches), publishes its own exit -- the only serial part --
+// and the chunk writes its rows' slots.  A chunk whose predecessor has not
+// published yet was dispatched after it (lower blockIdx.x first), so the wait
+// ends.  Each chunk then reduces the chain statistics of the groups it holds:
+// a group's part in its first chunk into agg, its part in the next into agg2
+// (so no chunk waits for another's slots).  A chunk that finds the chain
+// leaving every slot marks its frame (chain_broken = epoch), and
+// ent_chain_kernel then walks that frame serially with its repairs,
+// overwriting the slots and the group statistics; it skips every other frame.
 struct ChainParLds {
     uint32_t rows[kChainChunk][kRowWords];
     uint32_t fn[2][kChainThreads][kRowWords];
+    uint8_t slots[kChainChunk];   // the chain's slot of each row
     uint32_t carry, broken;
 };
 
-__global__ __launch_bounds__(kChainThreads) void ent_chain_fn_kernel(EntBatchDev b)
+// Ordered reduction (one wave) of the chain statistics of subsequences
+// [lo, hi) of frame F (hi - lo <= 256), slots from LDS (row k at slots[k - c0]).
+__device__ __forceinline__ SubStats range_stats(const EntBatchDev& b, const EntFrame& F, uint32_t lo, uint32_t hi,
+                                                const uint8_t* slots, uint32_t c0, int lane)
 {
-    __shared__ ChainParLds L;
-    const int tid = threadIdx.x;
-    const uint32_t c = blockIdx.x, f = blockIdx.y;
-    const EntFrame F = b.frames[f];
-    if (c == 0 && tid == 0) b.chain_broken[f] = 0;
-    const uint32_t c0 = c * kChainChunk;
-    if (c0 >= F.nsub) return;
-    const uint32_t cn = F.nsub - c0 < static_cast<uint32_t>(kChainChunk) ? F.nsub - c0 : kChainChunk;
-    chunk_load(L.rows, b.cmap + static_cast<uint64_t>(F.sub_base) * kSlotRow, c0, cn, tid);
-    __syncthreads();
-    const int cur = chunk_scan(L.rows, L.fn, cn, tid);
-    if (tid < kRowWords)   // the last thread's inclusive function: the whole chunk
-        b.chainfn[(static_cast<uint64_t>(f) * b.chain_chunks + c) * kRowWords + tid] = L.fn[cur][kChainThreads - 1][tid];
+    SubStats q[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {   // the four loads in flight together
+        const uint32_t k = lo + static_cast<uint32_t>(lane) * 4 + i;
+        if (k < hi) {
+            const uint64_t row = static_cast<uint64_t>(F.sub_base) + k;
+            q[i] = stats_of(reinterpret_cast<const u32x4*>(b.cand + row * kCandRow + slots[k - c0])[1]);
+        } else {
+            q[i] = stats_identity();
+        }
+    }
+    SubStats a = stats_identity();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a = stats_combine(a, q[i]);
+    return wave_reduce_ordered(a, lane);
 }
 
-__global__ __launch_bounds__(kChainThreads) void ent_chain_scan_kernel(EntBatchDev b)
+__global__ __launch_bounds__(kChainThreads) void ent_chain_lb_kernel(EntBatchDev b)
 {
     __shared__ ChainParLds L;
     const int tid = threadIdx.x;
@@ -1256,41 +1345,62 @@ __global__ __launch_bounds__(kChainThreads) void ent_chain_scan_kernel(EntBatchD
     const uint32_t n = F.nsub, c0 = c * kChainChunk;
     if (c0 >= n) return;
     const uint32_t cn = n - c0 < static_cast<uint32_t>(kChainChunk) ? n - c0 : kChainChunk;
-    if (tid == 0) {   // the slot entering this chunk: slot 0 through chunks 0 .. c-1
-        uint32_t s = 0;
-        for (uint32_t i = 0; i < c && s != kNoCand; ++i)
-            s = row_get(row_load(b.chainfn + (static_cast<uint64_t>(f) * b.chain_chunks + i) * kRowWords), s);
-        L.carry = s;
-        L.broken = 0;
-    }
+    if (tid == 0) L.broken = 0;
     chunk_load(L.rows, b.cmap + static_cast<uint64_t>(F.sub_base) * kSlotRow, c0, cn, tid);
     __syncthreads();
     const int cur = chunk_scan(L.rows, L.fn, cn, tid);
+    if (tid == 0) {   // look-back: the slot entering this chunk, then this chunk's exit
+        uint32_t* word = b.chainfn + (static_cast<uint64_t>(f) * b.chain_chunks + c) * kRowWords;
+        uint32_t carry = 0;
+        if (c > 0) {
+            uint32_t v;
+            while (((v = __hip_atomic_load(word - kRowWords, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) >> 8) !=
+                   b.chain_epoch)
+                __builtin_amdgcn_s_sleep(1);
+            carry = v & 0xFFu;
+        }
+        const uint32_t exit = carry == kNoCand ? kNoCand : row_get(row_load(L.fn[cur][kChainThreads - 1]), carry);
+        __hip_atomic_store(word, (b.chain_epoch << 8) | exit, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        L.carry = carry;
+    }
+    __syncthreads();
     const uint32_t carry = L.carry;
     const uint32_t slot = tid == 0 ? carry : (carry == kNoCand ? kNoCand : row_get(row_load(L.fn[cur][tid - 1]), carry));
     // a row whose map sends the chain's slot to none, before the frame's last
     // subsequence: the serial walk repairs it (chunks after it enter at none)
     const uint32_t r0 = static_cast<uint32_t>(tid) * kChainRows;
     uint32_t s = slot;
-    for (uint32_t r = r0; r < r0 + kChainRows && r < cn && s != kNoCand; ++r) {
+    for (uint32_t r = r0; r < r0 + kChainRows && r < cn; ++r) {
+        L.slots[r] = static_cast<uint8_t>(s);
+        if (s == kNoCand) continue;
         const uint32_t nx = row_get(row_load(L.rows[r]), s);
         if (nx == kNoCand && c0 + r + 1 < n) L.broken = 1;
         s = nx;
     }
     chunk_write_slots(L.rows, b.cslot, F.sub_base + c0, cn, tid, slot);
     __syncthreads();
-    if (tid == 0 && L.broken) b.chain_broken[f] = 1;
-}
-
-// Every group of the batch, one wave each (after the chain's slots are final).
-__global__ __launch_bounds__(kChainThreads) void ent_chain_agg_kernel(EntBatchDev b)
-{
-    const int lane = threadIdx.x & 63;
-    const uint32_t w = blockIdx.x * (kChainThreads / 64) + (threadIdx.x >> 6);
-    if (w >= b.nwg) return;
-    const EntFrame F = b.frames[b.wg_frame[w]];
-    const uint32_t g = w - F.wg_base;
-    if (g < frame_groups(F.nsub)) group_agg(b, F, g, lane);
+    if (L.broken || carry == kNoCand) {   // broken here or before: the walk redoes this frame
+        if (tid == 0 && L.broken) b.chain_broken[f] = b.chain_epoch;
+        return;
+    }
+    // group statistics: each group part in this chunk, one wave per part
+    const int wv = tid >> 6, lane = tid & 63;
+    const uint32_t g0 = c0 / kOwn, g1 = (c0 + cn - 1) / kOwn;
+    for (uint32_t g = g0 + static_cast<uint32_t>(wv); g <= g1; g += kChainThreads / 64) {
+        const uint32_t glo = g * kOwn, ghi = (g + 1) * kOwn < n ? (g + 1) * kOwn : n;
+        const uint32_t lo = glo > c0 ? glo : c0, hi = ghi < c0 + cn ? ghi : c0 + cn;
+        const SubStats a = range_stats(b, F, lo, hi, L.slots, c0, lane);
+        if (lane == 0) {
+            const uint32_t w = F.wg_base + g;
+            if (glo >= c0) {   // the group starts here
+                b.agg[w] = a;
+                b.linked[w] = 1u;
+                if (ghi <= c0 + cn) b.agg2[w] = stats_identity();
+            } else {
+                b.agg2[w] = a;
+            }
+        }
+    }
 }
 
 __global__ __launch_bounds__(256) void ent_link_kernel(EntBatchDev b)
@@ -1374,38 +1484,44 @@ __global__ __launch_bounds__(64) void ent_fallback_kernel(EntBatchDev b)
     if (lane == 0) repair_frame(b, f, tabs, blocks);
 }
 
-// Two threads per subsequence: thread t decodes the first half of group
-// subsequence t (entry -> the recorded mid-state), thread t + 256 the second
-// (mid-state -> end), so each serial chain is S/2 bits long while the sync
-// kernel keeps its S (the sync kernel is fastest at S = 4096,
-// writing at 2048).  A run that starts inside a block skips to the next DC unit
-// and a run finishes the block it started past its stop, so the halves write
-// disjoint blocks; the second half's block index and DC predictors are the
-// subsequence's prefix combined with the first half's statistics.
-constexpr int kWriteThreads = 2 * kGroupSubs;
+// Several threads per subsequence (write_pieces: halves, or quarters under the
+// speculative sync, which records the quarter states): in workgroup (w, p)
+// thread t decodes piece p of group subsequence t (from the state recorded at
+// the piece's start to the next piece's), so each serial chain is S/2 or S/4
+// bits long while the sync kernel keeps its S (the sync kernel
+// is fastest at S = 4096, writing at 2048).  A run that starts inside a block
+// skips to the next DC unit and a run finishes the block it started past its
+// stop, so the pieces write disjoint blocks; a piece's block index and DC
+// predictors are the subsequence's prefix combined with the statistics up to
+// the piece's start.  The pieces are separate 256-thread workgroups: more CUs
+// for a lone frame's few groups, one wave per SIMD.
+constexpr int kWriteThreads = kGroupSubs;
 
 __global__ __launch_bounds__(kWriteThreads) void ent_write_kernel(EntBatchDev b)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    int16_t* stage = reinterpret_cast<int16_t*>(smem);                                  // [512][kStageStride]
+    int16_t* stage = reinterpret_cast<int16_t*>(smem);                                  // [256][kStageStride]
     HuffLut* tabs = reinterpret_cast<HuffLut*>(smem + sizeof(int16_t) * kWriteThreads * kStageStride);
     SubStats* buf = reinterpret_cast<SubStats*>(stage);   // scan scratch before any block is staged
     static_assert(sizeof(SubStats) * kWriteThreads <= sizeof(int16_t) * kWriteThreads * kStageStride, "scratch");
     const int tid = threadIdx.x;
-    const int t = tid & (kGroupSubs - 1);
-    const bool second = tid >= kGroupSubs;
+    const int t = tid;
+    const uint32_t piece = blockIdx.y;
     const uint32_t w = blockIdx.x;
     const uint32_t f = b.wg_frame[w];
     const EntFrame F = b.frames[f];
     const uint32_t gl = w - F.wg_base;
-    const uint32_t S = b.sub_bits;
-    if (gl >= frame_groups(F.nsub)) return;
+    if (gl >= frame_groups(F.nsub) || piece >= write_pieces(b)) return;
     __shared__ BlockInfo blocks[kMaxBpm];
     load_tables(tabs, blocks, b.tabs + F.tab_base, F, b.frames + f, tid, kWriteThreads);
     // block index / DC predictors at this group's start: all previous groups of the frame
     SubStats pre = stats_identity();
     for (uint32_t base = 0; base < gl; base += kWriteThreads) {
-        const SubStats v = base + tid < gl ? b.agg[F.wg_base + base + tid] : stats_identity();
+        SubStats v = stats_identity();
+        if (base + tid < gl) {
+            v = b.agg[F.wg_base + base + tid];
+            if (b.agg2) v = stats_combine(v, b.agg2[F.wg_base + base + tid]);
+        }
         block_scan_inclusive<kWriteThreads>(v, buf, tid);
         const SubStats total = buf[kWriteThreads - 1];
         __syncthreads();
@@ -1414,19 +1530,16 @@ __global__ __launch_bounds__(kWriteThreads) void ent_write_kernel(EntBatchDev b)
     const int64_t k = group_sub(gl, t);
     const bool own = t >= kWarm && k < static_cast<int64_t>(F.nsub);
     const uint32_t ku = static_cast<uint32_t>(k);
-    // subsequence prefixes (the upper 256 entries are identities and do not disturb them)
-    const SubStats mine = own && !second ? sub_stats(b, F, ku) : stats_identity();
+    // subsequence prefixes
+    const SubStats mine = own ? sub_stats(b, F, ku) : stats_identity();
     block_scan_inclusive<kWriteThreads>(mine, buf, tid);
     SubStats excl = stats_combine(pre, t > 0 ? buf[t - 1] : stats_identity());
     __syncthreads();   // scratch reads done before blocks are staged
     if (!own) return;
-    uint64_t entry = sub_entry(b, F, ku);
-    uint32_t stop = ku * S + S / 2;
-    if (second) {
-        excl = stats_combine(excl, sub_stats1(b, F, ku));
-        entry = sub_mid(b, F, ku);
-        stop = (ku + 1) * S;
-    }
+    SubStats lead;
+    const uint64_t entry = piece_entry(b, F, ku, piece, lead);
+    excl = stats_combine(excl, lead);
+    const uint32_t stop = piece_stop(b, ku, piece);
     const RunCtx c = make_ctx(b, F, tabs, blocks);
     RunOut o;
     o.coefs = b.coefs + F.coef_off * 64;
@@ -1440,7 +1553,7 @@ __global__ __launch_bounds__(kWriteThreads) void ent_write_kernel(EntBatchDev b)
     SubStats st = stats_identity();
     run<true>(c, entry, stop, st, &o);
     uint32_t bad = (st.flags & kError) ? kStatusCorrupt : 0;
-    if (second && ku == F.nsub - 1 && excl.nblk + st.nblk != F.nblocks) bad |= kStatusCount;
+    if (piece + 1 == write_pieces(b) && ku == F.nsub - 1 && excl.nblk + st.nblk != F.nblocks) bad |= kStatusCount;
     if (bad) atomicOr(&b.status[f], bad);
 }
 
@@ -1831,6 +1944,51 @@ void emulate_spec_sync(const EntBatchDev& b)
                 }
             fprintf(stderr, "chain: nsub %u repairs %d; level-0 candidates -> spec %d, overflow %d, none %d\n", n,
                     nrepair, novf[0], novf[1], novf[kOvfLevels + 1]);
+            int chain_ovf = 0;   // subsequences the verified chain enters through an overflow slot
+            for (uint32_t k = 0; k < n; ++k) chain_ovf += b.cslot[F.sub_base + k] >= F.bpm;
+            fprintf(stderr, "chain: %d subsequences entered through an overflow or repair slot\n", chain_ovf);
+            // ent_cand_kernel's serial bits per thread (k, c) and per wave (64 lanes of one c)
+            std::vector<uint32_t> cost, wmax;
+            uint32_t nlev[kOvfLevels + 1] = {}, nmiss = 0;
+            for (uint32_t g = 0; g < frame_groups(n); ++g)
+                for (uint32_t c0 = 0; c0 < F.bpm; ++c0)
+                    for (int wv = 0; wv < kGroupSubs / 64; ++wv) {
+                        uint32_t wm = 0;
+                        for (int l = 0; l < 64; ++l) {
+                            const int t = wv * 64 + l;
+                            const int64_t k0 = group_sub(g, t);
+                            if (t < kWarm || k0 >= static_cast<int64_t>(n)) continue;
+                            uint32_t kk = static_cast<uint32_t>(k0), slot = c0, bits = 0;
+                            for (int level = 0;; ++level) {
+                                const uint64_t row = static_cast<uint64_t>(F.sub_base) + kk;
+                                const CandRec& r = b.cand[row * kCandRow + slot];
+                                bits += st_pos(r.mid) - st_pos(r.e);
+                                bool hit = false;
+                                for (uint32_t j = 0; j < F.bpm; ++j) hit |= same_state(r.mid, b.spec[row * kMaxBpm + j].cp);
+                                if (!hit) {
+                                    bits += st_pos(r.y) - st_pos(r.mid);
+                                    ++nmiss;
+                                }
+                                const uint32_t nx = b.cmap[row * kSlotRow + slot];
+                                if (nx == kNoCand || nx < F.bpm || level == kOvfLevels || kk + 1 >= n) {
+                                    ++nlev[level];
+                                    break;
+                                }
+                                slot = nx;
+                                ++kk;
+                            }
+                            cost.push_back(bits);
+                            wm = std::max(wm, bits);
+                        }
+                        if (wm) wmax.push_back(wm);
+                    }
+            auto pct = [](std::vector<uint32_t> v, double q) {
+                std::sort(v.begin(), v.end());
+                return v.empty() ? 0u : v[static_cast<size_t>(q * (v.size() - 1))];
+            };
+            fprintf(stderr, "cand threads %zu: levels %u/%u/%u, mid misses %u; bits p50 %u p90 %u p99 %u max %u; "
+                    "wave max p50 %u p90 %u max %u\n", cost.size(), nlev[0], nlev[1], nlev[2], nmiss, pct(cost, 0.5),
+                    pct(cost, 0.9), pct(cost, 0.99), pct(cost, 1.0), pct(wmax, 0.5), pct(wmax, 0.9), pct(wmax, 1.0));
         }
         for (uint32_t g = 0; g < frame_groups(n); ++g) {
             const uint32_t w = F.wg_base + g;
@@ -1963,8 +2121,10 @@ void emulate(const EntBatchDev& b)
         const RunCtx c = make_ctx(b, F, b.tabs + F.tab_base, blocks);
         SubStats pre = stats_identity();
         for (uint32_t i = 0; i < F.nsub; ++i) {
-            for (int half = 0; half < 2; ++half) {   // as ent_write_kernel: entry -> mid, mid -> end
-                const SubStats p = half ? stats_combine(pre, sub_stats1(b, F, i)) : pre;
+            for (uint32_t piece = 0; piece < write_pieces(b); ++piece) {   // as ent_write_kernel
+                SubStats lead;
+                const uint64_t entry = piece_entry(b, F, i, piece, lead);
+                const SubStats p = stats_combine(pre, lead);
                 RunOut o;
                 o.coefs = b.coefs + F.coef_off * 64;
                 o.stage = stage;
@@ -1975,10 +2135,10 @@ void emulate(const EntBatchDev& b)
                 o.pred[1] = p.dc[1];
                 o.pred[2] = p.dc[2];
                 SubStats s = stats_identity();
-                run<true>(c, half ? sub_mid(b, F, i) : sub_entry(b, F, i),
-                          half ? (i + 1) * S : i * S + S / 2, s, &o);
+                run<true>(c, entry, piece_stop(b, i, piece), s, &o);
                 if (s.flags & kError) b.status[f] |= kStatusCorrupt;
-                if (half && i == F.nsub - 1 && p.nblk + s.nblk != F.nblocks) b.status[f] |= kStatusCount;
+                if (piece + 1 == write_pieces(b) && i == F.nsub - 1 && p.nblk + s.nblk != F.nblocks)
+                    b.status[f] |= kStatusCount;
             }
             pre = stats_combine(pre, sub_stats(b, F, i));
         }
@@ -2012,8 +2172,7 @@ struct hjd_gdec {
     uint64_t* d_wentries = nullptr;
     uint32_t* d_linked = nullptr;
     SubStats* d_agg = nullptr;
-    uint32_t* d_status = nullptr;
-    uint32_t* h_status = nullptr;       // pinned
+    uint32_t* h_status = nullptr;       // pinned; the device's status words are in the batch header (H.status)
     int16_t* d_coefs = nullptr;
     uint8_t* d_raw = nullptr;           // raw scan bytes of device-destuffed frames (same offsets as the data area)
     uint32_t* d_tiles = nullptr;        // destuff scratch [3][max_tiles]
@@ -2024,8 +2183,13 @@ struct hjd_gdec {
     uint8_t* d_cslot = nullptr;
     uint32_t* d_chainfn = nullptr;
     uint32_t* d_chain_broken = nullptr;
+    SubStats* d_agg2 = nullptr;         // [group] (ent_chain_lb_kernel)
+    uint32_t chain_epoch = 0;           // the last launch's look-back tag
     int64_t chain_fn_rows = 0;      // capacity of d_chainfn in chunk functions
     uint8_t* d_steps = nullptr;         // [table][1 << kStepBits] (ent_steps_kernel)
+    std::vector<uint8_t> steps_tabs;    // the tables d_steps was last derived from (host copy, batch order)
+    double host_us[3] = {0, 0, 0};      // host time per phase (wait for staging, stage, issue): HJD_GDEC_HOST_TIMES
+    int64_t host_calls = 0;
     hipEvent_t staged = nullptr, done = nullptr;
     int64_t last_h2d = 0;               // bytes the last issue moved host -> device
     int64_t last_host_scan_bytes = 0;   // scan bytes the host CPU read + wrote for the staged frames
@@ -2252,11 +2416,14 @@ int hjd_gdec::assemble(uint8_t* blob, int16_t* coefs, int64_t* block_offsets, vo
             ntiles += (raw_region_len(static_cast<uint32_t>(p.raw_off & 15), p.raw_len) + kTileBytes - 1) / kTileBytes;
     o.rawf = align_up(o.qt + (d_outs ? 192 * 4 * static_cast<size_t>(n) : 0), kAlign);
     o.tilef = align_up(o.rawf + (ntiles ? sizeof(RawFrame) * ne : 0), kAlign);
-    o.used = align_up(o.tilef + 4 * ntiles, kAlign);
+    // per entropy frame status words, zero in the header's upload (no memset)
+    o.status = align_up(o.tilef + 4 * ntiles, kAlign);
+    o.used = align_up(o.status + 4 * static_cast<size_t>(ne), kAlign);
     if (o.used > caps.hdr_cap || ntiles > static_cast<size_t>(caps.max_tiles))
         return set_error(HJD_E_INVALID, "batch header exceeds its capacity");
 
     EntFrame* ef = reinterpret_cast<EntFrame*>(h_stage + o.frames);
+    memset(h_stage + o.status, 0, 4 * static_cast<size_t>(ne));
     HuffLut* tb = reinterpret_cast<HuffLut*>(h_stage + o.tabs);
     uint32_t* seg = reinterpret_cast<uint32_t*>(h_stage + o.seg);
     uint32_t* wgf = reinterpret_cast<uint32_t*>(h_stage + o.wg);
@@ -2347,6 +2514,8 @@ int hjd_gdec::assemble(uint8_t* blob, int16_t* coefs, int64_t* block_offsets, vo
     if (d.chain_chunks == 0) d.chain_chunks = 1;
     d.chainfn = nullptr;
     d.chain_broken = nullptr;
+    d.chain_epoch = 0;
+    d.agg2 = nullptr;
     d.spec = nullptr;
     d.cand = nullptr;
     d.cmap = nullptr;
@@ -2410,7 +2579,6 @@ int gdec_alloc(hjd_gdec* g)
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_wentries), 8 * kWarm * static_cast<size_t>(g->caps.max_wgs)));
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_linked), 4 * static_cast<size_t>(g->caps.max_wgs)));
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_agg), sizeof(SubStats) * static_cast<size_t>(g->caps.max_wgs)));
-    HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_status), 4 * kMaxScans * static_cast<size_t>(g->caps.max_frames)));
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_coefs), 128 * static_cast<size_t>(g->caps.max_blocks)));
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_raw), g->data_cap()));
     HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_tiles), 12 * static_cast<size_t>(g->caps.max_tiles)));
@@ -2427,6 +2595,9 @@ int gdec_alloc(hjd_gdec* g)
         g->chain_fn_rows = static_cast<int64_t>(ef * (n / kChainChunk + 1));
         HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_chainfn), 4 * kRowWords * static_cast<size_t>(g->chain_fn_rows)));
         HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_chain_broken), 4 * ef));
+        HJD_HIP(hipMemset(g->d_chain_broken, 0, 4 * ef));
+        HJD_HIP(hipMemset(g->d_chainfn, 0, 4 * kRowWords * static_cast<size_t>(g->chain_fn_rows)));
+        HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_agg2), sizeof(SubStats) * static_cast<size_t>(g->caps.max_wgs)));
     }
     HJD_HIP(hipEventCreateWithFlags(&g->staged, hipEventDisableTiming));
     HJD_HIP(hipEventCreateWithFlags(&g->done, hipEventDisableTiming));
@@ -2437,7 +2608,6 @@ int gdec_alloc(hjd_gdec* g)
 int launch_entropy(hjd_gdec* g, const EntBatchDev& b, hipStream_t s)
 {
     if (b.nwg == 0) return HJD_OK;
-    HJD_HIP(hipMemsetAsync(g->d_status, 0, 4 * static_cast<size_t>(b.nframes), s));
     if (b.ntiles) {
         hipLaunchKernelGGL(destuff_count_kernel, dim3(b.ntiles), dim3(kTileThreads), 0, s, b);
         HJD_HIP(hipGetLastError());
@@ -2446,27 +2616,27 @@ int launch_entropy(hjd_gdec* g, const EntBatchDev& b, hipStream_t s)
         hipLaunchKernelGGL(destuff_write_kernel, dim3(b.ntiles), dim3(kTileThreads), 0, s, b);
         HJD_HIP(hipGetLastError());
     }
-    hipLaunchKernelGGL(ent_steps_kernel, dim3(b.ntab_total, kStepGroups), dim3(kStepsThreads), 0, s, b);
-    HJD_HIP(hipGetLastError());
+    // the step tables depend on the Huffman tables only: a batch whose tables
+    // (in batch order) are the previous batch's reuses them
+    const uint8_t* tabs_h = g->h_stage + g->H.tabs;
+    const size_t tabs_n = sizeof(HuffLut) * b.ntab_total;
+    if (g->steps_tabs.size() != tabs_n || memcmp(g->steps_tabs.data(), tabs_h, tabs_n) != 0) {
+        hipLaunchKernelGGL(ent_steps_kernel, dim3(b.ntab_total, kStepGroups), dim3(kStepsThreads), 0, s, b);
+        HJD_HIP(hipGetLastError());
+        g->steps_tabs.assign(tabs_h, tabs_h + tabs_n);
+    }
     if (b.spec) {   // speculative sync: latency decoders
         const size_t tl = (sizeof(HuffLut) + (1u << kStepBits)) * b.ntab_max;
         hipLaunchKernelGGL(ent_spec_kernel, dim3(b.nwg, kMaxBpm), dim3(kGroupSubs), tl, s, b);
         HJD_HIP(hipGetLastError());
         hipLaunchKernelGGL(ent_cand_kernel, dim3(b.nwg, kMaxBpm), dim3(kGroupSubs), tl, s, b);
         HJD_HIP(hipGetLastError());
-        if (b.chain_broken) {   // chunks in parallel; the walk below then only repairs
-            hipLaunchKernelGGL(ent_chain_fn_kernel, dim3(b.chain_chunks, b.nframes), dim3(kChainThreads), 0, s, b);
-            HJD_HIP(hipGetLastError());
-            hipLaunchKernelGGL(ent_chain_scan_kernel, dim3(b.chain_chunks, b.nframes), dim3(kChainThreads), 0, s, b);
+        if (b.chain_broken) {   // chunks in parallel (+ group records); the walk below then only repairs
+            hipLaunchKernelGGL(ent_chain_lb_kernel, dim3(b.chain_chunks, b.nframes), dim3(kChainThreads), 0, s, b);
             HJD_HIP(hipGetLastError());
         }
         hipLaunchKernelGGL(ent_chain_kernel, dim3(b.nframes), dim3(kChainThreads), 0, s, b);   // + group records
         HJD_HIP(hipGetLastError());
-        if (b.chain_broken) {
-            hipLaunchKernelGGL(ent_chain_agg_kernel, dim3((b.nwg + kChainThreads / 64 - 1) / (kChainThreads / 64)),
-                               dim3(kChainThreads), 0, s, b);
-            HJD_HIP(hipGetLastError());
-        }
     } else {
         hipLaunchKernelGGL(ent_sync_kernel, dim3(b.nwg), dim3(kGroupSubs), sync_lds_bytes(b.ntab_max), s, b);
         HJD_HIP(hipGetLastError());
@@ -2478,8 +2648,8 @@ int launch_entropy(hjd_gdec* g, const EntBatchDev& b, hipStream_t s)
         HJD_HIP(hipGetLastError());
     }
     constexpr size_t kStageBytes = sizeof(int16_t) * kWriteThreads * kStageStride;
-    hipLaunchKernelGGL(ent_write_kernel, dim3(b.nwg), dim3(kWriteThreads), kStageBytes + sizeof(HuffLut) * b.ntab_max,
-                       s, b);
+    hipLaunchKernelGGL(ent_write_kernel, dim3(b.nwg, write_pieces(b)), dim3(kWriteThreads),
+                       kStageBytes + sizeof(HuffLut) * b.ntab_max, s, b);
     HJD_HIP(hipGetLastError());
     return HJD_OK;
 }
@@ -2508,7 +2678,7 @@ int gdec_issue(hjd_gdec* g, void* const* d_outs, const int32_t* pitches, int16_t
     b.wentries = g->d_wentries;
     b.linked = g->d_linked;
     b.agg = g->d_agg;
-    b.status = g->d_status;
+    b.status = reinterpret_cast<uint32_t*>(g->d_blob + g->H.status);
     b.raw = g->d_raw;
     b.tiles = g->d_tiles;
     b.steps_g = g->d_steps;
@@ -2521,6 +2691,9 @@ int gdec_issue(hjd_gdec* g, void* const* d_outs, const int32_t* pitches, int16_t
         if (static_cast<int64_t>(b.chain_chunks) * b.nframes <= g->chain_fn_rows) {
             b.chainfn = g->d_chainfn;
             b.chain_broken = g->d_chain_broken;
+            b.agg2 = g->d_agg2;
+            g->chain_epoch = g->chain_epoch % 0xFFFFFFu + 1u;   // 1 .. 2^24 - 1
+            b.chain_epoch = g->chain_epoch;
         }
     }
     // the device buffers are reused: order this call after the previous one
@@ -2633,7 +2806,7 @@ int gdec_issue(hjd_gdec* g, void* const* d_outs, const int32_t* pitches, int16_t
                                      static_cast<size_t>(host[i].height), hipMemcpyDeviceToHost, s));
         }
     }
-    HJD_HIP(hipMemcpyAsync(g->h_status, g->d_status, 4 * static_cast<size_t>(b.nframes), hipMemcpyDeviceToHost, s));
+    HJD_HIP(hipMemcpyAsync(g->h_status, b.status, 4 * static_cast<size_t>(b.nframes), hipMemcpyDeviceToHost, s));
     HJD_HIP(hipEventRecord(g->done, s));
     g->nframes_issued = n;
     return HJD_OK;
@@ -2644,12 +2817,20 @@ int gdec_run(hjd_gdec* g, const uint8_t* const* datas, const size_t* sizes, int 
              const int32_t* pitches, int16_t* coefs_out, int64_t* block_offsets, hipStream_t s)
 {
     if (!g || !g->gpu || !datas || !sizes) return set_error(HJD_E_INVALID, "NULL argument");
+    const auto t0 = std::chrono::steady_clock::now();
     int rc = g->wait_staging();
     if (rc) return rc;
+    const auto t1 = std::chrono::steady_clock::now();
     rc = g->stage_frames(datas, sizes, n);
     if (rc) return rc;
+    const auto t2 = std::chrono::steady_clock::now();
     rc = gdec_issue(g, d_outs, pitches, coefs_out, block_offsets, s);
     if (rc) return rc;
+    const auto t3 = std::chrono::steady_clock::now();
+    g->host_us[0] += std::chrono::duration<double, std::micro>(t1 - t0).count();
+    g->host_us[1] += std::chrono::duration<double, std::micro>(t2 - t1).count();
+    g->host_us[2] += std::chrono::duration<double, std::micro>(t3 - t2).count();
+    ++g->host_calls;
     // The caller may reuse its bytes once this returns (include/hjd_host.h):
     // scans read by DMA straight from the caller's pinned memory must have
     // landed first.  Only the uploads are waited for, not the kernels.
@@ -2744,6 +2925,10 @@ int hjd_gdec_create(hjd_ctx* ctx, int max_frames, int64_t max_scan_bytes, int64_
 int hjd_gdec_destroy(hjd_gdec* g)
 {
     if (!g) return HJD_OK;
+    if (g->host_calls && getenv("HJD_GDEC_HOST_TIMES"))
+        fprintf(stderr, "hjd_gdec host us/call over %lld calls: wait_staging %.1f stage %.1f issue %.1f\n",
+                static_cast<long long>(g->host_calls), g->host_us[0] / g->host_calls, g->host_us[1] / g->host_calls,
+                g->host_us[2] / g->host_calls);
     if (!g->gpu) {
         free(g->h_stage);
         delete g;
@@ -2754,8 +2939,8 @@ int hjd_gdec_destroy(hjd_gdec* g)
     if (g->h_stage) (void)hipHostFree(g->h_stage);
     if (g->h_status) (void)hipHostFree(g->h_status);
     void* dev[] = {g->d_blob, g->d_entries, g->d_stats, g->d_mids, g->d_stats1, g->d_wentries, g->d_linked, g->d_agg,
-                   g->d_status, g->d_coefs, g->d_raw, g->d_tiles, g->d_spec, g->d_cand, g->d_cmap, g->d_cslot,
-                   g->d_steps, g->d_chainfn, g->d_chain_broken};
+                   g->d_coefs, g->d_raw, g->d_tiles, g->d_spec, g->d_cand, g->d_cmap, g->d_cslot,
+                   g->d_steps, g->d_chainfn, g->d_chain_broken, g->d_agg2};
     for (void* p : dev)
         if (p) (void)hipFree(p);
     if (g->staged) (void)hipEventDestroy(g->staged);

@@ -463,10 +463,19 @@ __host__ __device__ __forceinline__ uint32_t long_code_entry(const HuffLut& t, u
 // mode: and until the block this run owns is complete).  Accumulates `st`
 // (must start as the identity).  Returns the exit state.  Per-component sums
 // live in scalars (selects, not indexed arrays: no scratch on the device).
-template <bool kWrite>
+// kMarks > 0 (sync mode): the run also passes marks mpos[0] < mpos[1] ... <=
+// stop and records, at the first unit boundary >= each, the state (mstate)
+// and the statistics since the previous mark (mstats; `st` then holds those
+// after the last mark) -- exactly what separate runs split there would give,
+// without a window reload per piece.
+template <bool kWrite, int kMarks = 0>
 __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry, uint32_t stop, SubStats& st,
-                                                 RunOut* out)
+                                                 RunOut* out, const uint32_t* mpos = nullptr,
+                                                 uint64_t* mstate = nullptr, SubStats* mstats = nullptr)
 {
+    static_assert(!kWrite || kMarks == 0, "marks: sync mode only");
+    int mi = 0;
+    uint32_t lim = kMarks ? mpos[0] : stop;   // the next mark, then stop
     uint32_t pos = st_pos(entry);
     uint32_t z = st_z(entry);
     uint32_t j = st_j(entry);
@@ -519,7 +528,22 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
         // seek) measured 13% slower -- its extra exits cost more exec-mask
         // bookkeeping per unit than the merge copies.
         for (;;) {
-            if (pos >= stop && (!kWrite || !owned)) break;
+            if (pos >= lim && (!kWrite || !owned)) {
+                if (kMarks && mi < kMarks) {   // a mark: its state and the statistics since the last one
+                    mstate[mi] = pack_state(pos, j, z, seg);
+                    mstats[mi].nblk = static_cast<uint32_t>(nblk);
+                    mstats[mi].flags = flags;
+                    mstats[mi].dc[0] = d0;
+                    mstats[mi].dc[1] = d1;
+                    mstats[mi].dc[2] = d2;
+                    nblk = d0 = d1 = d2 = 0;
+                    flags = 0;
+                    ++mi;
+                    lim = mi < kMarks ? mpos[mi] : stop;
+                    continue;
+                }
+                break;
+            }
             const uint32_t nwi = pos >> 5;
             if (nwi != bw.wi) {
                 if (nwi == bw.wi + 1) bw.advance(c);
@@ -570,7 +594,7 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
                 const uint32_t nb = step_bits(se), za = step_zadv(se);
                 const bool ends = za == kStepEnds;
                 // an EOB entry's units before the EOB move z by <= 14: z <= 49 keeps them <= 63
-                if (se != 0 && z + (ends ? 14 : za) <= 63 && left >= static_cast<int32_t>(nb) + 8 && pos + nb <= stop) {
+                if (se != 0 && z + (ends ? 14 : za) <= 63 && left >= static_cast<int32_t>(nb) + 8 && pos + nb <= lim) {
                     pos += nb;
                     if (ends) {
                         z = 0;
@@ -660,6 +684,18 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
             }
         }
         if (!done) result = pack_state(pos, j, z, seg);
+    }
+    // marks the run did not reach (the data ended first): the exit state, and
+    // the statistics so far for the first of them (as separate runs would give)
+    for (; kMarks && mi < kMarks; ++mi) {
+        mstate[mi] = result;
+        mstats[mi].nblk = static_cast<uint32_t>(nblk);
+        mstats[mi].flags = flags;
+        mstats[mi].dc[0] = d0;
+        mstats[mi].dc[1] = d1;
+        mstats[mi].dc[2] = d2;
+        nblk = d0 = d1 = d2 = 0;
+        flags = 0;
     }
     st.nblk = static_cast<uint32_t>(nblk);
     st.dc[0] = d0;

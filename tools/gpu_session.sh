@@ -13,6 +13,8 @@
 #                                --workload <workload> --no-cpu --no-stream <args>;
 #                                ktrace:default traces the driver's own command (python bench.py)
 #   pmc:<workload>               HBM bytes: FETCH_SIZE / WRITE_SIZE passes (tools/pmc/traffic.txt)
+#   ent:<workload>[:<args>]      SQ counters of the entropy kernels (tools/pmc/entropy.txt)
+#   htrace:<workload>[:<variant>]  HIP API + kernel + copy trace (no counters) of bench.py --workload
 #   sq:<workload>[:<args>]       SQ counters of the fused kernel (tools/pmc/pixel.txt),
 #                                256 frames at the default launch shape
 #   ab:<variant>:<workload>:<rounds>[:<args>]
@@ -61,6 +63,21 @@ for step in "$@"; do
           --no-444 --no-fhd --detail-out "$O/pmc_$a1.detail.json" > "$O/pmc_$a1.json" 2> "$O/pmc_$a1.err") \
           || fail pmc "$O/pmc_$a1.err"
       tail -c 300 "$O/pmc_$a1.json" ;;
+    htrace)
+      # HIP API + kernel trace of bench.py --workload <a1> (a2: a build/variants library, or product)
+      if [ -n "${a2:-}" ] && [ "$a2" != product ]; then export HJD_LIB=$R/build/variants/$a2/libhjd.so; fi
+      (cd /tmp && timeout -k 10 300 rocprofv3 --hip-trace --kernel-trace --memory-copy-trace --output-format csv \
+          -d "$O/htrace_${a1}_${a2:-product}" -o ht -- python3 "$R/bench.py" --workload "$a1" --steps 40 --warmup 5 \
+          --no-cpu > "$O/htrace_${a1}_${a2:-product}.json" 2> "$O/htrace_${a1}_${a2:-product}.err") \
+          || fail htrace "$O/htrace_${a1}_${a2:-product}.err"
+      unset HJD_LIB
+      tail -c 300 "$O/htrace_${a1}_${a2:-product}.json" ;;
+    ent)
+      # SQ counters of the entropy kernels (tools/pmc/entropy.txt, two passes)
+      (cd /tmp && timeout -k 10 300 rocprofv3 -i "$R/tools/pmc/entropy.txt" --output-format csv -d "$O/ent_$a1" -o ent -- \
+          python3 "$R/bench.py" --workload "$a1" --steps 20 --warmup 3 --no-cpu ${a2//,/ } \
+          --detail-out "$O/ent_$a1.detail.json" > "$O/ent_$a1.json" 2> "$O/ent_$a1.err") || fail ent "$O/ent_$a1.err"
+      tail -c 300 "$O/ent_$a1.json" ;;
     sq)
       (cd /tmp && timeout -k 10 300 rocprofv3 -i "$R/tools/pmc/pixel.txt" --output-format csv -d "$O/sq_$a1" -o px -- \
           python3 "$R/bench.py" --workload "$a1" --frames 256 --steps 2 --warmup 1 --no-cpu --no-stream --no-stages \
