@@ -414,13 +414,10 @@ Caps make_caps(int max_frames, int64_t max_scan_bytes, int64_t max_blocks, int s
     c.max_segs = max_blocks + ef;
     c.max_tiles = max_scan_bytes / kTileBytes + max_frames;
     const size_t per_frame = (sizeof(EntFrame) + sizeof(HuffLut) * kMaxTables + 4) * kMaxScans + sizeof(FrameRecord) +
-                             192 * 4 + sizeof(RawFrame);
+                             192 * 4 + sizeof(RawFrame) + 4;
     c.hdr_cap = align_up(per_frame * max_frames + 4 * static_cast<size_t>(c.max_segs + c.max_wgs + c.max_tiles) +
                              10 * kAlign, kAlign);
     c.data = c.hdr_cap;
-#ifdef HJD_TMP_DATA_SKEW
-    c.data += HJD_TMP_DATA_SKEW;
-#endif
     return c;
 }
 
@@ -443,7 +440,8 @@ struct EntBatchDev {
     uint32_t* linked;     // [group] 1 if joined to the previous group's chain
     SubStats* agg;
     SubStats* agg2;       // [group] null, or the rest of agg: a group's statistics in the next chain chunk
-    uint32_t* status;
+    uint32_t* status;     // [nframes] + one word: ent_write_kernel's finished-workgroup count
+    uint32_t* host_status;   // null, or pinned host words the last write workgroup copies status to
     int16_t* coefs;
     uint32_t nframes, nwg, sub_bits, ntab_max;   // ntab_max: tables of the largest frame (dynamic LDS)
     uint32_t ntab_total;                         // tables of the batch
@@ -1497,6 +1495,23 @@ __global__ __launch_bounds__(64) void ent_fallback_kernel(EntBatchDev b)
 // for a lone frame's few groups, one wave per SIMD.
 constexpr int kWriteThreads = kGroupSubs;
 
+// The write kernel's end: with b.host_status set, the last workgroup to
+// finish copies the frames' status words into pinned host memory, so no
+// status copy follows the kernels (the host reads them after the stream's
+// completion event).  Every workgroup counts itself once; the status words
+// were all final (agent-scope release) before its count.
+__device__ __forceinline__ void write_done(const EntBatchDev& b, int tid)
+{
+    if (!b.host_status) return;
+    __syncthreads();
+    if (tid != 0) return;
+    const uint32_t nwg = gridDim.x * gridDim.y;
+    if (__hip_atomic_fetch_add(b.status + b.nframes, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) != nwg - 1) return;
+    for (uint32_t f = 0; f < b.nframes; ++f)
+        b.host_status[f] = __hip_atomic_load(b.status + f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    __threadfence_system();
+}
+
 __global__ __launch_bounds__(kWriteThreads) void ent_write_kernel(EntBatchDev b)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -1511,50 +1526,53 @@ __global__ __launch_bounds__(kWriteThreads) void ent_write_kernel(EntBatchDev b)
     const uint32_t f = b.wg_frame[w];
     const EntFrame F = b.frames[f];
     const uint32_t gl = w - F.wg_base;
-    if (gl >= frame_groups(F.nsub) || piece >= write_pieces(b)) return;
     __shared__ BlockInfo blocks[kMaxBpm];
-    load_tables(tabs, blocks, b.tabs + F.tab_base, F, b.frames + f, tid, kWriteThreads);
-    // block index / DC predictors at this group's start: all previous groups of the frame
-    SubStats pre = stats_identity();
-    for (uint32_t base = 0; base < gl; base += kWriteThreads) {
-        SubStats v = stats_identity();
-        if (base + tid < gl) {
-            v = b.agg[F.wg_base + base + tid];
-            if (b.agg2) v = stats_combine(v, b.agg2[F.wg_base + base + tid]);
+    if (gl < frame_groups(F.nsub) && piece < write_pieces(b)) {   // (uniform in the workgroup)
+        load_tables(tabs, blocks, b.tabs + F.tab_base, F, b.frames + f, tid, kWriteThreads);
+        // block index / DC predictors at this group's start: all previous groups of the frame
+        SubStats pre = stats_identity();
+        for (uint32_t base = 0; base < gl; base += kWriteThreads) {
+            SubStats v = stats_identity();
+            if (base + tid < gl) {
+                v = b.agg[F.wg_base + base + tid];
+                if (b.agg2) v = stats_combine(v, b.agg2[F.wg_base + base + tid]);
+            }
+            block_scan_inclusive<kWriteThreads>(v, buf, tid);
+            const SubStats total = buf[kWriteThreads - 1];
+            __syncthreads();
+            pre = stats_combine(pre, total);
         }
-        block_scan_inclusive<kWriteThreads>(v, buf, tid);
-        const SubStats total = buf[kWriteThreads - 1];
-        __syncthreads();
-        pre = stats_combine(pre, total);
+        const int64_t k = group_sub(gl, t);
+        const bool own = t >= kWarm && k < static_cast<int64_t>(F.nsub);
+        const uint32_t ku = static_cast<uint32_t>(k);
+        // subsequence prefixes
+        const SubStats mine = own ? sub_stats(b, F, ku) : stats_identity();
+        block_scan_inclusive<kWriteThreads>(mine, buf, tid);
+        SubStats excl = stats_combine(pre, t > 0 ? buf[t - 1] : stats_identity());
+        __syncthreads();   // scratch reads done before blocks are staged
+        if (own) {
+            SubStats lead;
+            const uint64_t entry = piece_entry(b, F, ku, piece, lead);
+            excl = stats_combine(excl, lead);
+            const uint32_t stop = piece_stop(b, ku, piece);
+            const RunCtx c = make_ctx(b, F, tabs, blocks);
+            RunOut o;
+            o.coefs = b.coefs + F.coef_off * 64;
+            o.stage = stage + tid * kStageStride;
+            o.blk = excl.nblk;
+            o.nblocks = F.nblocks;
+            o.nout = F.nout;
+            o.pred[0] = excl.dc[0];
+            o.pred[1] = excl.dc[1];
+            o.pred[2] = excl.dc[2];
+            SubStats st = stats_identity();
+            run<true>(c, entry, stop, st, &o);
+            uint32_t bad = (st.flags & kError) ? kStatusCorrupt : 0;
+            if (piece + 1 == write_pieces(b) && ku == F.nsub - 1 && excl.nblk + st.nblk != F.nblocks) bad |= kStatusCount;
+            if (bad) __hip_atomic_fetch_or(&b.status[f], bad, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
-    const int64_t k = group_sub(gl, t);
-    const bool own = t >= kWarm && k < static_cast<int64_t>(F.nsub);
-    const uint32_t ku = static_cast<uint32_t>(k);
-    // subsequence prefixes
-    const SubStats mine = own ? sub_stats(b, F, ku) : stats_identity();
-    block_scan_inclusive<kWriteThreads>(mine, buf, tid);
-    SubStats excl = stats_combine(pre, t > 0 ? buf[t - 1] : stats_identity());
-    __syncthreads();   // scratch reads done before blocks are staged
-    if (!own) return;
-    SubStats lead;
-    const uint64_t entry = piece_entry(b, F, ku, piece, lead);
-    excl = stats_combine(excl, lead);
-    const uint32_t stop = piece_stop(b, ku, piece);
-    const RunCtx c = make_ctx(b, F, tabs, blocks);
-    RunOut o;
-    o.coefs = b.coefs + F.coef_off * 64;
-    o.stage = stage + tid * kStageStride;
-    o.blk = excl.nblk;
-    o.nblocks = F.nblocks;
-    o.nout = F.nout;
-    o.pred[0] = excl.dc[0];
-    o.pred[1] = excl.dc[1];
-    o.pred[2] = excl.dc[2];
-    SubStats st = stats_identity();
-    run<true>(c, entry, stop, st, &o);
-    uint32_t bad = (st.flags & kError) ? kStatusCorrupt : 0;
-    if (piece + 1 == write_pieces(b) && ku == F.nsub - 1 && excl.nblk + st.nblk != F.nblocks) bad |= kStatusCount;
-    if (bad) atomicOr(&b.status[f], bad);
+    write_done(b, tid);
 }
 
 // ---------------------------------------------------------------------------
@@ -2418,12 +2436,12 @@ int hjd_gdec::assemble(uint8_t* blob, int16_t* coefs, int64_t* block_offsets, vo
     o.tilef = align_up(o.rawf + (ntiles ? sizeof(RawFrame) * ne : 0), kAlign);
     // per entropy frame status words, zero in the header's upload (no memset)
     o.status = align_up(o.tilef + 4 * ntiles, kAlign);
-    o.used = align_up(o.status + 4 * static_cast<size_t>(ne), kAlign);
+    o.used = align_up(o.status + 4 * (static_cast<size_t>(ne) + 1), kAlign);
     if (o.used > caps.hdr_cap || ntiles > static_cast<size_t>(caps.max_tiles))
         return set_error(HJD_E_INVALID, "batch header exceeds its capacity");
 
     EntFrame* ef = reinterpret_cast<EntFrame*>(h_stage + o.frames);
-    memset(h_stage + o.status, 0, 4 * static_cast<size_t>(ne));
+    memset(h_stage + o.status, 0, 4 * (static_cast<size_t>(ne) + 1));
     HuffLut* tb = reinterpret_cast<HuffLut*>(h_stage + o.tabs);
     uint32_t* seg = reinterpret_cast<uint32_t*>(h_stage + o.seg);
     uint32_t* wgf = reinterpret_cast<uint32_t*>(h_stage + o.wg);
@@ -2516,6 +2534,7 @@ int hjd_gdec::assemble(uint8_t* blob, int16_t* coefs, int64_t* block_offsets, vo
     d.chain_broken = nullptr;
     d.chain_epoch = 0;
     d.agg2 = nullptr;
+    d.host_status = nullptr;
     d.spec = nullptr;
     d.cand = nullptr;
     d.cmap = nullptr;
@@ -2662,6 +2681,30 @@ struct HostCopy {
     int32_t width, height;
 };
 
+// Latency decoders: the staged bytes of a batch whose scans were all
+// destuffed on the host (its header, then its data area) are pulled from the
+// pinned staging by one kernel instead of two DMA copies: 1 MB moves in 23 us
+// against 31 us by DMA (tools/h2d_probe.hip, profiles/r06y_h2d_probe.json;
+// 64 workgroups beat 256 and 1024), and the kernel replaces the copy calls.
+// Staging and blob share their layout, so a segment is an offset and a length
+// (16-B multiples: the header is kAlign-aligned, a data run ends in its pad).
+constexpr int kPullSegs = 4;
+constexpr int kPullBlocks = 64;
+constexpr int kPullThreads = 256;
+struct PullSegs {
+    uint64_t off[kPullSegs];     // 16-B words
+    uint64_t words[kPullSegs];
+    uint32_t n;
+};
+
+__global__ __launch_bounds__(kPullThreads) void pull_kernel(const u32x4* src, u32x4* dst, PullSegs p)
+{
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kPullThreads;
+    for (uint32_t k = 0; k < p.n; ++k)
+        for (uint64_t w = blockIdx.x * static_cast<uint64_t>(kPullThreads) + threadIdx.x; w < p.words[k]; w += stride)
+            dst[p.off[k] + w] = src[p.off[k] + w];
+}
+
 int gdec_issue(hjd_gdec* g, void* const* d_outs, const int32_t* pitches, int16_t* coefs_out, int64_t* block_offsets,
                hipStream_t s, const HostCopy* host = nullptr)
 {
@@ -2679,6 +2722,7 @@ int gdec_issue(hjd_gdec* g, void* const* d_outs, const int32_t* pitches, int16_t
     b.linked = g->d_linked;
     b.agg = g->d_agg;
     b.status = reinterpret_cast<uint32_t*>(g->d_blob + g->H.status);
+    if (b.nwg) b.host_status = g->h_status;   // the write kernel delivers the status words
     b.raw = g->d_raw;
     b.tiles = g->d_tiles;
     b.steps_g = g->d_steps;
@@ -2699,7 +2743,16 @@ int gdec_issue(hjd_gdec* g, void* const* d_outs, const int32_t* pitches, int16_t
     // the device buffers are reused: order this call after the previous one
     // (which may have been issued on another stream)
     if (g->pending) HJD_HIP(hipStreamWaitEvent(s, g->done, 0));
-    HJD_HIP(hipMemcpyAsync(g->d_blob, g->h_stage, g->H.used, hipMemcpyHostToDevice, s));
+    bool pull = g->spec;   // latency decoders, every scan host-destuffed (one data run)
+    for (const Prepared& p : g->frames) pull = pull && p.destuff == kDestuffHost;
+    PullSegs segs{};
+    if (pull) {
+        segs.off[0] = 0;
+        segs.words[0] = g->H.used / 16;
+        segs.n = 1;
+    } else {
+        HJD_HIP(hipMemcpyAsync(g->d_blob, g->h_stage, g->H.used, hipMemcpyHostToDevice, s));
+    }
     // scan bytes: runs of consecutive frames staged the same way move in one copy
     // (host-destuffed -> data area; raw in staging -> raw area); raw bytes in the
     // caller's pinned memory go straight from there to the raw area.
@@ -2747,9 +2800,20 @@ int gdec_issue(hjd_gdec* g, void* const* d_outs, const int32_t* pitches, int16_t
             ++j;
         }
         uint8_t* dst = g->d_blob + g->caps.data + p.data_off;
-        HJD_HIP(hipMemcpyAsync(dst, g->h_stage + g->caps.data + p.data_off, hi - p.data_off, hipMemcpyHostToDevice, s));
+        if (pull && segs.n < kPullSegs) {
+            segs.off[segs.n] = (g->caps.data + p.data_off) / 16;
+            segs.words[segs.n] = (hi - p.data_off + 15) / 16;
+            ++segs.n;
+        } else {
+            HJD_HIP(hipMemcpyAsync(dst, g->h_stage + g->caps.data + p.data_off, hi - p.data_off, hipMemcpyHostToDevice, s));
+        }
         moved += static_cast<int64_t>(hi - p.data_off);
         i = j;
+    }
+    if (pull) {
+        hipLaunchKernelGGL(pull_kernel, dim3(kPullBlocks), dim3(kPullThreads), 0, s,
+                           reinterpret_cast<const u32x4*>(g->h_stage), reinterpret_cast<u32x4*>(g->d_blob), segs);
+        HJD_HIP(hipGetLastError());
     }
     // (hipMemcpyBatchAsync would submit these at once, but the HIP runtime this
     // library shares with PyTorch -- DESIGN.md s8 -- predates it)
@@ -2806,7 +2870,8 @@ int gdec_issue(hjd_gdec* g, void* const* d_outs, const int32_t* pitches, int16_t
                                      static_cast<size_t>(host[i].height), hipMemcpyDeviceToHost, s));
         }
     }
-    HJD_HIP(hipMemcpyAsync(g->h_status, b.status, 4 * static_cast<size_t>(b.nframes), hipMemcpyDeviceToHost, s));
+    if (!b.host_status)
+        HJD_HIP(hipMemcpyAsync(g->h_status, b.status, 4 * static_cast<size_t>(b.nframes), hipMemcpyDeviceToHost, s));
     HJD_HIP(hipEventRecord(g->done, s));
     g->nframes_issued = n;
     return HJD_OK;

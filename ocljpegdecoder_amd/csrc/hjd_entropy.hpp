@@ -467,7 +467,10 @@ __host__ __device__ __forceinline__ uint32_t long_code_entry(const HuffLut& t, u
 // stop and records, at the first unit boundary >= each, the state (mstate)
 // and the statistics since the previous mark (mstats; `st` then holds those
 // after the last mark) -- exactly what separate runs split there would give,
-// without a window reload per piece.
+// without a window reload per piece.  The marks are taken between passes of
+// the unit loop (one pass per mark), not inside it: a mark test in the loop
+// made every unit dearer (gfx950, same box: spec 118 vs 100 us, cand 147 vs
+// 115 us per FHD frame; profiles/r06y_*).
 template <bool kWrite, int kMarks = 0>
 __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry, uint32_t stop, SubStats& st,
                                                  RunOut* out, const uint32_t* mpos = nullptr,
@@ -475,7 +478,6 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
 {
     static_assert(!kWrite || kMarks == 0, "marks: sync mode only");
     int mi = 0;
-    uint32_t lim = kMarks ? mpos[0] : stop;   // the next mark, then stop
     uint32_t pos = st_pos(entry);
     uint32_t z = st_z(entry);
     uint32_t j = st_j(entry);
@@ -524,164 +526,162 @@ __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry
         result = 0;
         bool done = false;
         bw.seek(c, pos >> 5);
-        // One loop: a nested re-seek loop (so the window never merges with a
-        // seek) measured 13% slower -- its extra exits cost more exec-mask
-        // bookkeeping per unit than the merge copies.
-        for (;;) {
-            if (pos >= lim && (!kWrite || !owned)) {
-                if (kMarks && mi < kMarks) {   // a mark: its state and the statistics since the last one
-                    mstate[mi] = pack_state(pos, j, z, seg);
-                    mstats[mi].nblk = static_cast<uint32_t>(nblk);
-                    mstats[mi].flags = flags;
-                    mstats[mi].dc[0] = d0;
-                    mstats[mi].dc[1] = d1;
-                    mstats[mi].dc[2] = d2;
-                    nblk = d0 = d1 = d2 = 0;
-                    flags = 0;
-                    ++mi;
-                    lim = mi < kMarks ? mpos[mi] : stop;
-                    continue;
+        for (;; ++mi) {   // one pass per mark, then to stop
+            const uint32_t lim = mi < kMarks ? mpos[mi] : stop;
+            // One loop: a nested re-seek loop (so the window never merges with a
+            // seek) measured 13% slower -- its extra exits cost more exec-mask
+            // bookkeeping per unit than the merge copies.
+            for (;;) {
+                if (pos >= lim && (!kWrite || !owned)) break;
+                const uint32_t nwi = pos >> 5;
+                if (nwi != bw.wi) {
+                    if (nwi == bw.wi + 1) bw.advance(c);
+                    else bw.seek(c, nwi);   // an overrun of a restart pad moved pos back
                 }
-                break;
-            }
-            const uint32_t nwi = pos >> 5;
-            if (nwi != bw.wi) {
-                if (nwi == bw.wi + 1) bw.advance(c);
-                else bw.seek(c, nwi);   // an overrun of a restart pad moved pos back
-            }
-            const uint32_t peek = funnel(bw.w0, bw.w1, pos & 31);
-            // ---- restart-interval end: < 8 bits left, all ones (or overrun) ----
-            const int32_t left = static_cast<int32_t>(seg_end - pos);
-            if (left < 8) {
-                const bool ones = left <= 0 || (peek >> (32 - left)) == (1u << left) - 1;
-                if (ones) {
-                    if (left < 0 || (kWrite && owned)) flags |= kError;   // overrun / block cut by the pad
-                    pos = seg_end;
-                    ++seg;
-                    // write mode: the interval just closed must have held
-                    // exactly DRI MCUs (the host decoder counts them and resyncs
-                    // at the marker; a count that differs is corrupt data)
-                    if (kWrite && c.seg_blocks && seg < c.nseg && blk != seg * c.seg_blocks) flags |= kError;
-                    j = 0;
-                    z = 0;
-                    bi = block_of(c, 0);
-                    owned = false;
-                    cur = nullptr;
-                    flags |= kReset;
-                    d0 = d1 = d2 = 0;
-                    p0 = p1 = p2 = 0;
-                    if (seg >= c.nseg) {
-                        result = pack_state(c.data_bits, 0, 0, c.nseg);
-                        done = true;
-                        break;
-                    }
-                    seg_end = c.seg_end[seg];
-                    // consume the load inside this rare branch, so the loop
-                    // head does not wait for every outstanding memory op
-                    if (seg_end < pos) flags |= kError;
-                    continue;
-                }
-            }
-            const bool dc = z == 0;
-            // ---- sync mode: the AC units the peek holds, in one step ----
-            // Taken only where single units would give the same state: all of
-            // them end at or before `stop`, >= 8 bits before the segment end (no pad
-            // check in between), and z stays <= 63 (no index-63 error case).
-            // (A branch-free form that computes the step and the unit outcome in
-            // every lane and selects measured slower: DESIGN.md s10.1.)
-            if (!kWrite && c.steps && !dc) {
-                const uint32_t se = c.steps[bi.sac + (peek >> (32 - kStepBits))];
-                const uint32_t nb = step_bits(se), za = step_zadv(se);
-                const bool ends = za == kStepEnds;
-                // an EOB entry's units before the EOB move z by <= 14: z <= 49 keeps them <= 63
-                if (se != 0 && z + (ends ? 14 : za) <= 63 && left >= static_cast<int32_t>(nb) + 8 && pos + nb <= lim) {
-                    pos += nb;
-                    if (ends) {
+                const uint32_t peek = funnel(bw.w0, bw.w1, pos & 31);
+                // ---- restart-interval end: < 8 bits left, all ones (or overrun) ----
+                const int32_t left = static_cast<int32_t>(seg_end - pos);
+                if (left < 8) {
+                    const bool ones = left <= 0 || (peek >> (32 - left)) == (1u << left) - 1;
+                    if (ones) {
+                        if (left < 0 || (kWrite && owned)) flags |= kError;   // overrun / block cut by the pad
+                        pos = seg_end;
+                        ++seg;
+                        // write mode: the interval just closed must have held
+                        // exactly DRI MCUs (the host decoder counts them and resyncs
+                        // at the marker; a count that differs is corrupt data)
+                        if (kWrite && c.seg_blocks && seg < c.nseg && blk != seg * c.seg_blocks) flags |= kError;
+                        j = 0;
                         z = 0;
-                        j = j + 1 == static_cast<uint32_t>(c.bpm) ? 0 : j + 1;
-                        bi = block_of(c, j);
-                    } else {
-                        z += za;
-                    }
-                    continue;
-                }
-            }
-            // ---- one unit: Huffman symbol + extra bits (unit_entry fields) ----
-            const HuffLut& t = *reinterpret_cast<const HuffLut*>(reinterpret_cast<const char*>(c.tabs) +
-                                                                 (dc ? bi.tdc : bi.tac));
-            uint32_t e = t.lut[peek >> (32 - kLutBits)];
-            if (e == 0) e = long_code_entry(t, peek, dc, flags);
-            const uint32_t total = e & 31, s = (e >> 5) & 15;
-            uint32_t zk = e >> 9;
-            if (zk == kZkDcError) {   // DC symbol > 11
-                flags |= kError;
-                zk = 1;
-            }
-            // extra bits -> value (T.81 F.2.2.1 EXTEND); s = 0 gives 0
-            const uint32_t bits = ubfe(peek, 32 - total, s);
-            const uint32_t m = (1u << s) - 1;
-            const int32_t v = bits <= (m >> 1) ? static_cast<int32_t>(bits - m) : static_cast<int32_t>(bits);
-            pos += total;
-            const uint32_t zn = z + zk;
-            if (zn > 64 && zk != 64) flags |= kError;   // AC coefficient or ZRL past index 63 (not EOB)
-            // DC unit: a block starts (per-component sums by 0/1 multipliers, no branch)
-            const int32_t dv = dc ? v : 0;
-            nblk += dc ? 1 : 0;
-            d0 = mad24(dv, bi.m0, d0);
-            d1 = mad24(dv, bi.m1, d1);
-            d2 = mad24(dv, bi.m2, d2);
-            if (kWrite) {
-                if (dc) {
-                    owned = true;
-                    p0 = mad24(v, bi.m0, p0);
-                    p1 = mad24(v, bi.m1, p1);
-                    p2 = mad24(v, bi.m2, p2);
-                    // MCU-major destination; on valid data blk % bpm == j.  Blocks past
-                    // the scan's count are ignored (as the host decoder stops there).
-                    const uint32_t dst = block_dest(c, bu, bv, bi.ji >> 8);
-                    cur = nullptr;
-                    if (blk < out->nblocks) {
-                        if (dst < out->nout && blk_j == j) {
-                            cur = out->coefs + static_cast<uint64_t>(dst) * 64;
-                            zero_quarter(out->stage);
-                            out->stage[0] = static_cast<int16_t>(p0 * bi.m0 + p1 * bi.m1 + p2 * bi.m2);
-                            quarter = 0;
-                        } else {
-                            flags |= kError;   // a restart interval ended inside an MCU
+                        bi = block_of(c, 0);
+                        owned = false;
+                        cur = nullptr;
+                        flags |= kReset;
+                        d0 = d1 = d2 = 0;
+                        p0 = p1 = p2 = 0;
+                        if (seg >= c.nseg) {
+                            result = pack_state(c.data_bits, 0, 0, c.nseg);
+                            done = true;
+                            break;
                         }
+                        seg_end = c.seg_end[seg];
+                        // consume the load inside this rare branch, so the loop
+                        // head does not wait for every outstanding memory op
+                        if (seg_end < pos) flags |= kError;
+                        continue;
                     }
-                } else if (s != 0 && zn <= 64 && cur) {
-                    const uint32_t zi = zn - 1;   // the coefficient's index: z + run
-                    const uint32_t qz = zi >> 4;
-                    if (qz != quarter) {
-                        flush_quarters(cur, out->stage, quarter, qz);
-                        quarter = qz;
+                }
+                const bool dc = z == 0;
+                // ---- sync mode: the AC units the peek holds, in one step ----
+                // Taken only where single units would give the same state: all of
+                // them end at or before `stop`, >= 8 bits before the segment end (no pad
+                // check in between), and z stays <= 63 (no index-63 error case).
+                // (A branch-free form that computes the step and the unit outcome in
+                // every lane and selects measured slower: DESIGN.md s10.1.)
+                if (!kWrite && c.steps && !dc) {
+                    const uint32_t se = c.steps[bi.sac + (peek >> (32 - kStepBits))];
+                    const uint32_t nb = step_bits(se), za = step_zadv(se);
+                    const bool ends = za == kStepEnds;
+                    // an EOB entry's units before the EOB move z by <= 14: z <= 49 keeps them <= 63
+                    if (se != 0 && z + (ends ? 14 : za) <= 63 && left >= static_cast<int32_t>(nb) + 8 && pos + nb <= lim) {
+                        pos += nb;
+                        if (ends) {
+                            z = 0;
+                            j = j + 1 == static_cast<uint32_t>(c.bpm) ? 0 : j + 1;
+                            bi = block_of(c, j);
+                        } else {
+                            z += za;
+                        }
+                        continue;
                     }
-                    out->stage[zi & 15] = static_cast<int16_t>(v);
+                }
+                // ---- one unit: Huffman symbol + extra bits (unit_entry fields) ----
+                const HuffLut& t = *reinterpret_cast<const HuffLut*>(reinterpret_cast<const char*>(c.tabs) +
+                                                                     (dc ? bi.tdc : bi.tac));
+                uint32_t e = t.lut[peek >> (32 - kLutBits)];
+                if (e == 0) e = long_code_entry(t, peek, dc, flags);
+                const uint32_t total = e & 31, s = (e >> 5) & 15;
+                uint32_t zk = e >> 9;
+                if (zk == kZkDcError) {   // DC symbol > 11
+                    flags |= kError;
+                    zk = 1;
+                }
+                // extra bits -> value (T.81 F.2.2.1 EXTEND); s = 0 gives 0
+                const uint32_t bits = ubfe(peek, 32 - total, s);
+                const uint32_t m = (1u << s) - 1;
+                const int32_t v = bits <= (m >> 1) ? static_cast<int32_t>(bits - m) : static_cast<int32_t>(bits);
+                pos += total;
+                const uint32_t zn = z + zk;
+                if (zn > 64 && zk != 64) flags |= kError;   // AC coefficient or ZRL past index 63 (not EOB)
+                // DC unit: a block starts (per-component sums by 0/1 multipliers, no branch)
+                const int32_t dv = dc ? v : 0;
+                nblk += dc ? 1 : 0;
+                d0 = mad24(dv, bi.m0, d0);
+                d1 = mad24(dv, bi.m1, d1);
+                d2 = mad24(dv, bi.m2, d2);
+                if (kWrite) {
+                    if (dc) {
+                        owned = true;
+                        p0 = mad24(v, bi.m0, p0);
+                        p1 = mad24(v, bi.m1, p1);
+                        p2 = mad24(v, bi.m2, p2);
+                        // MCU-major destination; on valid data blk % bpm == j.  Blocks past
+                        // the scan's count are ignored (as the host decoder stops there).
+                        const uint32_t dst = block_dest(c, bu, bv, bi.ji >> 8);
+                        cur = nullptr;
+                        if (blk < out->nblocks) {
+                            if (dst < out->nout && blk_j == j) {
+                                cur = out->coefs + static_cast<uint64_t>(dst) * 64;
+                                zero_quarter(out->stage);
+                                out->stage[0] = static_cast<int16_t>(p0 * bi.m0 + p1 * bi.m1 + p2 * bi.m2);
+                                quarter = 0;
+                            } else {
+                                flags |= kError;   // a restart interval ended inside an MCU
+                            }
+                        }
+                    } else if (s != 0 && zn <= 64 && cur) {
+                        const uint32_t zi = zn - 1;   // the coefficient's index: z + run
+                        const uint32_t qz = zi >> 4;
+                        if (qz != quarter) {
+                            flush_quarters(cur, out->stage, quarter, qz);
+                            quarter = qz;
+                        }
+                        out->stage[zi & 15] = static_cast<int16_t>(v);
+                    }
+                }
+                if (zn >= 64) {   // EOB, ZRL or a coefficient reaching the end, or an error
+                    if (kWrite && owned) {
+                        if (cur) flush_quarters(cur, out->stage, quarter, 4);   // the rest of the block
+                        blk += 1;
+                        if (c.layout == kLayoutMcu) {
+                            const bool wrap = blk_j + 1 == static_cast<uint32_t>(c.bpm);
+                            blk_j = wrap ? 0 : blk_j + 1;
+                            bu += wrap ? 1 : 0;
+                        } else {
+                            const bool wrap = bu + 1 == (c.geo >> 8);
+                            bu = wrap ? 0 : bu + 1;
+                            bv += wrap ? 1 : 0;
+                        }
+                        owned = false;
+                        cur = nullptr;
+                    }
+                    z = 0;
+                    j = j + 1 == static_cast<uint32_t>(c.bpm) ? 0 : j + 1;
+                    bi = block_of(c, j);
+                } else {
+                    z = zn;
                 }
             }
-            if (zn >= 64) {   // EOB, ZRL or a coefficient reaching the end, or an error
-                if (kWrite && owned) {
-                    if (cur) flush_quarters(cur, out->stage, quarter, 4);   // the rest of the block
-                    blk += 1;
-                    if (c.layout == kLayoutMcu) {
-                        const bool wrap = blk_j + 1 == static_cast<uint32_t>(c.bpm);
-                        blk_j = wrap ? 0 : blk_j + 1;
-                        bu += wrap ? 1 : 0;
-                    } else {
-                        const bool wrap = bu + 1 == (c.geo >> 8);
-                        bu = wrap ? 0 : bu + 1;
-                        bv += wrap ? 1 : 0;
-                    }
-                    owned = false;
-                    cur = nullptr;
-                }
-                z = 0;
-                j = j + 1 == static_cast<uint32_t>(c.bpm) ? 0 : j + 1;
-                bi = block_of(c, j);
-            } else {
-                z = zn;
-            }
+            if (done || mi >= kMarks) break;   // the end of the data, or past the last mark
+            // mark mi: its state and the statistics since the previous one
+            mstate[mi] = pack_state(pos, j, z, seg);
+            mstats[mi].nblk = static_cast<uint32_t>(nblk);
+            mstats[mi].flags = flags;
+            mstats[mi].dc[0] = d0;
+            mstats[mi].dc[1] = d1;
+            mstats[mi].dc[2] = d2;
+            nblk = d0 = d1 = d2 = 0;
+            flags = 0;
         }
         if (!done) result = pack_state(pos, j, z, seg);
     }

@@ -2,6 +2,7 @@
 // reads the pinned host buffer directly (zero copy), timed with HIP events.
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include <cstring>
 #include <vector>
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("err %s line %d\n", hipGetErrorString(e), __LINE__); return 1; } } while (0)
 __global__ void pull(const uint4* __restrict__ src, uint4* __restrict__ dst, size_t n16)
