@@ -413,7 +413,7 @@ Caps make_caps(int max_frames, int64_t max_scan_bytes, int64_t max_blocks, int s
     // gray file) with Ri = 1 has one per block, so blocks + one per entropy frame
     c.max_segs = max_blocks + ef;
     c.max_tiles = max_scan_bytes / kTileBytes + max_frames;
-    const size_t per_frame = (sizeof(EntFrame) + sizeof(HuffLut) * kMaxTables + 4) * kMaxScans + sizeof(FrameRecord) +
+    const size_t per_frame = (sizeof(EntFrame) + sizeof(HuffLut) * kMaxTables + 8) * kMaxScans + sizeof(FrameRecord) +
                              192 * 4 + sizeof(RawFrame) + 4;
     c.hdr_cap = align_up(per_frame * max_frames + 4 * static_cast<size_t>(c.max_segs + c.max_wgs + c.max_tiles) +
                              10 * kAlign, kAlign);
@@ -440,7 +440,7 @@ struct EntBatchDev {
     uint32_t* linked;     // [group] 1 if joined to the previous group's chain
     SubStats* agg;
     SubStats* agg2;       // [group] null, or the rest of agg: a group's statistics in the next chain chunk
-    uint32_t* status;     // [nframes] + one word: ent_write_kernel's finished-workgroup count
+    uint32_t* status;     // [nframes], ent_write_kernel's finished-workgroup count, [nframes] chain chunk counts
     uint32_t* host_status;   // null, or pinned host words the last write workgroup copies status to
     int16_t* coefs;
     uint32_t nframes, nwg, sub_bits, ntab_max;   // ntab_max: tables of the largest frame (dynamic LDS)
@@ -1224,15 +1224,12 @@ __device__ __forceinline__ void group_agg(const EntBatchDev& b, const EntFrame& 
     }
 }
 
-__global__ __launch_bounds__(kChainThreads) void ent_chain_kernel(EntBatchDev b)
+// The serial walk of frame f by one workgroup (the chain kernel's, or the
+// look-back kernel's last chunk of a frame whose chain needs a repair).
+__device__ __forceinline__ void chain_walk(const EntBatchDev& b, uint32_t f, ChainLds& L, int tid)
 {
-    __shared__ ChainLds L;
-    const int tid = threadIdx.x;
-    const uint32_t f = blockIdx.x;
     const EntFrame F = b.frames[f];
-    // the look-back kernel ran every chunk in parallel; walk serially only a
-    // frame where the chain leaves its slots (the repairs need the order)
-    const uint32_t n = b.chain_broken && b.chain_broken[f] != b.chain_epoch ? 0u : F.nsub;
+    const uint32_t n = F.nsub;
     uint8_t* cm = b.cmap + static_cast<uint64_t>(F.sub_base) * kSlotRow;
     if (tid == 0) {
         L.carry = 0;
@@ -1280,13 +1277,19 @@ __global__ __launch_bounds__(kChainThreads) void ent_chain_kernel(EntBatchDev b)
         __syncthreads();
         if (r0 < cn && (r0 + kChainRows >= cn)) L.carry = s;   // the thread holding the chunk's last row
     }
-    if (n == 0) return;   // not walked: the look-back kernel's group statistics stand
     __syncthreads();
     const int wv = tid >> 6, lane = tid & 63;
     for (uint32_t g = wv; g < frame_groups(F.nsub); g += kChainThreads / 64) {
         group_agg(b, F, g, lane);
         if (b.agg2 && lane == 0) b.agg2[F.wg_base + g] = stats_identity();
     }
+}
+
+// Every frame walked serially (decoders without look-back words).
+__global__ __launch_bounds__(kChainThreads) void ent_chain_kernel(EntBatchDev b)
+{
+    __shared__ ChainLds L;
+    chain_walk(b, blockIdx.x, L, threadIdx.x);
 }
 
 // ---- the chain, chunks in parallel (the case without repairs) -----------------
@@ -1303,13 +1306,18 @@ __global__ __launch_bounds__(kChainThreads) void ent_chain_kernel(EntBatchDev b)
 // a group's part in its first chunk into agg, its part in the next into agg2
 // (so no chunk waits for another's slots).  A chunk that finds the chain
 // leaving every slot marks its frame (chain_broken = epoch), and
-// ent_chain_kernel then walks that frame serially with its repairs,
-// overwriting the slots and the group statistics; it skips every other frame.
+// the frame's last chunk to finish (a per-frame count in the batch header)
+// then walks that frame serially with its repairs (chain_walk), overwriting
+// the slots and the group statistics.
 struct ChainParLds {
     uint32_t rows[kChainChunk][kRowWords];
     uint32_t fn[2][kChainThreads][kRowWords];
     uint8_t slots[kChainChunk];   // the chain's slot of each row
-    uint32_t carry, broken;
+    uint32_t carry, broken, walk;
+};
+union ChainLbLds {
+    ChainParLds p;
+    ChainLds w;   // the walk, after the chunk's own work
 };
 
 // Ordered reduction (one wave) of the chain statistics of subsequences
@@ -1336,12 +1344,13 @@ __device__ __forceinline__ SubStats range_stats(const EntBatchDev& b, const EntF
 
 __global__ __launch_bounds__(kChainThreads) void ent_chain_lb_kernel(EntBatchDev b)
 {
-    __shared__ ChainParLds L;
+    __shared__ ChainLbLds U;
+    ChainParLds& L = U.p;
     const int tid = threadIdx.x;
     const uint32_t c = blockIdx.x, f = blockIdx.y;
     const EntFrame F = b.frames[f];
     const uint32_t n = F.nsub, c0 = c * kChainChunk;
-    if (c0 >= n) return;
+    if (c0 >= n) return;   // (uniform: past this frame's chunks, not counted)
     const uint32_t cn = n - c0 < static_cast<uint32_t>(kChainChunk) ? n - c0 : kChainChunk;
     if (tid == 0) L.broken = 0;
     chunk_load(L.rows, b.cmap + static_cast<uint64_t>(F.sub_base) * kSlotRow, c0, cn, tid);
@@ -1377,14 +1386,12 @@ __global__ __launch_bounds__(kChainThreads) void ent_chain_lb_kernel(EntBatchDev
     }
     chunk_write_slots(L.rows, b.cslot, F.sub_base + c0, cn, tid, slot);
     __syncthreads();
-    if (L.broken || carry == kNoCand) {   // broken here or before: the walk redoes this frame
-        if (tid == 0 && L.broken) b.chain_broken[f] = b.chain_epoch;
-        return;
-    }
+    const bool broken = L.broken || carry == kNoCand;   // here or before: the walk redoes this frame
+    if (tid == 0 && L.broken) __hip_atomic_store(&b.chain_broken[f], b.chain_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // group statistics: each group part in this chunk, one wave per part
     const int wv = tid >> 6, lane = tid & 63;
-    const uint32_t g0 = c0 / kOwn, g1 = (c0 + cn - 1) / kOwn;
-    for (uint32_t g = g0 + static_cast<uint32_t>(wv); g <= g1; g += kChainThreads / 64) {
+    const uint32_t g0 = c0 / kOwn, g1 = broken ? 0 : (c0 + cn - 1) / kOwn;
+    for (uint32_t g = g0 + static_cast<uint32_t>(wv); !broken && g <= g1; g += kChainThreads / 64) {
         const uint32_t glo = g * kOwn, ghi = (g + 1) * kOwn < n ? (g + 1) * kOwn : n;
         const uint32_t lo = glo > c0 ? glo : c0, hi = ghi < c0 + cn ? ghi : c0 + cn;
         const SubStats a = range_stats(b, F, lo, hi, L.slots, c0, lane);
@@ -1399,6 +1406,19 @@ __global__ __launch_bounds__(kChainThreads) void ent_chain_lb_kernel(EntBatchDev
             }
         }
     }
+    // the frame's last chunk to finish walks it if some chunk found a break
+    __syncthreads();
+    if (tid == 0) {
+        const uint32_t nch = (n + kChainChunk - 1) / kChainChunk;
+        const bool last = __hip_atomic_fetch_add(b.status + b.nframes + 1 + f, 1u, __ATOMIC_ACQ_REL,
+                                                 __HIP_MEMORY_SCOPE_AGENT) == nch - 1;
+        L.walk = last && __hip_atomic_load(&b.chain_broken[f], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                             b.chain_epoch;
+    }
+    __syncthreads();
+    const bool walk = L.walk;
+    __syncthreads();   // (the walk's LDS overlays this kernel's)
+    if (walk) chain_walk(b, f, U.w, tid);
 }
 
 __global__ __launch_bounds__(256) void ent_link_kernel(EntBatchDev b)
@@ -2212,6 +2232,7 @@ struct hjd_gdec {
     int64_t last_h2d = 0;               // bytes the last issue moved host -> device
     int64_t last_host_scan_bytes = 0;   // scan bytes the host CPU read + wrote for the staged frames
     bool pending = false;
+    bool staged_by_done = false;        // the last issue pulled its staging: `done` also means staged
     std::vector<Prepared> frames;
     size_t data_used = 0;
     int nframes_issued = 0;
@@ -2263,7 +2284,7 @@ int hjd_gdec::wait_staging()
 {
     if (gpu && pending) {
         HJD_HIP(hipSetDevice(device));
-        HJD_HIP(hipEventSynchronize(staged));
+        HJD_HIP(hipEventSynchronize(staged_by_done ? done : staged));
     }
     return HJD_OK;
 }
@@ -2436,12 +2457,12 @@ int hjd_gdec::assemble(uint8_t* blob, int16_t* coefs, int64_t* block_offsets, vo
     o.tilef = align_up(o.rawf + (ntiles ? sizeof(RawFrame) * ne : 0), kAlign);
     // per entropy frame status words, zero in the header's upload (no memset)
     o.status = align_up(o.tilef + 4 * ntiles, kAlign);
-    o.used = align_up(o.status + 4 * (static_cast<size_t>(ne) + 1), kAlign);
+    o.used = align_up(o.status + 4 * (2 * static_cast<size_t>(ne) + 1), kAlign);
     if (o.used > caps.hdr_cap || ntiles > static_cast<size_t>(caps.max_tiles))
         return set_error(HJD_E_INVALID, "batch header exceeds its capacity");
 
     EntFrame* ef = reinterpret_cast<EntFrame*>(h_stage + o.frames);
-    memset(h_stage + o.status, 0, 4 * (static_cast<size_t>(ne) + 1));
+    memset(h_stage + o.status, 0, 4 * (2 * static_cast<size_t>(ne) + 1));
     HuffLut* tb = reinterpret_cast<HuffLut*>(h_stage + o.tabs);
     uint32_t* seg = reinterpret_cast<uint32_t*>(h_stage + o.seg);
     uint32_t* wgf = reinterpret_cast<uint32_t*>(h_stage + o.wg);
@@ -2650,11 +2671,10 @@ int launch_entropy(hjd_gdec* g, const EntBatchDev& b, hipStream_t s)
         HJD_HIP(hipGetLastError());
         hipLaunchKernelGGL(ent_cand_kernel, dim3(b.nwg, kMaxBpm), dim3(kGroupSubs), tl, s, b);
         HJD_HIP(hipGetLastError());
-        if (b.chain_broken) {   // chunks in parallel (+ group records); the walk below then only repairs
+        if (b.chain_broken)   // chunks in parallel (+ group records; a broken frame's last chunk walks it)
             hipLaunchKernelGGL(ent_chain_lb_kernel, dim3(b.chain_chunks, b.nframes), dim3(kChainThreads), 0, s, b);
-            HJD_HIP(hipGetLastError());
-        }
-        hipLaunchKernelGGL(ent_chain_kernel, dim3(b.nframes), dim3(kChainThreads), 0, s, b);   // + group records
+        else   // every frame walked
+            hipLaunchKernelGGL(ent_chain_kernel, dim3(b.nframes), dim3(kChainThreads), 0, s, b);
         HJD_HIP(hipGetLastError());
     } else {
         hipLaunchKernelGGL(ent_sync_kernel, dim3(b.nwg), dim3(kGroupSubs), sync_lds_bytes(b.ntab_max), s, b);
@@ -2833,7 +2853,11 @@ int gdec_issue(hjd_gdec* g, void* const* d_outs, const int32_t* pitches, int16_t
     }
     g->last_h2d = moved;
     g->last_host_scan_bytes = host_bytes;
-    HJD_HIP(hipEventRecord(g->staged, s));
+    // (pulled: the staging is free when `done` fires -- an event between the
+    // pull and the first entropy kernel delayed that kernel by ~6 us, and a
+    // latency decoder's next call waits for `done` anyway)
+    if (!pull) HJD_HIP(hipEventRecord(g->staged, s));
+    g->staged_by_done = pull;
     g->pending = true;
     // a multi-scan file's non-interleaved scans leave its MCU-padding blocks
     // uncoded: they must read as zeros (as the host decoder's)
@@ -3428,7 +3452,7 @@ int hjd_gstream::open_batch(std::unique_lock<std::mutex>& lk)
         hjd_gdec* g = slots[s];
         if (g->pending) {
             lk.unlock();
-            const hipError_t e = hipEventSynchronize(g->staged);
+            const hipError_t e = hipEventSynchronize(g->staged_by_done ? g->done : g->staged);
             lk.lock();
             if (e != hipSuccess) return set_error(HJD_E_HIP, "hipEventSynchronize: %s", hipGetErrorString(e));
         }
