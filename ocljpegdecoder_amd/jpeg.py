@@ -52,6 +52,8 @@ def _src(data):
     bytes / bytearray / memoryview / uint8 numpy array / ctypes array.  (A copy
     per call cost a 1 MB FHD JPEG ~0.1 ms of allocation, page faults and memcpy
     on the latency path.)  The library only reads the bytes (const uint8_t*)."""
+    if isinstance(data, bytes):   # the object's own buffer (c_char_p does not copy): ~1 us
+        return ctypes.cast(ctypes.c_char_p(data), _u8p), len(data), data
     if isinstance(data, ctypes.Array):
         return ctypes.cast(data, _u8p), len(data), data
     a = data if isinstance(data, np.ndarray) else np.frombuffer(data, np.uint8)
@@ -230,10 +232,20 @@ def _ptr_size(d):
 
 
 def _byte_arrays(datas):
-    items = [_ptr_size(d) for d in datas]
-    arr_d = (_u8p * len(items))(*[ctypes.cast(a, _u8p) for a, _, _ in items])
-    arr_s = (ctypes.c_size_t * len(items))(*[n for _, n, _ in items])
-    return [k for _, _, k in items], arr_d, arr_s
+    """(objects to keep alive, uint8* array, size_t array) of the inputs; bytes
+    objects take the direct path (a decode call's Python cost is on the
+    single-image latency path)."""
+    ptrs, sizes, keep = [], [], []
+    for d in datas:
+        if isinstance(d, bytes):
+            p, n, k = _src(d)
+        else:
+            a, n, k = _ptr_size(d)
+            p = ctypes.cast(a, _u8p)
+        ptrs.append(p)
+        sizes.append(n)
+        keep.append(k)
+    return keep + ptrs, (_u8p * len(ptrs))(*ptrs), (ctypes.c_size_t * len(sizes))(*sizes)
 
 
 def _stream_handle(stream):
