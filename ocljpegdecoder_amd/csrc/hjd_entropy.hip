@@ -86,12 +86,21 @@ int build_lut(HuffLut& t, const uint8_t counts[16], const uint8_t* syms, int nsy
     return 0;
 }
 
+// A host destuff that hands finished output to the GPU while it runs (a
+// latency decoder's lone image): fire(h, done) once `done` >= next output
+// bytes are final; fire sets the next threshold.
+struct DestuffHook {
+    size_t next;
+    void (*fire)(DestuffHook* h, size_t done);
+    void* ctx;
+};
+
 // Copy an entropy-coded segment without byte stuffing and RST markers.  Ends
 // at the first marker that is not RSTn (normally EOI) or at the end of the
 // buffer.  seg_end receives the destuffed BIT offset where each restart
 // interval ends (the last one = total length).
 int destuff(const uint8_t* p, const uint8_t* end, uint8_t* out, size_t cap, std::vector<uint32_t>& seg_end,
-            size_t& out_len)
+            size_t& out_len, DestuffHook* hook = nullptr)
 {
     uint8_t* q = out;
     uint8_t* const qend = out + cap;
@@ -99,6 +108,7 @@ int destuff(const uint8_t* p, const uint8_t* end, uint8_t* out, size_t cap, std:
     seg_end.clear();
     while (p < end) {
         p = hjd_internal::copy_until_ff(p, end, q, qend);
+        if (hook && static_cast<size_t>(q - out) >= hook->next) hook->fire(hook, static_cast<size_t>(q - out));
         if (p == end) break;
         if (*p != 0xFF) return set_error(HJD_E_INVALID, "scan larger than the staging capacity");
         if (p + 1 >= end) break;                       // truncated at FF
@@ -221,13 +231,15 @@ inline int64_t scan_segments(const hjd_internal::ScanHeader& h)
 
 // Host destuff of one scan into dst (cap bytes, the pad included).
 int destuff_scan(const hjd_internal::ScanHeader& h, const uint8_t* data, size_t size, uint8_t* dst, size_t cap,
-                 Prepared& q)
+                 Prepared& q, DestuffHook* hook = nullptr)
 {
     if (h.scan_offset > size) return set_error(HJD_E_INVALID, "scan offset past the end of the file");
     if (cap <= kDataPad) return set_error(HJD_E_INVALID, "scan bytes exceed the batch capacity");
     size_t len = 0;
     q.raw_len = static_cast<uint32_t>(std::min<size_t>(size - h.scan_offset, 0xFFFFFFFFu));   // bytes the host reads
-    int rc = destuff(data + h.scan_offset, data + size, dst, cap - kDataPad, q.seg_end, len);
+    // a large scan: the first ~60 % of the output goes to the GPU while the host destuffs the rest
+    if (hook) hook->next = size - h.scan_offset >= (256u << 10) ? (size - h.scan_offset) * 3 / 5 : SIZE_MAX;
+    int rc = destuff(data + h.scan_offset, data + size, dst, cap - kDataPad, q.seg_end, len, hook);
     if (rc) return rc;
     if (len == 0) return set_error(HJD_E_INVALID, "empty scan");
     if (len >= (1u << 28)) return set_error(HJD_E_INVALID, "scan too large for one frame (>= 256 MiB)");
@@ -270,7 +282,7 @@ int prepare_multiscan(const uint8_t* data, size_t size, uint8_t* dst, size_t cap
 }
 
 int prepare(const uint8_t* data, size_t size, uint8_t* dst, size_t cap, Prepared& pf, int mode = kDestuffHost,
-            uint64_t raw_off = 0)
+            uint64_t raw_off = 0, DestuffHook* hook = nullptr)
 {
     hjd_internal::ScanHeader h;
     int rc = hjd_internal::parse_scan_header(data, size, &h);
@@ -307,7 +319,7 @@ int prepare(const uint8_t* data, size_t size, uint8_t* dst, size_t cap, Prepared
         pf.data_bits = static_cast<uint32_t>(raw * 8);      // upper bound (groups are laid out for it)
         return HJD_OK;
     }
-    return destuff_scan(h, data, size, dst, cap + kDataPad, pf);
+    return destuff_scan(h, data, size, dst, cap + kDataPad, pf, hook);
 }
 
 // Device destuff ("Destuff on the GPU").  A frame whose scan
@@ -2195,6 +2207,10 @@ uint32_t spec_lead_bits()
 // ---------------------------------------------------------------------------
 // Batch object
 // ---------------------------------------------------------------------------
+namespace {
+void gdec_early_pull(DestuffHook* h, size_t done);
+}
+
 struct hjd_gdec {
     hjd_ctx* ctx = nullptr;
     int device = 0, num_cu = 256;
@@ -2233,6 +2249,9 @@ struct hjd_gdec {
     int64_t last_host_scan_bytes = 0;   // scan bytes the host CPU read + wrote for the staged frames
     bool pending = false;
     bool staged_by_done = false;        // the last issue pulled its staging: `done` also means staged
+    hipStream_t early_stream = nullptr; // this call's stream when its lone image may be pulled early
+    bool early = false;                 // early pull enabled for this call
+    size_t prepulled = 0;               // data-area bytes of frame 0 already pulled (gdec_early_pull)
     std::vector<Prepared> frames;
     size_t data_used = 0;
     int nframes_issued = 0;
@@ -2362,7 +2381,9 @@ int hjd_gdec::prepare_frame(int i, const uint8_t* data, size_t size, size_t data
     p.data_off = data_off;
     if (!data) return p.rc = set_error(HJD_E_INVALID, "frame %d: NULL data", i);
     if (cap <= kDataPad) return p.rc = set_error(HJD_E_INVALID, "scan bytes exceed the batch capacity");
-    int rc = prepare(data, size, data_area() + data_off, cap - kDataPad, p, mode, raw_off);
+    DestuffHook hook{SIZE_MAX, gdec_early_pull, this};
+    int rc = prepare(data, size, data_area() + data_off, cap - kDataPad, p, mode, raw_off,
+                     early && i == 0 && data_off == 0 ? &hook : nullptr);
     if (rc) return p.rc = rc;
     return HJD_OK;
 }
@@ -2725,6 +2746,27 @@ __global__ __launch_bounds__(kPullThreads) void pull_kernel(const u32x4* src, u3
             dst[p.off[k] + w] = src[p.off[k] + w];
 }
 
+// DestuffHook::fire of a latency decoder's lone image: pull the destuffed
+// bytes that are final so far (16-B words) while the host destuffs the rest;
+// gdec_issue pulls the remainder with the header.  One early pull per call
+// (each costs a launch on the host, ~5 us: two measured no better).
+void gdec_early_pull(DestuffHook* h, size_t done)
+{
+    hjd_gdec* g = static_cast<hjd_gdec*>(h->ctx);
+    h->next = SIZE_MAX;
+    const size_t upto = done & ~static_cast<size_t>(15);
+    if (upto <= g->prepulled) return;
+    PullSegs segs{};
+    segs.off[0] = (g->caps.data + g->prepulled) / 16;   // frame 0: data_off 0
+    segs.words[0] = (upto - g->prepulled) / 16;
+    segs.n = 1;
+    if (hipSetDevice(g->device) != hipSuccess) return;
+    if (g->pending && hipStreamWaitEvent(g->early_stream, g->done, 0) != hipSuccess) return;
+    hipLaunchKernelGGL(pull_kernel, dim3(kPullBlocks), dim3(kPullThreads), 0, g->early_stream,
+                       reinterpret_cast<const u32x4*>(g->h_stage), reinterpret_cast<u32x4*>(g->d_blob), segs);
+    if (hipGetLastError() == hipSuccess) g->prepulled = upto;
+}
+
 int gdec_issue(hjd_gdec* g, void* const* d_outs, const int32_t* pitches, int16_t* coefs_out, int64_t* block_offsets,
                hipStream_t s, const HostCopy* host = nullptr)
 {
@@ -2821,8 +2863,9 @@ int gdec_issue(hjd_gdec* g, void* const* d_outs, const int32_t* pitches, int16_t
         }
         uint8_t* dst = g->d_blob + g->caps.data + p.data_off;
         if (pull && segs.n < kPullSegs) {
-            segs.off[segs.n] = (g->caps.data + p.data_off) / 16;
-            segs.words[segs.n] = (hi - p.data_off + 15) / 16;
+            const size_t pre = i == 0 ? g->prepulled : 0;   // (frame 0 starts the data area)
+            segs.off[segs.n] = (g->caps.data + p.data_off + pre) / 16;
+            segs.words[segs.n] = (hi - p.data_off - pre + 15) / 16;
             ++segs.n;
         } else {
             HJD_HIP(hipMemcpyAsync(dst, g->h_stage + g->caps.data + p.data_off, hi - p.data_off, hipMemcpyHostToDevice, s));
@@ -2910,8 +2953,15 @@ int gdec_run(hjd_gdec* g, const uint8_t* const* datas, const size_t* sizes, int 
     int rc = g->wait_staging();
     if (rc) return rc;
     const auto t1 = std::chrono::steady_clock::now();
+    g->early = g->spec && n == 1;   // a lone image may be pulled while it is destuffed
+    g->early_stream = s;
+    g->prepulled = 0;
     rc = g->stage_frames(datas, sizes, n);
-    if (rc) return rc;
+    g->early = false;
+    if (rc) {
+        if (g->prepulled) (void)hipStreamSynchronize(s);   // an early pull still reads the staging
+        return rc;
+    }
     const auto t2 = std::chrono::steady_clock::now();
     rc = gdec_issue(g, d_outs, pitches, coefs_out, block_offsets, s);
     if (rc) return rc;
