@@ -70,24 +70,19 @@ def explain(orig: bytes, d: bytes, host_err: str, info) -> str:
     return "unexplained"
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--mutants", type=int, default=2000)
-    ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--json")
-    ap.add_argument("--keep")
-    a = ap.parse_args()
+def classify(data_list, mutants, seed, keep=None):
+    """Mutate and classify; returns (counts, explanations of ref_accepts_only,
+    examples per divergent class)."""
     import ocljpegdecoder_amd as hjd
     import oracle_py as O
     from test_truncation import _ref_decode
-    rng = np.random.default_rng(a.seed)
-    srcs = [open(os.path.join(O.GOLDEN, n + ".jpg"), "rb").read() for n in FILES]
+    rng = np.random.default_rng(seed)
     cnt = collections.Counter()
     why = collections.Counter()
     examples = collections.defaultdict(list)
-    for i in range(a.mutants):
-        k = i % len(srcs)
-        data = srcs[k]
+    for i in range(mutants):
+        k = i % len(data_list)
+        name, data = data_list[k]
         so = hjd.parse(data).scan_offset
         d = mutate(data, so, rng)
         ref_ok, cap = _ref_decode(d)
@@ -109,11 +104,24 @@ def main():
         if cls == "ref_accepts_only":
             why[explain(data, d, err, hjd.parse(data))] += 1
         if cls not in ("both_reject", "both_accept_equal"):
-            examples[cls].append({"mutant": i, "file": FILES[k], "host_error": err[-120:]})
-            if a.keep:
-                os.makedirs(a.keep, exist_ok=True)
-                with open(os.path.join(a.keep, f"{cls}_{i}.jpg"), "wb") as f:
+            examples[cls].append({"mutant": i, "file": name, "host_error": err[-120:]})
+            if keep:
+                os.makedirs(keep, exist_ok=True)
+                with open(os.path.join(keep, f"{cls}_{i}.jpg"), "wb") as f:
                     f.write(d)
+    return cnt, why, examples
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mutants", type=int, default=2000)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--json")
+    ap.add_argument("--keep")
+    a = ap.parse_args()
+    import oracle_py as O
+    srcs = [(n, open(os.path.join(O.GOLDEN, n + ".jpg"), "rb").read()) for n in FILES]
+    cnt, why, examples = classify(srcs, a.mutants, a.seed, a.keep)
     out = {"mutants": a.mutants, "seed": a.seed, "counts": dict(cnt),
            "ref_accepts_only_explained": dict(why),
            "examples": {k: v[:20] for k, v in examples.items()}}
