@@ -48,3 +48,29 @@ def test_single_image_default_is_speculative(hjd, ctx, monkeypatch):
     import oracle_py as O
     np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32),
                                   O.decode_q16(ref, info.qt, info.width, info.height, info.sampling))
+
+
+def test_early_pull_and_a_late_destuff_error(hjd, ctx, monkeypatch):
+    """A lone large scan is pulled to the GPU in two parts, the first while the
+    host still destuffs (gdec_early_pull).  A wrong RSTn near the end fails the
+    host destuff after that first pull; the same decoder then decodes a good
+    file exactly (the early pull of the failed call cannot leak into it)."""
+    monkeypatch.delenv("HJD_SYNC_SPEC", raising=False)
+    import torch
+    import oracle_py as O
+    good = E._pil(1920, 1080, 95, 2, seed=71, restart_marker_blocks=8)
+    info = hjd.parse(good)
+    assert len(good) - info.scan_offset >= 256 << 10   # the early pull's threshold
+    at = good.rindex(b"\xff\xd0", 0, len(good) - 64)    # a late RST0
+    bad = good[:at + 1] + bytes([0xD0 + (good[at + 1] - 0xD0 + 3) % 8]) + good[at + 2:]
+    assert at > info.scan_offset + (len(good) - info.scan_offset) * 3 // 4
+    out = torch.full((info.height, info.width), -1, dtype=torch.int32, device="cuda")
+    ref, rinfo = hjd.decode_coefs(good)
+    exp = O.decode_q16(ref, rinfo.qt, rinfo.width, rinfo.height, rinfo.sampling)
+    with hjd.GpuDecoder(ctx, 1, len(good), info.nblocks) as gd:
+        for _ in range(2):
+            with pytest.raises(Exception, match="expected RST"):
+                gd.decode([bad], [out])
+            gd.decode([good], [out])
+            assert gd.sync()[0] & ~1 == 0
+            np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), exp)
