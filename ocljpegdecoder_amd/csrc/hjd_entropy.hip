@@ -471,7 +471,7 @@ struct EntBatchDev {
     uint8_t* cmap;               // [sub][kSlotRow]
     uint8_t* cslot;              // [sub] the verified chain's slot (ent_chain_lb_kernel / ent_chain_kernel)
     uint32_t spec_lead;          // lead-in of the spec runs (bits)
-    uint32_t* chainfn;           // [frame][chain_chunks][5] look-back words of the chunks (ent_chain_lb_kernel)
+    uint32_t* chainfn;           // [frame][chain_chunks][kLbWords] look-back words of the chunks (ent_chain_lb_kernel)
     uint32_t* chain_broken;      // [frame] chain_epoch: the chain leaves its slots somewhere (serial walk with repairs)
     uint32_t chain_chunks;       // chunks of the frame with the most subsequences (grid width)
     uint32_t chain_epoch;        // 1 .. 2^24 - 1, new per launch: tags the look-back words (no clearing)
@@ -1092,9 +1092,10 @@ __global__ __launch_bounds__(kGroupSubs) void ent_cand_kernel(EntBatchDev b)
 // Maps and functions are rows of kSlotRow bytes handled as 5 dwords; a lookup
 // selects its byte in registers (LDS byte reads cost ~5x more here).
 constexpr int kChainThreads = 512;
-constexpr int kChainRows = 8;                                  // rows per thread and chunk
-constexpr int kChainChunk = kChainThreads * kChainRows;        // 4096 subsequences
+constexpr int kChainRows = 2;                                  // rows per thread and chunk
+constexpr int kChainChunk = kChainThreads * kChainRows;        // 1024 subsequences
 constexpr int kRowWords = kSlotRow / 4;
+constexpr int kLbWords = 8;   // look-back words per chunk (ent_chain_lb_kernel)
 
 struct ChainLds {
     uint32_t rows[kChainChunk][kRowWords];      // the chunk's slot maps
@@ -1151,7 +1152,7 @@ __device__ __forceinline__ SlotRow slot_ident()
 __device__ __forceinline__ void chunk_load(uint32_t (*rows)[kRowWords], const uint8_t* cm, uint32_t c0, uint32_t cn,
                                            int tid)
 {
-    constexpr int kWords = kChainChunk * kRowWords / kChainThreads;   // 40
+    constexpr int kWords = kChainChunk * kRowWords / kChainThreads;   // 10
     const uint32_t* src = reinterpret_cast<const uint32_t*>(cm + static_cast<uint64_t>(c0) * kSlotRow);
     uint32_t* dst = &rows[0][0];
     const uint32_t nw = cn * kRowWords;
@@ -1198,14 +1199,14 @@ __device__ __forceinline__ uint32_t chunk_write_slots(const uint32_t (*rows)[kRo
 {
     const uint32_t r0 = static_cast<uint32_t>(tid) * kChainRows;
     uint32_t s = slot;
-    uint32_t packed[kChainRows / 4] = {};
+    uint32_t packed[(kChainRows + 3) / 4] = {};
 #pragma unroll
     for (int i = 0; i < kChainRows; ++i) {
         packed[i >> 2] |= (s & 0xFFu) << ((i & 3) * 8);
         if (r0 + i < cn) s = row_get(row_load(rows[r0 + i]), s);
     }
     uint8_t* out = cslot + base + r0;
-    if (r0 + kChainRows <= cn && ((base + r0) & 3) == 0) {
+    if (kChainRows % 4 == 0 && r0 + kChainRows <= cn && ((base + r0) & 3) == 0) {
 #pragma unroll
         for (int i = 0; i < kChainRows / 4; ++i) reinterpret_cast<uint32_t*>(out)[i] = packed[i];
     } else {
@@ -1305,15 +1306,17 @@ __global__ __launch_bounds__(kChainThreads) void ent_chain_kernel(EntBatchDev b)
 }
 
 // ---- the chain, chunks in parallel (the case without repairs) -----------------
-// ent_chain_kernel's walk takes its chunks one after another (~20 us each; a
-// lone FHD frame has four).  Where no repair is needed the chunks are
+// ent_chain_kernel's walk takes its chunks one after another (a lone FHD
+// frame has 16 of 1024 subsequences; 1024 measured best for the look-back
+// kernel: 17.3 us per FHD frame against 20.0 at 2048 and 19.8 at 512).  Where no repair is needed the chunks are
 // independent given their entering slot, so one kernel over (chunk, frame)
 // runs them side by side with a decoupled look-back: every chunk composes its
-// maps into one function (the scan), then thread 0 waits for its predecessor's
-// exit slot (a look-back word tagged with the launch's epoch, so nothing is
-// cleared between launches), publishes its own exit -- the only serial part --
-// and the chunk writes its rows' slots.  A chunk whose predecessor has not
-// published yet was dispatched after it (lower blockIdx.x first), so the wait
+// maps into one function (the scan) and publishes it, then thread 0 finds the
+// slot entering the chunk from the nearest published exit before it and the
+// published maps in between (look-back words tagged with the launch's epoch,
+// so nothing is cleared between launches), publishes its own exit, and the
+// chunk writes its rows' slots.  A chunk whose predecessor has published
+// nothing yet was dispatched after it (lower blockIdx.x first), so the wait
 // ends.  Each chunk then reduces the chain statistics of the groups it holds:
 // a group's part in its first chunk into agg, its part in the next into agg2
 // (so no chunk waits for another's slots).  A chunk that finds the chain
@@ -1368,18 +1371,63 @@ __global__ __launch_bounds__(kChainThreads) void ent_chain_lb_kernel(EntBatchDev
     chunk_load(L.rows, b.cmap + static_cast<uint64_t>(F.sub_base) * kSlotRow, c0, cn, tid);
     __syncthreads();
     const int cur = chunk_scan(L.rows, L.fn, cn, tid);
-    if (tid == 0) {   // look-back: the slot entering this chunk, then this chunk's exit
-        uint32_t* word = b.chainfn + (static_cast<uint64_t>(f) * b.chain_chunks + c) * kRowWords;
-        uint32_t carry = 0;
-        if (c > 0) {
-            uint32_t v;
-            while (((v = __hip_atomic_load(word - kRowWords, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) >> 8) !=
-                   b.chain_epoch)
-                __builtin_amdgcn_s_sleep(1);
-            carry = v & 0xFFu;
+    // look-back (a word row per chunk: [0] epoch << 8 | exit slot, [1] epoch
+    // once [2..6], the chunk's composed map, are written).  The map is published
+    // first; the entry slot is then found by walking back to the nearest
+    // published exit (chunk 0's entry is slot 0) and applying the maps of the
+    // chunks in between, so no chunk waits for its predecessor's exit.
+    uint32_t* const lb = b.chainfn + static_cast<uint64_t>(f) * b.chain_chunks * kLbWords;
+    if (tid == 0) {   // (one thread writes the map and releases it)
+        for (int i = 0; i < kRowWords; ++i) lb[c * kLbWords + 2 + i] = L.fn[cur][kChainThreads - 1][i];
+        __hip_atomic_store(lb + c * kLbWords + 1, b.chain_epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (tid < 64 && c <= 64) {   // wave 0: lane i < c reads chunk i's words, all in flight together
+        const uint32_t i = static_cast<uint32_t>(tid);
+        uint32_t ex = 0, m[kRowWords] = {};
+        bool ready = i >= c;
+        while (!ready) {
+            ex = __hip_atomic_load(lb + i * kLbWords, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            ready = (ex >> 8) == b.chain_epoch ||
+                    __hip_atomic_load(lb + i * kLbWords + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == b.chain_epoch;
+            if (!ready) __builtin_amdgcn_s_sleep(1);
         }
+        const bool has_exit = i < c && (ex >> 8) == b.chain_epoch;
+        if (i < c && !has_exit)
+            for (int k = 0; k < kRowWords; ++k) m[k] = lb[i * kLbWords + 2 + k];
+        // from the last chunk before c with a published exit (else chunk 0,
+        // entered at slot 0) through the maps of the chunks after it
+        const uint64_t ballot = __ballot(has_exit);
+        const int last = ballot ? 63 - __builtin_clzll(ballot) : -1;
+        uint32_t sl = last >= 0 ? static_cast<uint32_t>(__shfl(static_cast<int>(ex & 0xFFu), last)) : 0u;
+        for (int j = last + 1; j < static_cast<int>(c); ++j) {   // (uniform bounds: the whole wave shuffles)
+            SlotRow r;
+#pragma unroll
+            for (int k = 0; k < kRowWords; ++k) r.w[k] = static_cast<uint32_t>(__shfl(static_cast<int>(m[k]), j));
+            if (sl != kNoCand) sl = row_get(r, sl);
+        }
+        if (tid == 0) {
+            const uint32_t exit = sl == kNoCand ? kNoCand : row_get(row_load(L.fn[cur][kChainThreads - 1]), sl);
+            __hip_atomic_store(lb + c * kLbWords, (b.chain_epoch << 8) | exit, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            L.carry = sl;
+        }
+    } else if (tid == 0 && c > 64) {   // a long frame: thread 0 walks back
+        uint32_t j = c, carry = 0;   // carry: the slot entering chunk j
+        while (j > 0) {
+            const uint32_t v = __hip_atomic_load(lb + (j - 1) * kLbWords, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            if ((v >> 8) == b.chain_epoch) {
+                carry = v & 0xFFu;
+                break;
+            }
+            if (__hip_atomic_load(lb + (j - 1) * kLbWords + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) ==
+                b.chain_epoch)
+                --j;   // its map is there: look further back
+            else
+                __builtin_amdgcn_s_sleep(1);
+        }
+        for (; j < c; ++j)   // forward through the maps of chunks j .. c-1
+            if (carry != kNoCand) carry = row_get(row_load(lb + j * kLbWords + 2), carry);
         const uint32_t exit = carry == kNoCand ? kNoCand : row_get(row_load(L.fn[cur][kChainThreads - 1]), carry);
-        __hip_atomic_store(word, (b.chain_epoch << 8) | exit, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(lb + c * kLbWords, (b.chain_epoch << 8) | exit, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         L.carry = carry;
     }
     __syncthreads();
@@ -2654,10 +2702,10 @@ int gdec_alloc(hjd_gdec* g)
         // chunk functions: [entropy frame][chunks of the largest frame]
         const size_t ef = kMaxScans * static_cast<size_t>(g->caps.max_frames);
         g->chain_fn_rows = static_cast<int64_t>(ef * (n / kChainChunk + 1));
-        HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_chainfn), 4 * kRowWords * static_cast<size_t>(g->chain_fn_rows)));
+        HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_chainfn), 4 * kLbWords * static_cast<size_t>(g->chain_fn_rows)));
         HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_chain_broken), 4 * ef));
         HJD_HIP(hipMemset(g->d_chain_broken, 0, 4 * ef));
-        HJD_HIP(hipMemset(g->d_chainfn, 0, 4 * kRowWords * static_cast<size_t>(g->chain_fn_rows)));
+        HJD_HIP(hipMemset(g->d_chainfn, 0, 4 * kLbWords * static_cast<size_t>(g->chain_fn_rows)));
         HJD_HIP(hipMalloc(reinterpret_cast<void**>(&g->d_agg2), sizeof(SubStats) * static_cast<size_t>(g->caps.max_wgs)));
     }
     HJD_HIP(hipEventCreateWithFlags(&g->staged, hipEventDisableTiming));
