@@ -470,7 +470,7 @@ __host__ __device__ __forceinline__ uint32_t long_code_entry(const HuffLut& t, u
 // without a window reload per piece.  The marks are taken between passes of
 // the unit loop (one pass per mark), not inside it: a mark test in the loop
 // made every unit dearer (gfx950, same box: spec 118 vs 100 us, cand 147 vs
-// 115 us per FHD frame; profiles/r06y_*).
+// 115 us per FHD frame; profiles/r06yz_fhd420_kernel_medians.json).
 template <bool kWrite, int kMarks = 0>
 __host__ __device__ __forceinline__ uint64_t run(const RunCtx& c, uint64_t entry, uint32_t stop, SubStats& st,
                                                  RunOut* out, const uint32_t* mpos = nullptr,
