@@ -807,20 +807,38 @@ __device__ __forceinline__ SubStats shfl_down_stats(const SubStats& s, int d)
     return r;
 }
 
-// Ordered inclusive scan of one value per thread over the workgroup (LDS).
+__device__ __forceinline__ SubStats shfl_up_stats(const SubStats& s, int d)
+{
+    SubStats r;
+    r.nblk = static_cast<uint32_t>(__shfl_up(static_cast<int>(s.nblk), d));
+    r.flags = static_cast<uint32_t>(__shfl_up(static_cast<int>(s.flags), d));
+    r.dc[0] = __shfl_up(s.dc[0], d);
+    r.dc[1] = __shfl_up(s.dc[1], d);
+    r.dc[2] = __shfl_up(s.dc[2], d);
+    return r;
+}
+
+// Ordered inclusive scan of one value per thread over the workgroup: each wave
+// scans its 64 lanes by shuffles, then the waves' totals are combined through
+// LDS (two barriers instead of two per step).  On return buf[t] holds thread
+// t's inclusive result and the workgroup is synchronised.
 template <int N = kGroupSubs>
 __device__ __forceinline__ SubStats block_scan_inclusive(SubStats v, SubStats* buf, int tid)
 {
+    static_assert(N % 64 == 0 && N / 64 <= 16, "whole waves");
+    const int lane = tid & 63, wv = tid >> 6;
+    for (int d = 1; d < 64; d <<= 1) {
+        const SubStats o = shfl_up_stats(v, d);
+        if (lane >= d) v = stats_combine(o, v);
+    }
+    __shared__ SubStats wsum[N / 64];
+    if (lane == 63) wsum[wv] = v;
+    __syncthreads();
+    SubStats pre = stats_identity();
+    for (int w = 0; w < wv; ++w) pre = stats_combine(pre, wsum[w]);
+    v = stats_combine(pre, v);
     buf[tid] = v;
     __syncthreads();
-    for (int d = 1; d < N; d <<= 1) {
-        SubStats o = v;
-        if (tid >= d) o = stats_combine(buf[tid - d], v);
-        __syncthreads();
-        buf[tid] = o;
-        v = o;
-        __syncthreads();
-    }
     return v;
 }
 
