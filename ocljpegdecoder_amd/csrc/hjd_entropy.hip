@@ -2060,9 +2060,13 @@ void emulate_spec_sync(const EntBatchDev& b)
                 }
             fprintf(stderr, "chain: nsub %u repairs %d; level-0 candidates -> spec %d, overflow %d, none %d\n", n,
                     nrepair, novf[0], novf[1], novf[kOvfLevels + 1]);
-            int chain_ovf = 0;   // subsequences the verified chain enters through an overflow slot
-            for (uint32_t k = 0; k < n; ++k) chain_ovf += b.cslot[F.sub_base + k] >= F.bpm;
-            fprintf(stderr, "chain: %d subsequences entered through an overflow or repair slot\n", chain_ovf);
+            int chain_lvl[kOvfLevels + 2] = {};   // the verified chain's slots by level (last: repair)
+            for (uint32_t k = 0; k < n; ++k) {
+                const uint32_t sl = b.cslot[F.sub_base + k];
+                ++chain_lvl[sl >= static_cast<uint32_t>(kSlots) ? kOvfLevels + 1 : sl / F.bpm];
+            }
+            fprintf(stderr, "chain: slots by level %d / %d / %d, repair %d\n", chain_lvl[0], chain_lvl[1], chain_lvl[2],
+                    chain_lvl[3]);
             // ent_cand_kernel's serial bits per thread (k, c) and per wave (64 lanes of one c)
             std::vector<uint32_t> cost, wmax;
             uint32_t nlev[kOvfLevels + 1] = {}, nmiss = 0;
@@ -2315,6 +2319,7 @@ struct hjd_gdec {
     int64_t last_host_scan_bytes = 0;   // scan bytes the host CPU read + wrote for the staged frames
     bool pending = false;
     bool staged_by_done = false;        // the last issue pulled its staging: `done` also means staged
+    uint32_t batch_sub_bits = 0;        // S of the batch being assembled (0: caps.sub_bits)
     hipStream_t early_stream = nullptr; // this call's stream when its lone image may be pulled early
     bool early = false;                 // early pull enabled for this call
     size_t prepulled = 0;               // data-area bytes of frame 0 already pulled (gdec_early_pull)
@@ -2499,7 +2504,7 @@ int hjd_gdec::assemble(uint8_t* blob, int16_t* coefs, int64_t* block_offsets, vo
                        const int32_t* pitches, EntBatchDev& d)
 {
     const int n = static_cast<int>(frames.size());
-    const uint32_t S = static_cast<uint32_t>(caps.sub_bits);
+    const uint32_t S = batch_sub_bits ? batch_sub_bits : static_cast<uint32_t>(caps.sub_bits);
     // entropy frames: the n JPEGs' (first) scans, then the further scans of
     // multi-scan files (scan_file: their JPEG), all writing the JPEG's blocks
     std::vector<const Prepared*> ents;
@@ -2795,6 +2800,10 @@ struct HostCopy {
 // 64 workgroups beat 256 and 1024), and the kernel replaces the copy calls.
 // Staging and blob share their layout, so a segment is an offset and a length
 // (16-B multiples: the header is kAlign-aligned, a data run ends in its pad).
+constexpr uint64_t kDenseBitsPerBlock = 200;   // (a q90 FHD 4:2:0 frame: 164; q95: 232; q100: 436)
+constexpr uint32_t kDenseSubBits = kDefaultSubBits / 2;
+constexpr uint64_t kVeryDenseBitsPerBlock = 320;
+constexpr uint32_t kVeryDenseSubBits = 4 * kDefaultSubBits;
 constexpr int kPullSegs = 4;
 constexpr int kPullBlocks = 64;
 constexpr int kPullThreads = 256;
@@ -2839,6 +2848,32 @@ int gdec_issue(hjd_gdec* g, void* const* d_outs, const int32_t* pitches, int16_t
     HJD_HIP(hipSetDevice(g->device));
     const int n = static_cast<int>(g->frames.size());
     int16_t* coefs = coefs_out ? coefs_out : g->d_coefs;
+    // Dense scans sync slowly: at S = 512 a q95 FHD frame breaks the
+    // speculative chain ~200 times and a q100 one ~3,600 times, each break a
+    // serial single-thread repair (8 ms and worse per image).  Above
+    // kDenseBitsPerBlock a latency decoder takes the round-based sync instead,
+    // at longer subsequences the denser the scan (q95 FHD 4:2:0: 1.4 ms at
+    // S = 1024; q100: 7.7 ms at 8192 against 14 at 2048; tools/fhd_env_sweep.py,
+    // profiles/r06zt_dense_latency.json).  Never shorter than the decoder's S
+    // (its capacity is sized for that).
+    bool spec = g->spec;
+    g->batch_sub_bits = 0;
+    if (spec) {
+        uint64_t bits = 0, blocks = 0;
+        for (const Prepared& p : g->frames) {
+            bits += p.data_bits;
+            blocks += static_cast<uint64_t>(p.nblocks);
+            for (const Prepared& q : p.more) {
+                bits += q.data_bits;
+                blocks += static_cast<uint64_t>(q.nblocks);
+            }
+        }
+        if (bits > kDenseBitsPerBlock * blocks) {
+            spec = false;
+            const uint32_t want = bits > kVeryDenseBitsPerBlock * blocks ? kVeryDenseSubBits : kDenseSubBits;
+            g->batch_sub_bits = std::max(want, static_cast<uint32_t>(g->caps.sub_bits));
+        }
+    }
     EntBatchDev b;
     int rc = g->assemble(g->d_blob, coefs, block_offsets, d_outs, pitches, b);
     if (rc) return rc;
@@ -2854,7 +2889,7 @@ int gdec_issue(hjd_gdec* g, void* const* d_outs, const int32_t* pitches, int16_t
     b.raw = g->d_raw;
     b.tiles = g->d_tiles;
     b.steps_g = g->d_steps;
-    if (g->spec) {
+    if (spec) {
         b.spec = g->d_spec;
         b.cand = g->d_cand;
         b.cmap = g->d_cmap;
