@@ -1299,9 +1299,11 @@ __device__ __forceinline__ void chain_walk(const EntBatchDev& b, uint32_t f, Cha
                 __syncthreads();
                 if (tid == 0) L.tables_loaded = 1;
             }
-            if (tid == 0)
+            if (tid == 0) {   // (the status bit tells the host a repair ran: hjd_gdec_sync)
                 chain_repair(make_ctx(b, F, L.tabs, L.blocks, L.steps), b, F, static_cast<uint32_t>(brk >> 8),
                              static_cast<uint32_t>(brk & 0xFF));
+                atomicOr(&b.status[f], kStatusFallback);
+            }
         }
         // the chain's slot of each of this thread's rows
         const uint32_t s = chunk_write_slots(L.rows, b.cslot, F.sub_base + c0, cn, tid, slot);
@@ -2051,6 +2053,7 @@ void emulate_spec_sync(const EntBatchDev& b)
             prev = slot;
             slot = b.cmap[row * kSlotRow + slot];
         }
+        if (nrepair) b.status[f] |= kStatusFallback;
         if (getenv("HJD_EMU_ROUNDS")) {
             int novf[kOvfLevels + 2] = {};
             for (uint32_t k = 0; k < n; ++k)
@@ -2268,10 +2271,22 @@ void emulate(const EntBatchDev& b)
 }  // namespace
 
 // Lead-in of the speculative sync's spec runs (HJD_SPEC_LEAD overrides; tuning).
-uint32_t spec_lead_bits()
+// A chain breaks where none of a subsequence's spec runs has met the true
+// decode by its checkpoint; a longer lead-in makes that rarer and costs every
+// spec run its length.  Measured FHD single images (ms at W = 512 / 1536,
+// profiles/r06zx_spec_lead.json): bench q90 4:2:0 0.40 / 0.46 (no break),
+// another q90 4:2:0 at the same 164 bits per block 0.61 / 0.46 (2 breaks),
+// q90 4:4:4 0.96 / 0.47 (9 breaks), q93 4:2:0 1.10 / 0.75 (19 / 3 breaks;
+// none at 2048, host emulation).  Bits per block do not tell these apart, so
+// the decoder goes by its own history: a batch whose chain needed a repair
+// moves the next batches one step up the ladder, and kLeadBatches clean
+// batches move them one step down (a camera's frames look alike).
+constexpr uint32_t kLeadLadder[] = {512, 1536, 2560};
+constexpr uint32_t kLeadSteps = sizeof(kLeadLadder) / sizeof(kLeadLadder[0]), kLeadBatches = 32;
+uint32_t spec_lead_bits(uint32_t step)
 {
     const char* e = getenv("HJD_SPEC_LEAD");   // read per batch (~100 ns): tests switch it in-process
-    return e ? static_cast<uint32_t>(atoi(e)) : 512u;
+    return e ? static_cast<uint32_t>(atoi(e)) : kLeadLadder[step < kLeadSteps ? step : kLeadSteps - 1];
 }
 
 // ---------------------------------------------------------------------------
@@ -2320,6 +2335,9 @@ struct hjd_gdec {
     bool pending = false;
     bool staged_by_done = false;        // the last issue pulled its staging: `done` also means staged
     uint32_t batch_sub_bits = 0;        // S of the batch being assembled (0: caps.sub_bits)
+    bool batch_spec = false;            // the pending batch took the speculative sync
+    uint32_t lead_step = 0;             // spec_lead_bits' ladder step for the next batch
+    uint32_t lead_left = 0;             // clean batches before it steps down
     hipStream_t early_stream = nullptr; // this call's stream when its lone image may be pulled early
     bool early = false;                 // early pull enabled for this call
     size_t prepulled = 0;               // data-area bytes of frame 0 already pulled (gdec_early_pull)
@@ -2874,6 +2892,7 @@ int gdec_issue(hjd_gdec* g, void* const* d_outs, const int32_t* pitches, int16_t
             g->batch_sub_bits = std::max(want, static_cast<uint32_t>(g->caps.sub_bits));
         }
     }
+    g->batch_spec = spec;
     EntBatchDev b;
     int rc = g->assemble(g->d_blob, coefs, block_offsets, d_outs, pitches, b);
     if (rc) return rc;
@@ -2894,7 +2913,7 @@ int gdec_issue(hjd_gdec* g, void* const* d_outs, const int32_t* pitches, int16_t
         b.cand = g->d_cand;
         b.cmap = g->d_cmap;
         b.cslot = g->d_cslot;
-        b.spec_lead = spec_lead_bits();
+        b.spec_lead = spec_lead_bits(g->lead_step);
         if (static_cast<int64_t>(b.chain_chunks) * b.nframes <= g->chain_fn_rows) {
             b.chainfn = g->d_chainfn;
             b.chain_broken = g->d_chain_broken;
@@ -3229,10 +3248,20 @@ int hjd_gdec_sync(hjd_gdec* g, int32_t* status)
     for (size_t e = 0; e < g->scan_file.size(); ++e)   // a JPEG's further scans
         g->h_status[g->scan_file[e]] |= g->h_status[g->nframes_issued + e];
     int bad = 0;
+    bool repaired = false;
     for (int i = 0; i < g->nframes_issued; ++i) {
         const uint32_t s = g->h_status[i] & ~kStatusFallback;
         if (status) status[i] = static_cast<int32_t>(g->h_status[i]);
         if (s) ++bad;
+        repaired = repaired || (g->h_status[i] & kStatusFallback);
+    }
+    if (g->batch_spec) {   // the lead-in of the next batches (spec_lead_bits)
+        if (repaired) {
+            g->lead_step = std::min(g->lead_step + 1, kLeadSteps - 1);
+            g->lead_left = kLeadBatches;
+        } else if (g->lead_step && --g->lead_left == 0) {
+            g->lead_left = --g->lead_step ? kLeadBatches : 0;
+        }
     }
     g->pending = false;
     if (bad) return set_error(HJD_E_INVALID, "%d of %d frames had corrupt entropy data", bad, g->nframes_issued);
@@ -3491,7 +3520,7 @@ int hjd_debug_entropy_emulate(const uint8_t* data, size_t size, int sub_bits, in
         b.cmap = g.e_cmap.data();
         g.e_cslot.assign(n + 16, 0);
         b.cslot = g.e_cslot.data();
-        b.spec_lead = spec_lead_bits();
+        b.spec_lead = spec_lead_bits(0);
     }
     b.entries = g.e_entries.data();
     b.stats = g.e_stats.data();

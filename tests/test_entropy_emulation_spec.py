@@ -41,3 +41,17 @@ def test_reference_sample_all_leads(hjd, monkeypatch):
             ref, _ = hjd.decode_coefs(data)
             got, status = hjd.emulate_entropy(data, 64)
             np.testing.assert_array_equal(got, ref, err_msg=f"{name} lead={lead}")
+
+
+def test_repair_sets_status_bit_and_long_leads_avoid_it(hjd, monkeypatch):
+    """The premise of the decoder's lead-in ladder (spec_lead_bits): status bit
+    0 reports that the chain needed a repair; this q90 4:4:4 FHD frame breaks
+    9 times at the short lead-in (512 bits) and never at the ladder's next
+    step (1536).  The GPU test of the ladder relies on exactly this."""
+    data = E._pil(1920, 1080, 90, 0, seed=5)
+    ref, _ = hjd.decode_coefs(data)
+    for lead, bit in ((512, 1), (1536, 0)):
+        monkeypatch.setenv("HJD_SPEC_LEAD", str(lead))
+        got, status = hjd.emulate_entropy(data, 512)
+        np.testing.assert_array_equal(got, ref, err_msg=f"lead={lead}")
+        assert status == bit, (lead, status)

@@ -50,6 +50,28 @@ def test_single_image_default_is_speculative(hjd, ctx, monkeypatch):
                                   O.decode_q16(ref, info.qt, info.width, info.height, info.sampling))
 
 
+def test_lead_ladder_after_a_repair(hjd, ctx, monkeypatch):
+    """A latency decoder whose chain needed a repair (status bit 0) decodes the
+    next frames with a longer lead-in (spec_lead_bits' ladder): this frame
+    breaks at 512 bits and not at 1536 (pinned by the emulation,
+    test_entropy_emulation_spec.py), so the first call reports a repair and
+    the next ones none; every call's coefficients are exact."""
+    monkeypatch.delenv("HJD_SYNC_SPEC", raising=False)
+    monkeypatch.delenv("HJD_SPEC_LEAD", raising=False)
+    import torch
+    d = E._pil(1920, 1080, 90, 0, seed=5)
+    ref, info = hjd.decode_coefs(d)
+    coefs = torch.empty((info.nblocks, 64), dtype=torch.int16, device="cuda")
+    bits = []
+    with hjd.GpuDecoder(ctx, 1, len(d), info.nblocks) as gd:
+        for _ in range(3):
+            coefs.fill_(0x5A5A)
+            gd.decode_coefs([d], coefs)
+            bits.append(gd.sync()[0])
+            np.testing.assert_array_equal(coefs.cpu().numpy(), ref)
+    assert bits == [1, 0, 0]
+
+
 def test_early_pull_and_a_late_destuff_error(hjd, ctx, monkeypatch):
     """A lone large scan is pulled to the GPU in two parts, the first while the
     host still destuffs (gdec_early_pull).  A wrong RSTn near the end fails the
