@@ -2819,9 +2819,11 @@ struct HostCopy {
 // Staging and blob share their layout, so a segment is an offset and a length
 // (16-B multiples: the header is kAlign-aligned, a data run ends in its pad).
 constexpr uint64_t kDenseBitsPerBlock = 200;   // (a q90 FHD 4:2:0 frame: 164; q95: 232; q100: 436)
-constexpr uint32_t kDenseSubBits = kDefaultSubBits / 2;
-constexpr uint64_t kVeryDenseBitsPerBlock = 320;
-constexpr uint32_t kVeryDenseSubBits = 4 * kDefaultSubBits;
+// the round-based S of a dense scan: the first tier whose bits per block bound
+// it (best S measured per FHD frame: q95 232 / 243 -> 1024, q97 286 / 301 and
+// q98 322 -> 2048, q99 388 and q100 436 -> 8192; profiles/r06zz_dense_sub_bits.json)
+constexpr struct { uint64_t bits_per_block; uint32_t sub_bits; } kDenseTiers[] = {
+    {260, 1024}, {360, 2048}, {0, 8192}};   // (the last: everything denser)
 constexpr int kPullSegs = 4;
 constexpr int kPullBlocks = 64;
 constexpr int kPullThreads = 256;
@@ -2870,10 +2872,10 @@ int gdec_issue(hjd_gdec* g, void* const* d_outs, const int32_t* pitches, int16_t
     // speculative chain ~200 times and a q100 one ~3,600 times, each break a
     // serial single-thread repair (8 ms and worse per image).  Above
     // kDenseBitsPerBlock a latency decoder takes the round-based sync instead,
-    // at longer subsequences the denser the scan (q95 FHD 4:2:0: 1.4 ms at
-    // S = 1024; q100: 7.7 ms at 8192 against 14 at 2048; tools/fhd_env_sweep.py,
-    // profiles/r06zt_dense_latency.json).  Never shorter than the decoder's S
-    // (its capacity is sized for that).
+    // at longer subsequences the denser the scan (kDenseTiers: q95 FHD 4:2:0
+    // 1.4 ms at S = 1024; q98 2.4 at 2048 against 6.0 at 1024; q100 7.6 at 8192
+    // against 14 at 2048; tools/fhd_env_sweep.py).  Never shorter than the
+    // decoder's S (its capacity is sized for that).
     bool spec = g->spec;
     g->batch_sub_bits = 0;
     if (spec) {
@@ -2888,7 +2890,11 @@ int gdec_issue(hjd_gdec* g, void* const* d_outs, const int32_t* pitches, int16_t
         }
         if (bits > kDenseBitsPerBlock * blocks) {
             spec = false;
-            const uint32_t want = bits > kVeryDenseBitsPerBlock * blocks ? kVeryDenseSubBits : kDenseSubBits;
+            const char* e = getenv("HJD_DENSE_SUB_BITS");   // tuning: the dense scans' S
+            constexpr size_t nt = sizeof(kDenseTiers) / sizeof(kDenseTiers[0]);
+            size_t t = 0;
+            while (t + 1 < nt && bits > kDenseTiers[t].bits_per_block * blocks) ++t;
+            const uint32_t want = e ? static_cast<uint32_t>(atoi(e)) : kDenseTiers[t].sub_bits;
             g->batch_sub_bits = std::max(want, static_cast<uint32_t>(g->caps.sub_bits));
         }
     }
