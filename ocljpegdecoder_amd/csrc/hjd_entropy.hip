@@ -472,7 +472,7 @@ struct EntBatchDev {
     uint8_t* cslot;              // [sub] the verified chain's slot (ent_chain_lb_kernel / ent_chain_kernel)
     uint32_t spec_lead;          // lead-in of the spec runs (bits)
     uint32_t* chainfn;           // [frame][chain_chunks][kLbWords] look-back words of the chunks (ent_chain_lb_kernel)
-    uint32_t* chain_broken;      // [frame] chain_epoch: the chain leaves its slots somewhere (serial walk with repairs)
+    uint32_t* chain_broken;      // non-null: the look-back chain kernel runs (its words are allocated)
     uint32_t chain_chunks;       // chunks of the frame with the most subsequences (grid width)
     uint32_t chain_epoch;        // 1 .. 2^24 - 1, new per launch: tags the look-back words (no clearing)
 };
@@ -1255,62 +1255,68 @@ __device__ __forceinline__ void group_agg(const EntBatchDev& b, const EntFrame& 
     }
 }
 
-// The serial walk of frame f by one workgroup (the chain kernel's, or the
-// look-back kernel's last chunk of a frame whose chain needs a repair).
+// Chunk [c0, c0 + cn) of frame F entered at slot `carry`, by one workgroup,
+// repairing every break on the way (tid 0 runs the repair; the chunk's maps
+// are reloaded after each, and a repair may run on into the next chunk's
+// rows): writes the chunk's cslot and returns the slot after its last row.
+__device__ __forceinline__ uint32_t walk_chunk(const EntBatchDev& b, uint32_t f, const EntFrame& F, ChainLds& L,
+                                               uint32_t c0, uint32_t cn, uint32_t carry, int tid)
+{
+    const uint32_t n = F.nsub;
+    uint8_t* cm = b.cmap + static_cast<uint64_t>(F.sub_base) * kSlotRow;
+    const uint32_t r0 = static_cast<uint32_t>(tid) * kChainRows;   // this thread's rows within the chunk
+    uint32_t slot;
+    for (;;) {
+        __syncthreads();
+        chunk_load(L.rows, cm, c0, cn, tid);
+        if (tid == 0) L.brk = ~0ull;
+        __syncthreads();
+        const int cur = chunk_scan(L.rows, L.fn, cn, tid);
+        slot = tid == 0 ? carry : (carry == kNoCand ? kNoCand : row_get(row_load(L.fn[cur][tid - 1]), carry));
+        // the first subsequence without a slot: the row whose map sends the
+        // chain's slot to none (subsequence 0's slots all exist)
+        uint32_t s = slot;
+        for (uint32_t r = r0; r < r0 + kChainRows && r < cn && s != kNoCand; ++r) {
+            const uint32_t nx = row_get(row_load(L.rows[r]), s);
+            if (nx == kNoCand && c0 + r + 1 < n) {
+                atomicMin(&L.brk, (static_cast<unsigned long long>(c0 + r + 1) << 8) | s);
+                break;
+            }
+            s = nx;
+        }
+        __syncthreads();
+        const unsigned long long brk = L.brk;
+        if (brk == ~0ull) break;
+        if (!L.tables_loaded) {   // the frame's tables, for the repair runs (rare)
+            load_tables(L.tabs, L.blocks, b.tabs + F.tab_base, F, b.frames + f, tid, kChainThreads);
+            __syncthreads();
+            fill_steps(L.steps, L.tabs, F.ntab, tid, kChainThreads);
+            __syncthreads();
+            if (tid == 0) L.tables_loaded = 1;
+        }
+        if (tid == 0) {   // (the status bit tells the host a repair ran: hjd_gdec_sync)
+            chain_repair(make_ctx(b, F, L.tabs, L.blocks, L.steps), b, F, static_cast<uint32_t>(brk >> 8),
+                         static_cast<uint32_t>(brk & 0xFF));
+            atomicOr(&b.status[f], kStatusFallback);
+        }
+    }
+    // the chain's slot of each of this thread's rows
+    const uint32_t s = chunk_write_slots(L.rows, b.cslot, F.sub_base + c0, cn, tid, slot);
+    __syncthreads();
+    if (r0 < cn && (r0 + kChainRows >= cn)) L.carry = s;   // the thread holding the chunk's last row
+    __syncthreads();
+    return L.carry;
+}
+
+// The serial walk of frame f by one workgroup (decoders without look-back words).
 __device__ __forceinline__ void chain_walk(const EntBatchDev& b, uint32_t f, ChainLds& L, int tid)
 {
     const EntFrame F = b.frames[f];
     const uint32_t n = F.nsub;
-    uint8_t* cm = b.cmap + static_cast<uint64_t>(F.sub_base) * kSlotRow;
-    if (tid == 0) {
-        L.carry = 0;
-        L.tables_loaded = 0;
-    }
-    for (uint32_t c0 = 0; c0 < n; c0 += kChainChunk) {
-        const uint32_t cn = n - c0 < static_cast<uint32_t>(kChainChunk) ? n - c0 : kChainChunk;
-        const uint32_t r0 = static_cast<uint32_t>(tid) * kChainRows;   // this thread's rows within the chunk
-        uint32_t slot;
-        for (;;) {
-            __syncthreads();
-            chunk_load(L.rows, cm, c0, cn, tid);
-            if (tid == 0) L.brk = ~0ull;
-            __syncthreads();
-            const int cur = chunk_scan(L.rows, L.fn, cn, tid);
-            const uint32_t carry = L.carry;
-            slot = tid == 0 ? carry : (carry == kNoCand ? kNoCand : row_get(row_load(L.fn[cur][tid - 1]), carry));
-            // the first subsequence without a slot: the row whose map sends the
-            // chain's slot to none (subsequence 0's slots all exist)
-            uint32_t s = slot;
-            for (uint32_t r = r0; r < r0 + kChainRows && r < cn && s != kNoCand; ++r) {
-                const uint32_t nx = row_get(row_load(L.rows[r]), s);
-                if (nx == kNoCand && c0 + r + 1 < n) {
-                    atomicMin(&L.brk, (static_cast<unsigned long long>(c0 + r + 1) << 8) | s);
-                    break;
-                }
-                s = nx;
-            }
-            __syncthreads();
-            const unsigned long long brk = L.brk;
-            if (brk == ~0ull) break;
-            if (!L.tables_loaded) {   // the frame's tables, for the repair runs (rare)
-                load_tables(L.tabs, L.blocks, b.tabs + F.tab_base, F, b.frames + f, tid, kChainThreads);
-                __syncthreads();
-                fill_steps(L.steps, L.tabs, F.ntab, tid, kChainThreads);
-                __syncthreads();
-                if (tid == 0) L.tables_loaded = 1;
-            }
-            if (tid == 0) {   // (the status bit tells the host a repair ran: hjd_gdec_sync)
-                chain_repair(make_ctx(b, F, L.tabs, L.blocks, L.steps), b, F, static_cast<uint32_t>(brk >> 8),
-                             static_cast<uint32_t>(brk & 0xFF));
-                atomicOr(&b.status[f], kStatusFallback);
-            }
-        }
-        // the chain's slot of each of this thread's rows
-        const uint32_t s = chunk_write_slots(L.rows, b.cslot, F.sub_base + c0, cn, tid, slot);
-        __syncthreads();
-        if (r0 < cn && (r0 + kChainRows >= cn)) L.carry = s;   // the thread holding the chunk's last row
-    }
-    __syncthreads();
+    if (tid == 0) L.tables_loaded = 0;
+    uint32_t carry = 0;
+    for (uint32_t c0 = 0; c0 < n; c0 += kChainChunk)
+        carry = walk_chunk(b, f, F, L, c0, n - c0 < static_cast<uint32_t>(kChainChunk) ? n - c0 : kChainChunk, carry, tid);
     const int wv = tid >> 6, lane = tid & 63;
     for (uint32_t g = wv; g < frame_groups(F.nsub); g += kChainThreads / 64) {
         group_agg(b, F, g, lane);
@@ -1339,16 +1345,17 @@ __global__ __launch_bounds__(kChainThreads) void ent_chain_kernel(EntBatchDev b)
 // nothing yet was dispatched after it (lower blockIdx.x first), so the wait
 // ends.  Each chunk then reduces the chain statistics of the groups it holds:
 // a group's part in its first chunk into agg, its part in the next into agg2
-// (so no chunk waits for another's slots).  A chunk that finds the chain
-// leaving every slot marks its frame (chain_broken = epoch), and
-// the frame's last chunk to finish (a per-frame count in the batch header)
-// then walks that frame serially with its repairs (chain_walk), overwriting
-// the slots and the group statistics.
+// (so no chunk waits for another's slots).  A chunk whose path leaves every
+// slot repairs it itself (walk_chunk) before it publishes its exit; the maps
+// send the chunks after it to none, and those wait for that exit instead.
+// Breaks in different chunks are repaired side by side (the walk of a whole
+// frame by one workgroup after any break cost ~50 us per break on a q90 4:4:4
+// FHD frame).
 struct ChainParLds {
     uint32_t rows[kChainChunk][kRowWords];
     uint32_t fn[2][kChainThreads][kRowWords];
     uint8_t slots[kChainChunk];   // the chain's slot of each row
-    uint32_t carry, broken, walk;
+    uint32_t carry, broken, published;
 };
 union ChainLbLds {
     ChainParLds p;
@@ -1425,11 +1432,7 @@ __global__ __launch_bounds__(kChainThreads) void ent_chain_lb_kernel(EntBatchDev
             for (int k = 0; k < kRowWords; ++k) r.w[k] = static_cast<uint32_t>(__shfl(static_cast<int>(m[k]), j));
             if (sl != kNoCand) sl = row_get(r, sl);
         }
-        if (tid == 0) {
-            const uint32_t exit = sl == kNoCand ? kNoCand : row_get(row_load(L.fn[cur][kChainThreads - 1]), sl);
-            __hip_atomic_store(lb + c * kLbWords, (b.chain_epoch << 8) | exit, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-            L.carry = sl;
-        }
+        if (tid == 0) L.carry = sl;
     } else if (tid == 0 && c > 64) {   // a long frame: thread 0 walks back
         uint32_t j = c, carry = 0;   // carry: the slot entering chunk j
         while (j > 0) {
@@ -1446,15 +1449,33 @@ __global__ __launch_bounds__(kChainThreads) void ent_chain_lb_kernel(EntBatchDev
         }
         for (; j < c; ++j)   // forward through the maps of chunks j .. c-1
             if (carry != kNoCand) carry = row_get(row_load(lb + j * kLbWords + 2), carry);
-        const uint32_t exit = carry == kNoCand ? kNoCand : row_get(row_load(L.fn[cur][kChainThreads - 1]), carry);
-        __hip_atomic_store(lb + c * kLbWords, (b.chain_epoch << 8) | exit, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         L.carry = carry;
+    }
+    // The maps send the chain to none where a chunk before this one breaks:
+    // that chunk repairs itself and then publishes its exit, so wait for the
+    // exit of chunk c - 1 (published exits are never none, but a frame's last
+    // chunk's).  This chunk publishes its exit now unless its own path breaks.
+    if (tid == 0) {
+        uint32_t sl = L.carry;
+        while (sl == kNoCand) {
+            const uint32_t v = __hip_atomic_load(lb + (c - 1) * kLbWords, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            if ((v >> 8) == b.chain_epoch)
+                sl = v & 0xFFu;
+            else
+                __builtin_amdgcn_s_sleep(1);
+        }
+        const uint32_t exit = row_get(row_load(L.fn[cur][kChainThreads - 1]), sl);
+        L.published = exit != kNoCand || c0 + cn >= n;
+        if (L.published)
+            __hip_atomic_store(lb + c * kLbWords, (b.chain_epoch << 8) | exit, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        L.carry = sl;
     }
     __syncthreads();
     const uint32_t carry = L.carry;
+    const bool published = L.published;
     const uint32_t slot = tid == 0 ? carry : (carry == kNoCand ? kNoCand : row_get(row_load(L.fn[cur][tid - 1]), carry));
     // a row whose map sends the chain's slot to none, before the frame's last
-    // subsequence: the serial walk repairs it (chunks after it enter at none)
+    // subsequence: this chunk repairs it below (walk_chunk)
     const uint32_t r0 = static_cast<uint32_t>(tid) * kChainRows;
     uint32_t s = slot;
     for (uint32_t r = r0; r < r0 + kChainRows && r < cn; ++r) {
@@ -1466,15 +1487,22 @@ __global__ __launch_bounds__(kChainThreads) void ent_chain_lb_kernel(EntBatchDev
     }
     chunk_write_slots(L.rows, b.cslot, F.sub_base + c0, cn, tid, slot);
     __syncthreads();
-    const bool broken = L.broken || carry == kNoCand;   // here or before: the walk redoes this frame
-    if (tid == 0 && L.broken) __hip_atomic_store(&b.chain_broken[f], b.chain_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool broken = L.broken;
+    const uint8_t* slots = L.slots;
+    if (broken) {   // the walk's LDS overlays this kernel's: after the barrier above
+        if (tid == 0) U.w.tables_loaded = 0;
+        const uint32_t exit = walk_chunk(b, f, F, U.w, c0, cn, carry, tid);
+        if (tid == 0 && !published)
+            __hip_atomic_store(lb + c * kLbWords, (b.chain_epoch << 8) | exit, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        slots = b.cslot + F.sub_base + c0;   // (written by walk_chunk; its last barrier orders them)
+    }
     // group statistics: each group part in this chunk, one wave per part
     const int wv = tid >> 6, lane = tid & 63;
-    const uint32_t g0 = c0 / kOwn, g1 = broken ? 0 : (c0 + cn - 1) / kOwn;
-    for (uint32_t g = g0 + static_cast<uint32_t>(wv); !broken && g <= g1; g += kChainThreads / 64) {
+    const uint32_t g0 = c0 / kOwn, g1 = (c0 + cn - 1) / kOwn;
+    for (uint32_t g = g0 + static_cast<uint32_t>(wv); g <= g1; g += kChainThreads / 64) {
         const uint32_t glo = g * kOwn, ghi = (g + 1) * kOwn < n ? (g + 1) * kOwn : n;
         const uint32_t lo = glo > c0 ? glo : c0, hi = ghi < c0 + cn ? ghi : c0 + cn;
-        const SubStats a = range_stats(b, F, lo, hi, L.slots, c0, lane);
+        const SubStats a = range_stats(b, F, lo, hi, slots, c0, lane);
         if (lane == 0) {
             const uint32_t w = F.wg_base + g;
             if (glo >= c0) {   // the group starts here
@@ -1486,19 +1514,6 @@ __global__ __launch_bounds__(kChainThreads) void ent_chain_lb_kernel(EntBatchDev
             }
         }
     }
-    // the frame's last chunk to finish walks it if some chunk found a break
-    __syncthreads();
-    if (tid == 0) {
-        const uint32_t nch = (n + kChainChunk - 1) / kChainChunk;
-        const bool last = __hip_atomic_fetch_add(b.status + b.nframes + 1 + f, 1u, __ATOMIC_ACQ_REL,
-                                                 __HIP_MEMORY_SCOPE_AGENT) == nch - 1;
-        L.walk = last && __hip_atomic_load(&b.chain_broken[f], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                             b.chain_epoch;
-    }
-    __syncthreads();
-    const bool walk = L.walk;
-    __syncthreads();   // (the walk's LDS overlays this kernel's)
-    if (walk) chain_walk(b, f, U.w, tid);
 }
 
 __global__ __launch_bounds__(256) void ent_link_kernel(EntBatchDev b)
