@@ -72,6 +72,33 @@ def test_lead_ladder_after_a_repair(hjd, ctx, monkeypatch):
     assert bits == [1, 0, 0]
 
 
+@pytest.mark.parametrize("q,sub,seed", [(95, 2, 3), (97, 0, 3), (98, 2, 3), (100, 2, 8)])
+def test_dense_single_images_take_the_round_based_tiers(hjd, ctx, monkeypatch, q, sub, seed):
+    """Latency decoders leave the speculative sync for dense scans (> 200 bits
+    per block) and run the round-based one at a longer S than their own
+    (kDenseTiers: 1024, 2048, 8192 for these four FHD frames of 232, 301,
+    322 and 436 bits per block).  Coefficients and pixels stay exact, the
+    decoder reused across calls."""
+    monkeypatch.delenv("HJD_SYNC_SPEC", raising=False)
+    monkeypatch.delenv("HJD_SPEC_LEAD", raising=False)
+    import torch
+    import oracle_py as O
+    d = E._pil(1920, 1080, q, sub, seed=seed)
+    ref, info = hjd.decode_coefs(d)
+    coefs = torch.empty((info.nblocks, 64), dtype=torch.int16, device="cuda")
+    out = torch.full((info.height, info.width), -1, dtype=torch.int32, device="cuda")
+    with hjd.GpuDecoder(ctx, 1, len(d), info.nblocks) as gd:
+        for _ in range(2):
+            coefs.fill_(0x5A5A)
+            gd.decode_coefs([d], coefs)
+            assert gd.sync()[0] & ~1 == 0
+            np.testing.assert_array_equal(coefs.cpu().numpy(), ref)
+        gd.decode([d], [out])
+        gd.sync()
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32),
+                                  O.decode_q16(ref, info.qt, info.width, info.height, info.sampling))
+
+
 def test_early_pull_and_a_late_destuff_error(hjd, ctx, monkeypatch):
     """A lone large scan is pulled to the GPU in two parts, the first while the
     host still destuffs (gdec_early_pull).  A wrong RSTn near the end fails the
