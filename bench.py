@@ -687,7 +687,7 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
         c = pcie_ceiling(torch, dev, "h2d", busy["coef_bytes_per_frame"], [1, 2])
         busy["pcie_ceiling_GBps"] = c["GBps"]
         busy["pcie_ceiling_Mpx_s"] = round(c["GBps"] * 1e9 / (busy["coef_bytes_per_frame"] / (w * h)) / 1e6, 1)
-    d2h_c = pcie_ceiling(torch, dev, "d2h", h * pitch, sorted({2, 4, nslots})) if d2h else None
+    d2h_c = pcie_ceiling(torch, dev, "d2h", h * pitch, sorted({2, 4, nslots}), host_bufs=ring) if d2h else None
     if rank == 0:
         jpeg_bytes = int(np.mean([len(d) for d in pool]))
         res = {
@@ -730,7 +730,8 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
                     "rows": d2h_c["rows"],
                     "how": "device -> pinned host copies on this GPU after the timed region, as the stream "
                            "returns frames: 2, 4 and the stream's slot count of concurrent streams, one frame's "
-                           "output per copy (plus one stream of 256 MiB copies); the best rate is the ceiling"},
+                           "output per copy, into a fresh pinned buffer and into the stream's own ring (plus one "
+                           "stream of 256 MiB copies); the best rate is the ceiling"},
                 "pipeline": busy,
                 "output_checked_vs_oracle": bool(ok),
                 "coefs_vs_reference_mcu_data": dict(pin_count, how="sha256 of each checked pool file's host "
@@ -763,20 +764,27 @@ def run_stream(args, wl, hjd, torch, dist, world, rank, dev):
         sys.exit(1)
 
 
-def pcie_ceiling(torch, dev, direction, chunk_bytes, stream_counts, total_bytes=4 << 30):
+def pcie_ceiling(torch, dev, direction, chunk_bytes, stream_counts, total_bytes=4 << 30, host_bufs=None):
     """Pinned host <-> device copy rate on this GPU (GB/s) the way the stream
     uses PCIe: `n` concurrent HIP streams, each copying `chunk_bytes` pieces
     (one batch's JPEG scans for H2D, one frame's BGRX for D2H) round-robin,
     for every n in stream_counts, plus one stream of 256 MiB copies (the
-    round-3 measurement).  Returns {"GBps": best, "rows": [...]} -- the best
-    of these is the ceiling the stream's rate is divided by."""
+    round-3 measurement).  With host_bufs (pinned tensors of >= chunk_bytes:
+    the stream's own), the n-stream rows are repeated on them, so that where
+    the pages of a fresh buffer land does not set the ceiling below the rate
+    the stream's buffers allow.  Returns {"GBps": best, "rows": [...]} -- the
+    best of these is the ceiling the stream's rate is divided by."""
     chunk = max(1 << 20, int(chunk_bytes) // 4096 * 4096)
     nmax = max(stream_counts)
     span = max(256 << 20, chunk * nmax)
     host = torch.empty(span, dtype=torch.uint8).pin_memory()
     devb = torch.empty(span, dtype=torch.uint8, device=dev)
     rows = []
-    for n, size in [(1, 256 << 20)] + [(n, chunk) for n in stream_counts]:
+    own = [b.view(-1).view(torch.uint8)[:chunk] for b in host_bufs] if host_bufs else []
+    own = [b for b in own if b.numel() == chunk]
+    runs = [(1, 256 << 20, False)] + [(n, chunk, False) for n in stream_counts] + \
+        [(n, chunk, True) for n in stream_counts if own]
+    for n, size, on_own in runs:
         streams = [torch.cuda.Stream(dev) for _ in range(n)]
         ncopies = max(n, int(total_bytes // size))
         pieces = max(1, span // size)
@@ -784,11 +792,12 @@ def pcie_ceiling(torch, dev, direction, chunk_bytes, stream_counts, total_bytes=
         def issue(k):
             st = streams[k % n]
             off = (k % pieces) * size
+            hb = own[k % len(own)] if on_own else host[off:off + size]
             with torch.cuda.stream(st):
                 if direction == "h2d":
-                    devb[off:off + size].copy_(host[off:off + size], non_blocking=True)
+                    devb[off:off + size].copy_(hb, non_blocking=True)
                 else:
-                    host[off:off + size].copy_(devb[off:off + size], non_blocking=True)
+                    hb.copy_(devb[off:off + size], non_blocking=True)
         for k in range(n):
             issue(k)
         torch.cuda.synchronize()
@@ -797,7 +806,8 @@ def pcie_ceiling(torch, dev, direction, chunk_bytes, stream_counts, total_bytes=
             issue(k)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-        rows.append({"streams": n, "copy_bytes": size, "GBps": round(ncopies * size / dt / 1e9, 2)})
+        rows.append({"streams": n, "copy_bytes": size, "GBps": round(ncopies * size / dt / 1e9, 2),
+                     **({"host": "the stream's buffers"} if on_own else {})})
     del host, devb
     return {"GBps": max(r["GBps"] for r in rows), "rows": rows}
 
