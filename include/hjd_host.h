@@ -172,7 +172,9 @@ int hjd_gdec_set_output_format(hjd_gdec* g, int out_format);
  * (0 when every scan was destuffed on the GPU) and bytes moved host -> device. */
 int hjd_gdec_last_bytes(hjd_gdec* g, int64_t* host_scan_bytes, int64_t* h2d_bytes);
 
-#define HJD_GDEC_SEQUENTIAL 1   /* verification fell back to the sequential path */
+#define HJD_GDEC_SEQUENTIAL 1   /* verification needed the sequential path (round-based sync) or a
+                                   serial chain repair (speculative sync: the decoder then moves its
+                                   next calls to a longer lead-in) */
 #define HJD_GDEC_CORRUPT 2      /* invalid Huffman data on the decoded chain */
 #define HJD_GDEC_COUNT 4        /* fewer blocks than the frame needs */
 

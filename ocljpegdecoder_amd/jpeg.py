@@ -312,6 +312,10 @@ class GpuDecoder:
         return {"host_scan_bytes": hb.value, "h2d_bytes": h2d.value}
 
     def sync(self, raise_on_error: bool = True) -> List[int]:
+        """Wait for the last call; per-frame status words (include/hjd_host.h:
+        bit 0 HJD_GDEC_SEQUENTIAL is informational, a sequential verification
+        or a chain repair; bits 1-2 are errors and raise unless
+        raise_on_error is False)."""
         status = (ctypes.c_int32 * max(self._n, 1))()
         rc = self.lib.hjd_gdec_sync(self.handle, status)
         if raise_on_error:
