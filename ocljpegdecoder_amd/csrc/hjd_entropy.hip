@@ -2295,9 +2295,13 @@ void emulate(const EntBatchDev& b)
 // none at 2048, host emulation).  Bits per block do not tell these apart, so
 // the decoder goes by its own history: a batch whose chain needed a repair
 // moves the next batches one step up the ladder, and kLeadBatches clean
-// batches move them one step down (a camera's frames look alike).
+// batches move them one step down (a camera's frames look alike).  A repair
+// right after a step down doubles the clean run the next step down waits for
+// (up to kLeadBatchesMax), so a stream that needs the long lead-in pays a
+// repaired frame ever more rarely.
 constexpr uint32_t kLeadLadder[] = {512, 1536, 2560};
-constexpr uint32_t kLeadSteps = sizeof(kLeadLadder) / sizeof(kLeadLadder[0]), kLeadBatches = 32;
+constexpr uint32_t kLeadSteps = sizeof(kLeadLadder) / sizeof(kLeadLadder[0]), kLeadBatches = 32,
+                   kLeadBatchesMax = 4096;
 uint32_t spec_lead_bits(uint32_t step)
 {
     const char* e = getenv("HJD_SPEC_LEAD");   // read per batch (~100 ns): tests switch it in-process
@@ -2353,6 +2357,8 @@ struct hjd_gdec {
     bool batch_spec = false;            // the pending batch took the speculative sync
     uint32_t lead_step = 0;             // spec_lead_bits' ladder step for the next batch
     uint32_t lead_left = 0;             // clean batches before it steps down
+    uint32_t lead_hold = kLeadBatches;  // the clean run a step down waits for
+    bool lead_stepped_down = false;     // the batch in flight runs one step lower than the last
     hipStream_t early_stream = nullptr; // this call's stream when its lone image may be pulled early
     bool early = false;                 // early pull enabled for this call
     size_t prepulled = 0;               // data-area bytes of frame 0 already pulled (gdec_early_pull)
@@ -3278,10 +3284,16 @@ int hjd_gdec_sync(hjd_gdec* g, int32_t* status)
     }
     if (g->batch_spec) {   // the lead-in of the next batches (spec_lead_bits)
         if (repaired) {
+            if (g->lead_stepped_down) g->lead_hold = std::min(2 * g->lead_hold, kLeadBatchesMax);
             g->lead_step = std::min(g->lead_step + 1, kLeadSteps - 1);
-            g->lead_left = kLeadBatches;
-        } else if (g->lead_step && --g->lead_left == 0) {
-            g->lead_left = --g->lead_step ? kLeadBatches : 0;
+            g->lead_left = g->lead_hold;
+            g->lead_stepped_down = false;
+        } else {
+            g->lead_stepped_down = false;
+            if (g->lead_step && --g->lead_left == 0) {
+                g->lead_left = --g->lead_step ? g->lead_hold : 0;
+                g->lead_stepped_down = true;
+            }
         }
     }
     g->pending = false;
